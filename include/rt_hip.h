@@ -1,0 +1,144 @@
+/*
+ * rt_hip.h -- C ABI of the MI355X-native render path (librt_hip.so).
+ *
+ * This is the drop-in boundary for the reference's per-pixel render loop.  In the
+ * reference the boundary is the OpenGL compute-dispatch contract: sampler units 0/1
+ * bound to the geometry / LBVH "buffer textures", a set of uniforms, an optional light
+ * SSBO, then glDispatchCompute.  Each entry point below replaces one such dispatch
+ * (file:line citations are relative to /root/reference/Raytracing-Sandbox/Src/):
+ *
+ *   rt_render_iow01  <- In_One_Weekend::Sphere::OnUpdate             01_Adding_Sphere/Sphere.cpp:51-64
+ *                       (uniforms Sphere.cpp:54-61, dispatch (W,H,1) Sphere.cpp:63)
+ *   rt_render_iow03  <- In_One_Weekend::Adding_Materials::OnUpdate   03_Shadows_and_Materials/materials.cpp:118-146
+ *                       (uniforms :121-135, textures :137-140, per-tile dispatch :142-143)
+ *   rt_render_inw    <- In_Next_Week::RT_Base<>::OnUpdateBase        In-Next-Week/base.h:148-173
+ *                       (layout 1 = BVH stage, 01_BoundingVolumeHierarchy/BVH.cpp:26-43;
+ *                        layout 4 = Lights stage + SSBO, 04_Lights_Camera_And_Action/lights.cpp:15-37)
+ *   rt_lbvh_build    <- LBVH::ConstructLBVH_Buff                      In-Next-Week/LBVH/lbvh.h:215-269
+ *                       (called from base.h:135 on every redraw)
+ *
+ * Conventions:
+ *   - POD structs, caller-owned host memory, library-owned device memory.
+ *   - int status: 0 = ok, negative = error (RT_E_*); no exceptions cross the ABI.
+ *   - Output images are row-major, row y = pixel_coords.y (GL bottom row first),
+ *     RGBA float32 with alpha = 1, exactly the reference's rgba32f image memory.
+ *     The depth image (INW only) is one float per pixel (the reference's r32f image).
+ *   - The *_async variants take DEVICE pointers (inputs already resident in HBM) and a
+ *     hipStream_t passed as void*; they never allocate or synchronise (graph-capturable).
+ *   - Threading: calls are reentrant per distinct output buffer.
+ *
+ * Numerics contract shared with the CPU oracle (DESIGN.md "Numerics contract"):
+ * IEEE binary32, GLSL evaluation order, no FMA contraction, GLSL a/b == a*RN(1/b),
+ * correctly rounded sqrt and reciprocal, transcendentals only in host-built double
+ * precision tables.  Under this contract the GPU image is bit-identical to the oracle's.
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* status codes */
+#define RT_OK            0
+#define RT_E_ARG        -1   /* bad argument (null pointer, non-positive size, bad layout) */
+#define RT_E_HIP        -2   /* a HIP runtime call failed */
+#define RT_E_NODEVICE   -3   /* no usable gfx950 device */
+#define RT_E_UNSUPPORTED -4  /* a feature the path does not implement (e.g. TextureIndex > 0) */
+
+/* Camera uniforms.
+ *   IOW-01: u_CameraPosn, u_CameraDirn, u_FocusDist            (01_Adding_Sphere/computeShaderSrc.glsl:5-7)
+ *   IOW-03: u_CameraPosn, u_CameraDirn, u_FOV_y, u_CamAperture, u_CamFocusDist (03...glsl:7-13)
+ *   INW   : u_Camera{Position, Direction, FOV_y, FocusDist[0], Aperture} (01_BoundingVolumeHierarchy/computeShaderSrc.glsl:221-228)
+ * dir is passed exactly as the reference host computes it (IOW: normalized FrontFromPitchYaw,
+ * materials.cpp:321-328; INW: RT_Base::m_Camera.Front(), NOT normalized, base.h:274-281). */
+typedef struct rt_camera {
+    float pos[3];
+    float dir[3];
+    float fov_y_rad;
+    float aperture;
+    float focus_dist;
+} rt_camera;
+
+/* Render parameters.
+ *   width, height : full image size (imageSize(img_output))
+ *   spp           : IOW-03 u_NumOfSamples; INW local_size_x (samples per pixel, any value >= 1)
+ *   max_bounces   : IOW-03 u_NumOfBounce; INW u_NumOfBounces
+ *   tile_*        : rectangle of pixels to render (IOW-03 u_TileIndex*u_TileSize and the
+ *                   per-tile dispatch size, materials.cpp:126-143).  tile_w/tile_h <= 0 => full image.
+ *   show_normal   : IOW-01/IOW-03 u_ShowNormal
+ *   device        : HIP device ordinal for the blocking entry points (-1 = current) */
+typedef struct rt_params {
+    int width, height, spp, max_bounces;
+    int tile_x0, tile_y0, tile_w, tile_h;
+    int show_normal;
+    int device;
+} rt_params;
+
+/* Counters, identical definitions in the kernels and in the oracle (DESIGN.md "Counters"). */
+typedef struct rt_stats {
+    uint64_t segments;        /* rays cast (primary + secondary), i.e. closest-hit queries   */
+    uint64_t node_visits;     /* LBVH nodes fetched+tested (closest-hit, shadow, RI walks)   */
+    uint64_t prim_tests;      /* primitive tests (IOW linear loop, INW leaves, RI inside)    */
+    uint64_t shadow_queries;  /* INW-04 shadow rays                                          */
+    uint64_t stack_drops;     /* pushes silently dropped by a full stack                     */
+    uint64_t nan_drops;       /* secondary directions that came out NaN                      */
+    double   ms;              /* device time of the render launch(es), milliseconds          */
+} rt_stats;
+
+/* ---- version / device ------------------------------------------------------------ */
+int  rt_abi_version(void);
+/* Returns RT_OK if a gfx950 device is visible; writes its name (<=255 chars). */
+int  rt_device_info(int device, char *name_out, int name_cap, int *cu_count);
+
+/* ---- blocking entry points (host buffers in, host buffers out) -------------------- */
+int rt_render_iow01(const rt_camera *cam, const float sphere[4] /* centre xyz, radius */,
+                    const rt_params *p, float *rgba /* W*H*4 */, rt_stats *st);
+
+int rt_render_iow03(const float *types /* N, float(Geom_type) */,
+                    const float *records /* N*24, materials.h:11-19 */, uint32_t n,
+                    const rt_camera *cam, const rt_params *p, float *rgba, rt_stats *st);
+
+int rt_render_inw(const float *geom /* N*28, layout 1 (BVH.h:12-19) or 4 (lights.h:15-21) */,
+                  uint32_t n, int layout,
+                  const float *nodes /* (2N-1)*8, BFS, lbvh.h:48-54 */,
+                  const float *lights /* L*7: BBmin[3] BBmax[3] uint idx (bit-cast), lights.h:187-192 */,
+                  uint32_t n_lights,
+                  const rt_camera *cam, const rt_params *p,
+                  float *rgba /* W*H*4 */, float *depth /* W*H, may be NULL */, rt_stats *st);
+
+/* LBVH builder: aabbs = N*(min xyz, max xyz) in geometry order -> (2N-1)*8 floats. */
+int rt_lbvh_build(const float *aabbs, uint32_t n, float *nodes_out);
+
+/* ---- asynchronous device entry points (bench / multi-GPU path) ---------------------
+ * A prepared scene owns its device buffers (scene records, LBVH nodes, sample tables).
+ * rt_scene_dev_* return an opaque handle; render calls enqueue on `stream`.
+ * Counters are accumulated atomically into d_counters (6 x uint64, device memory). */
+typedef struct rt_dev_scene rt_dev_scene;
+
+rt_dev_scene *rt_dev_scene_iow03(const float *types, const float *records, uint32_t n,
+                                 int spp, int device);
+rt_dev_scene *rt_dev_scene_inw(const float *geom, uint32_t n, int layout, const float *nodes,
+                               const float *lights, uint32_t n_lights, int spp, int device);
+void rt_dev_scene_free(rt_dev_scene *s);
+
+/* Render one tile list.  tiles: device int array of n_tiles (tx, ty) pairs of tile_size^2
+ * tiles; out_packed: device float array n_tiles*tile_size*tile_size*4 (tile-major, row-major
+ * inside a tile; pixels outside the image are written as 0).  out_depth may be NULL. */
+int rt_render_tiles_async(rt_dev_scene *s, const rt_camera *cam, const rt_params *p,
+                          const int *d_tiles, int n_tiles, int tile_size,
+                          float *d_out_packed, float *d_out_depth_packed,
+                          uint64_t *d_counters, void *stream);
+
+/* Render the rectangle in p->tile_* into a full W*H image resident on the device. */
+int rt_render_image_async(rt_dev_scene *s, const rt_camera *cam, const rt_params *p,
+                          float *d_rgba, float *d_depth, uint64_t *d_counters, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_HIP_H */

@@ -1,0 +1,452 @@
+// rt_capi.hip -- implementation of include/rt_hip.h and include/rt_scene.h.
+//
+// Owns device memory, converts the reference's record layouts into the kernels' device
+// layouts (hot/cold split, per-object reciprocals hoisted under the numerics contract),
+// builds the sample tables and launches.  No exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+#include "../../include/rt_scene.h"
+#include "rt_host.hpp"
+#include "rt_kernels.hpp"
+
+namespace {
+
+#define HIP_OK(expr)                                             \
+    do {                                                         \
+        hipError_t e_ = (expr);                                  \
+        if (e_ != hipSuccess) {                                  \
+            std::fprintf(stderr, "[rt_hip] %s failed: %s\n", #expr, hipGetErrorString(e_)); \
+            return RT_E_HIP;                                     \
+        }                                                        \
+    } while (0)
+
+struct DevBuf {  // RAII device allocation
+    void *p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t alloc(size_t b) { bytes = b; return hipMalloc(&p, b ? b : 16); }
+    hipError_t upload(const void *src, size_t b) {
+        hipError_t e = alloc(b);
+        if (e != hipSuccess || !b) return e;
+        return hipMemcpy(p, src, b, hipMemcpyHostToDevice);
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+int check_device(int device) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RT_E_NODEVICE;
+    if (device >= 0) {
+        if (device >= count) return RT_E_NODEVICE;
+        if (hipSetDevice(device) != hipSuccess) return RT_E_HIP;
+    }
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return RT_E_HIP;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cur) != hipSuccess) return RT_E_HIP;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RT_E_NODEVICE;
+    return RT_OK;
+}
+
+bool params_ok(const rt_params *p) {
+    return p && p->width > 0 && p->height > 0 && p->spp >= 1 && p->max_bounces >= 0;
+}
+
+// Uniforms of one dispatch.  screen_dist = 1/(2 tan(FOV/2)) is evaluated on the host in
+// double and rounded (contract: transcendentals only on the host).
+rtk::Frame make_frame(const rt_camera *cam, const rt_params *p) {
+    rtk::Frame f;
+    std::memset(&f, 0, sizeof(f));
+    f.W = p->width; f.H = p->height; f.spp = p->spp; f.max_bounces = p->max_bounces;
+    f.show_normal = p->show_normal;
+    if (p->tile_w > 0 && p->tile_h > 0) { f.x0 = p->tile_x0; f.y0 = p->tile_y0; f.tw = p->tile_w; f.th = p->tile_h; }
+    else { f.x0 = 0; f.y0 = 0; f.tw = p->width; f.th = p->height; }
+    if (cam) {
+        std::memcpy(f.pos, cam->pos, sizeof(f.pos));
+        std::memcpy(f.dir, cam->dir, sizeof(f.dir));
+        f.aperture = cam->aperture;
+        f.focus = cam->focus_dist;
+        f.screen_dist = 1.0f / (2.0f * (float)std::tan((double)(cam->fov_y_rad * 0.5f)));
+    }
+    f.inv_spp = 1.0f / (float)p->spp;
+    return f;
+}
+
+}  // namespace
+
+// A prepared scene: device-resident records, LBVH nodes, lights and sample tables.
+struct rt_dev_scene {
+    int kind = 0;  // 3 = IOW-03, 11/14 = INW layout 1/4
+    int device = 0;
+    int spp = 0;
+    uint32_t n = 0, n_lights = 0;
+    int layout = 0;
+    DevBuf hot, cold, nodes, lights, sunflower, fib, ring;
+};
+
+namespace {
+
+int build_tables(rt_dev_scene *s, int spp) {
+    std::vector<float> sf(size_t(spp) * 2), fib3(size_t(spp) * 3), fib4(size_t(spp) * 4, 0.0f);
+    std::vector<int> ring(size_t(spp) * 2);
+    rtamd::sample_tables(spp, sf.data(), fib3.data(), ring.data());
+    for (int i = 0; i < spp; i++)
+        for (int k = 0; k < 3; k++) fib4[size_t(i) * 4 + k] = fib3[size_t(i) * 3 + k];
+    HIP_OK(s->sunflower.upload(sf.data(), sf.size() * sizeof(float)));
+    HIP_OK(s->fib.upload(fib4.data(), fib4.size() * sizeof(float)));
+    HIP_OK(s->ring.upload(ring.data(), ring.size() * sizeof(int)));
+    s->spp = spp;
+    return RT_OK;
+}
+
+int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n, int spp) {
+    std::vector<float> hot(size_t(n) * rtk::kIowHot, 0.0f), cold(size_t(n) * rtk::kIowCold, 0.0f);
+    for (uint32_t j = 0; j < n; j++) {
+        const float *r = rec + size_t(j) * 24;
+        float *h = hot.data() + size_t(j) * rtk::kIowHot;
+        float *c = cold.data() + size_t(j) * rtk::kIowCold;
+        h[0] = r[0]; h[1] = r[1]; h[2] = r[2];
+        h[3] = types[j];
+        for (int k = 0; k < 9; k++) h[4 + k] = r[3 + k];
+        for (int k = 0; k < 3; k++) { h[13 + k] = r[12 + k]; h[16 + k] = 1.0f / r[12 + k]; }
+        for (int k = 0; k < 3; k++) { c[k] = r[15 + k]; c[3 + k] = r[18 + k]; }
+        c[6] = r[21]; c[7] = r[22];
+    }
+    s->kind = 3; s->n = n;
+    HIP_OK(s->hot.upload(hot.data(), hot.size() * sizeof(float)));
+    HIP_OK(s->cold.upload(cold.data(), cold.size() * sizeof(float)));
+    return build_tables(s, spp);
+}
+
+int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const float *nodes,
+             const float *lights, uint32_t n_lights, int spp) {
+    std::vector<float> hot(size_t(n) * rtk::kInwHot, 0.0f), cold(size_t(n) * rtk::kInwCold, 0.0f);
+    for (uint32_t j = 0; j < n; j++) {
+        const float *f = geom + size_t(j) * 28;
+        float *h = hot.data() + size_t(j) * rtk::kInwHot;
+        float *c = cold.data() + size_t(j) * rtk::kInwCold;
+        for (int k = 0; k < 20; k++) h[k] = f[k];  // pos R scale delta type extra
+        for (int k = 0; k < 3; k++) {
+            h[20 + k] = 1.0f / f[12 + k];                  // a / scale  -> a * RN(1/scale)
+            h[23 + k] = 1.0f / (f[12 + k] * f[12 + k]);    // a / (s*s)  -> a * RN(1/RN(s*s))
+        }
+        h[26] = layout == 4 ? f[19] : f[20];  // RI accumulated by the surrounding-RI walk
+        if (layout == 1) {  // BVH.h:6-19
+            c[0] = f[21]; c[1] = f[22]; c[2] = f[23]; c[3] = f[24];
+            c[4] = f[25]; c[5] = f[26]; c[6] = f[27]; c[7] = f[20];
+        } else {            // lights.h:6-21
+            c[0] = f[20]; c[1] = f[21]; c[2] = f[22]; c[3] = f[23];
+            c[4] = f[24]; c[5] = f[25]; c[6] = f[26]; c[7] = f[19];
+        }
+    }
+    s->kind = layout == 4 ? 14 : 11;
+    s->n = n; s->layout = layout; s->n_lights = layout == 4 ? n_lights : 0;
+    HIP_OK(s->hot.upload(hot.data(), hot.size() * sizeof(float)));
+    HIP_OK(s->cold.upload(cold.data(), cold.size() * sizeof(float)));
+    HIP_OK(s->nodes.upload(nodes, size_t(2 * n - 1) * 8 * sizeof(float)));
+    if (s->n_lights) HIP_OK(s->lights.upload(lights, size_t(s->n_lights) * 7 * sizeof(float)));
+    else HIP_OK(s->lights.alloc(16));
+    return build_tables(s, spp);
+}
+
+int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
+    hipError_t e;
+    if (s->kind == 3) {
+        rtk::IowScene sc{s->hot.as<float>(), s->cold.as<float>(), s->n, s->sunflower.as<float>(),
+                         s->fib.as<float>(), s->ring.as<int>()};
+        e = rtk::launch_iow03(f, sc, st);
+    } else {
+        rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
+                         s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>()};
+        e = rtk::launch_inw(f, sc, st);
+    }
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
+        return RT_E_HIP;
+    }
+    return RT_OK;
+}
+
+// blocking render of one scene into host buffers
+int render_blocking(rt_dev_scene *s, const rt_camera *cam, const rt_params *p, float *rgba, float *depth,
+                    rt_stats *st) {
+    rtk::Frame f = make_frame(cam, p);
+    const size_t npx = size_t(p->width) * p->height;
+    DevBuf d_rgba, d_depth, d_ctr;
+    HIP_OK(d_rgba.alloc(npx * 16));
+    HIP_OK(hipMemcpy(d_rgba.p, rgba, npx * 16, hipMemcpyHostToDevice));  // untouched pixels keep their value
+    if (depth) {
+        HIP_OK(d_depth.alloc(npx * 4));
+        HIP_OK(hipMemcpy(d_depth.p, depth, npx * 4, hipMemcpyHostToDevice));
+    }
+    HIP_OK(d_ctr.alloc(6 * sizeof(unsigned long long)));
+    HIP_OK(hipMemset(d_ctr.p, 0, 6 * sizeof(unsigned long long)));
+    f.out_rgba = d_rgba.as<float>();
+    f.out_depth = depth ? d_depth.as<float>() : nullptr;
+    f.counters = d_ctr.as<unsigned long long>();
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventRecord(e0, nullptr));
+    int rc = launch_scene(s, f, nullptr);
+    HIP_OK(hipEventRecord(e1, nullptr));
+    HIP_OK(hipEventSynchronize(e1));
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc != RT_OK) return rc;
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(rgba, d_rgba.p, npx * 16, hipMemcpyDeviceToHost));
+    if (depth) HIP_OK(hipMemcpy(depth, d_depth.p, npx * 4, hipMemcpyDeviceToHost));
+    if (st) {
+        unsigned long long c[6];
+        HIP_OK(hipMemcpy(c, d_ctr.p, sizeof(c), hipMemcpyDeviceToHost));
+        st->segments = c[0]; st->node_visits = c[1]; st->prim_tests = c[2];
+        st->shadow_queries = c[3]; st->stack_drops = c[4]; st->nan_drops = c[5];
+        st->ms = ms;
+    }
+    return RT_OK;
+}
+
+bool inw_textured(const float *geom, uint32_t n, int layout) {
+    if (layout != 4) return false;
+    for (uint32_t g = 0; g < n; g++)
+        if (uint32_t(geom[size_t(g) * 28 + 27] + 0.1f) > 0) return true;
+    return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_device_info(int device, char *name_out, int name_cap, int *cu_count) {
+    int rc = check_device(device);
+    if (rc != RT_OK) return rc;
+    int cur = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&cur) != hipSuccess || hipGetDeviceProperties(&prop, cur) != hipSuccess) return RT_E_HIP;
+    if (name_out && name_cap > 0) std::snprintf(name_out, size_t(name_cap), "%s (%s)", prop.name, prop.gcnArchName);
+    if (cu_count) *cu_count = prop.multiProcessorCount;
+    return RT_OK;
+}
+
+int rt_render_iow01(const rt_camera *cam, const float sphere[4], const rt_params *p, float *rgba, rt_stats *st) {
+    if (!cam || !sphere || !params_ok(p) || !rgba) return RT_E_ARG;
+    int rc = check_device(p->device);
+    if (rc != RT_OK) return rc;
+    rtk::Frame f = make_frame(cam, p);
+    std::memcpy(f.sphere, sphere, sizeof(f.sphere));
+    const size_t npx = size_t(p->width) * p->height;
+    DevBuf d_rgba;
+    HIP_OK(d_rgba.alloc(npx * 16));
+    HIP_OK(hipMemcpy(d_rgba.p, rgba, npx * 16, hipMemcpyHostToDevice));
+    f.out_rgba = d_rgba.as<float>();
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventRecord(e0, nullptr));
+    hipError_t e = rtk::launch_iow01(f, nullptr);
+    HIP_OK(hipEventRecord(e1, nullptr));
+    HIP_OK(hipEventSynchronize(e1));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    HIP_OK(e);
+    HIP_OK(hipMemcpy(rgba, d_rgba.p, npx * 16, hipMemcpyDeviceToHost));
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        st->segments = uint64_t(f.tw) * uint64_t(f.th);
+        st->ms = ms;
+    }
+    return RT_OK;
+}
+
+int rt_render_iow03(const float *types, const float *records, uint32_t n, const rt_camera *cam,
+                    const rt_params *p, float *rgba, rt_stats *st) {
+    if (!types || !records || !cam || !params_ok(p) || !rgba) return RT_E_ARG;
+    int rc = check_device(p->device);
+    if (rc != RT_OK) return rc;
+    std::unique_ptr<rt_dev_scene> s(new (std::nothrow) rt_dev_scene());
+    if (!s) return RT_E_ARG;
+    rc = make_iow03(s.get(), types, records, n, p->spp);
+    if (rc != RT_OK) return rc;
+    return render_blocking(s.get(), cam, p, rgba, nullptr, st);
+}
+
+int rt_render_inw(const float *geom, uint32_t n, int layout, const float *nodes, const float *lights,
+                  uint32_t n_lights, const rt_camera *cam, const rt_params *p, float *rgba, float *depth,
+                  rt_stats *st) {
+    if (!geom || !nodes || n == 0 || !cam || !params_ok(p) || !rgba) return RT_E_ARG;
+    if (layout != 1 && layout != 4) return RT_E_ARG;
+    if (layout == 4 && n_lights > 0 && !lights) return RT_E_ARG;
+    if (inw_textured(geom, n, layout)) return RT_E_UNSUPPORTED;
+    int rc = check_device(p->device);
+    if (rc != RT_OK) return rc;
+    std::unique_ptr<rt_dev_scene> s(new (std::nothrow) rt_dev_scene());
+    if (!s) return RT_E_ARG;
+    rc = make_inw(s.get(), geom, n, layout, nodes, lights, n_lights, p->spp);
+    if (rc != RT_OK) return rc;
+    return render_blocking(s.get(), cam, p, rgba, depth, st);
+}
+
+int rt_lbvh_build(const float *aabbs, uint32_t n, float *nodes_out) {
+    if (!aabbs || !nodes_out || n == 0) return RT_E_ARG;
+    try {
+        std::vector<float> v = rtamd::lbvh_build(aabbs, n);
+        std::memcpy(nodes_out, v.data(), v.size() * sizeof(float));
+    } catch (...) {
+        return RT_E_ARG;
+    }
+    return RT_OK;
+}
+
+rt_dev_scene *rt_dev_scene_iow03(const float *types, const float *records, uint32_t n, int spp, int device) {
+    if (!types || !records || spp < 1) return nullptr;
+    if (check_device(device) != RT_OK) return nullptr;
+    rt_dev_scene *s = new (std::nothrow) rt_dev_scene();
+    if (!s) return nullptr;
+    (void)hipGetDevice(&s->device);
+    if (make_iow03(s, types, records, n, spp) != RT_OK) { delete s; return nullptr; }
+    return s;
+}
+
+rt_dev_scene *rt_dev_scene_inw(const float *geom, uint32_t n, int layout, const float *nodes, const float *lights,
+                               uint32_t n_lights, int spp, int device) {
+    if (!geom || !nodes || n == 0 || spp < 1 || (layout != 1 && layout != 4)) return nullptr;
+    if (layout == 4 && n_lights > 0 && !lights) return nullptr;
+    if (inw_textured(geom, n, layout)) return nullptr;
+    if (check_device(device) != RT_OK) return nullptr;
+    rt_dev_scene *s = new (std::nothrow) rt_dev_scene();
+    if (!s) return nullptr;
+    (void)hipGetDevice(&s->device);
+    if (make_inw(s, geom, n, layout, nodes, lights, n_lights, spp) != RT_OK) { delete s; return nullptr; }
+    return s;
+}
+
+void rt_dev_scene_free(rt_dev_scene *s) { delete s; }
+
+int rt_render_tiles_async(rt_dev_scene *s, const rt_camera *cam, const rt_params *p, const int *d_tiles,
+                          int n_tiles, int tile_size, float *d_out_packed, float *d_out_depth_packed,
+                          uint64_t *d_counters, void *stream) {
+    if (!s || !cam || !params_ok(p) || !d_tiles || n_tiles <= 0 || !d_out_packed) return RT_E_ARG;
+    if (tile_size <= 0 || tile_size % 16 != 0) return RT_E_ARG;
+    if (p->spp != s->spp) return RT_E_ARG;  // tables are built for the scene's spp
+    rtk::Frame f = make_frame(cam, p);
+    f.tiles = d_tiles; f.n_tiles = n_tiles; f.tile_size = tile_size;
+    f.out_rgba = d_out_packed; f.out_depth = d_out_depth_packed;
+    f.counters = reinterpret_cast<unsigned long long *>(d_counters);
+    return launch_scene(s, f, static_cast<hipStream_t>(stream));
+}
+
+int rt_render_image_async(rt_dev_scene *s, const rt_camera *cam, const rt_params *p, float *d_rgba, float *d_depth,
+                          uint64_t *d_counters, void *stream) {
+    if (!s || !cam || !params_ok(p) || !d_rgba) return RT_E_ARG;
+    if (p->spp != s->spp) return RT_E_ARG;
+    rtk::Frame f = make_frame(cam, p);
+    f.out_rgba = d_rgba; f.out_depth = d_depth;
+    f.counters = reinterpret_cast<unsigned long long *>(d_counters);
+    return launch_scene(s, f, static_cast<hipStream_t>(stream));
+}
+
+// ------------------------------------------------------------------------ rt_scene.h
+int rt_scene_preset(int preset, uint32_t seed, int n_hint, rt_geom_desc *out, int cap, rt_cam_desc *cam,
+                    rt_params *params) {
+    try {
+        std::vector<rt_geom_desc> v;
+        rt_cam_desc c;
+        rt_params p;
+        int n = rtamd::scene_preset(preset, seed, n_hint, v, c, p);
+        if (n < 0) return n;
+        if (out) {
+            if (cap < n) return RT_E_ARG;
+            std::memcpy(out, v.data(), v.size() * sizeof(rt_geom_desc));
+        }
+        if (cam) *cam = c;
+        if (params) *params = p;
+        return n;
+    } catch (...) {
+        return RT_E_ARG;
+    }
+}
+
+int rt_camera_from_desc(const rt_cam_desc *d, int stage, rt_camera *out) {
+    if (!d || !out) return RT_E_ARG;
+    const bool iow = stage == RT_STAGE_IOW01 || stage == RT_STAGE_IOW03;
+    if (!iow && stage != RT_STAGE_INW01 && stage != RT_STAGE_INW04) return RT_E_ARG;
+    rtamd::Vec3 fr = rtamd::front_from_pitch_yaw(d->pitch_deg, d->yaw_deg, iow);
+    std::memcpy(out->pos, d->position, sizeof(out->pos));
+    out->dir[0] = fr.x; out->dir[1] = fr.y; out->dir[2] = fr.z;
+    out->fov_y_rad = rtamd::radians(d->fov_y_deg);
+    out->aperture = d->aperture;
+    out->focus_dist = d->focus_dist;
+    return RT_OK;
+}
+
+int rt_pack_iow03(const rt_geom_desc *g, uint32_t n, float *types, float *records) {
+    if (!g || !types || !records) return RT_E_ARG;
+    for (uint32_t k = 0; k < n; k++) {
+        rtamd::IowGeometry geo = rtamd::to_iow(g[k]);
+        geo.fill_buffer(records + size_t(k) * 24);
+        types[k] = float(geo.type);
+    }
+    return RT_OK;
+}
+
+int rt_pack_inw(const rt_geom_desc *g, uint32_t n, int layout, float *geom, float *aabbs, float *lights,
+                uint32_t *n_lights) {
+    if (!g || (layout != 1 && layout != 4)) return RT_E_ARG;
+    uint32_t nl = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        std::pair<rtamd::Vec3, rtamd::Vec3> bb;
+        if (layout == 1) {
+            rtamd::GeometryData d = rtamd::to_inw01(g[k]);
+            if (geom) d.fill_buffer(geom + size_t(k) * 28);
+            bb = d.bb_min_max();
+        } else {
+            rtamd::GeometryData04 d = rtamd::to_inw04(g[k]);
+            if (geom) d.fill_buffer(geom + size_t(k) * 28);
+            bb = d.bb_min_max();
+            if (d.emissive) {  // Lights::FillBuffer, lights.cpp:261-264
+                if (lights) {
+                    float *L = lights + size_t(nl) * 7;
+                    L[0] = bb.first.x; L[1] = bb.first.y; L[2] = bb.first.z;
+                    L[3] = bb.second.x; L[4] = bb.second.y; L[5] = bb.second.z;
+                    uint32_t idx = k;
+                    std::memcpy(L + 6, &idx, 4);
+                }
+                nl++;
+            }
+        }
+        if (aabbs) {
+            float *b = aabbs + size_t(k) * 6;
+            b[0] = bb.first.x; b[1] = bb.first.y; b[2] = bb.first.z;
+            b[3] = bb.second.x; b[4] = bb.second.y; b[5] = bb.second.z;
+        }
+    }
+    if (n_lights) *n_lights = nl;
+    return RT_OK;
+}
+
+int rt_sample_tables(int spp, float *sunflower, float *fib, int *ring) {
+    if (spp < 1) return RT_E_ARG;
+    rtamd::sample_tables(spp, sunflower, fib, ring);
+    return RT_OK;
+}
+
+}  // extern "C"

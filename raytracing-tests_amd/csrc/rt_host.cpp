@@ -1,0 +1,529 @@
+// rt_host.cpp -- scene description, packers, LBVH builder, sample tables, presets.
+// See rt_host.hpp for the reference map.  Compiled with -ffp-contract=off: every float
+// expression here must round exactly as the reference's host code (glm) does.
+#include "rt_host.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <random>
+
+namespace rtamd {
+
+// ----------------------------------------------------------------------------- glm slice
+Mat3 operator*(const Mat3 &a, const Mat3 &b) {
+    Mat3 r;
+    for (int j = 0; j < 3; j++)  // glm: Result[j] = A[0]*B[j][0] + A[1]*B[j][1] + A[2]*B[j][2]
+        r.col[j] = a.col[0] * b.col[j].x + a.col[1] * b.col[j].y + a.col[2] * b.col[j].z;
+    return r;
+}
+Vec3 operator*(const Mat3 &m, Vec3 v) {
+    return {m.col[0].x * v.x + m.col[1].x * v.y + m.col[2].x * v.z,
+            m.col[0].y * v.x + m.col[1].y * v.y + m.col[2].y * v.z,
+            m.col[0].z * v.x + m.col[1].z * v.y + m.col[2].z * v.z};
+}
+Mat3 inverse(const Mat3 &m) {
+    auto M = [&](int c, int r) { return m.at(c, r); };
+    float det = +M(0, 0) * (M(1, 1) * M(2, 2) - M(2, 1) * M(1, 2)) -
+                M(1, 0) * (M(0, 1) * M(2, 2) - M(2, 1) * M(0, 2)) +
+                M(2, 0) * (M(0, 1) * M(1, 2) - M(1, 1) * M(0, 2));
+    float o = 1.0f / det;
+    Mat3 r;
+    r.col[0].x = +(M(1, 1) * M(2, 2) - M(2, 1) * M(1, 2)) * o;
+    r.col[1].x = -(M(1, 0) * M(2, 2) - M(2, 0) * M(1, 2)) * o;
+    r.col[2].x = +(M(1, 0) * M(2, 1) - M(2, 0) * M(1, 1)) * o;
+    r.col[0].y = -(M(0, 1) * M(2, 2) - M(2, 1) * M(0, 2)) * o;
+    r.col[1].y = +(M(0, 0) * M(2, 2) - M(2, 0) * M(0, 2)) * o;
+    r.col[2].y = -(M(0, 0) * M(2, 1) - M(2, 0) * M(0, 1)) * o;
+    r.col[0].z = +(M(0, 1) * M(1, 2) - M(1, 1) * M(0, 2)) * o;
+    r.col[1].z = -(M(0, 0) * M(1, 2) - M(1, 0) * M(0, 2)) * o;
+    r.col[2].z = +(M(0, 0) * M(1, 1) - M(1, 0) * M(0, 1)) * o;
+    return r;
+}
+float radians(float deg) { return deg * static_cast<float>(0.01745329251994329576923690768489); }
+Mat3 make_rotation_x(float rad) {
+    float c = std::cos(rad), s = std::sin(rad);
+    return Mat3::from_cols(1.0f, 0.0f, 0.0f, 0.0f, c, -s, 0.0f, s, c);
+}
+Mat3 make_rotation_y(float rad) {
+    float c = std::cos(rad), s = std::sin(rad);
+    return Mat3::from_cols(c, 0.0f, s, 0.0f, 1.0f, 0.0f, -s, 0.0f, c);
+}
+Mat3 make_rotation_z(float rad) {
+    float c = std::cos(rad), s = std::sin(rad);
+    return Mat3::from_cols(c, -s, 0.0f, s, c, 0.0f, 0.0f, 0.0f, 1.0f);
+}
+Mat3 rotation_zxy(const Vec3 &deg) {
+    return make_rotation_z(radians(deg.z)) * make_rotation_x(radians(deg.x)) * make_rotation_y(radians(deg.y));
+}
+
+static inline float rmin(float x, float y) { return x > y ? y : x; }  // MIN, utility.h:10
+static inline float rmax(float x, float y) { return x > y ? x : y; }  // MAX, utility.h:11
+
+// ------------------------------------------------------------------------------- IOW-03
+void IowGeometry::reset_inv_rotation() { inv_rotation = inverse(rotation_zxy(rotation)); }
+void IowGeometry::fill_buffer(float r[24]) const {
+    for (int i = 0; i < 3; i++) r[i] = position[i];
+    for (int i = 0; i < 9; i++) r[3 + i] = inv_rotation.at(i / 3, i % 3);
+    for (int i = 0; i < 3; i++) r[12 + i] = scale[i];
+    for (int i = 0; i < 3; i++) r[15 + i] = color[i];
+    for (int i = 0; i < 3; i++) r[18 + i] = material[i];
+    r[21] = scatteritivity[0];
+    r[22] = scatteritivity[1];
+    r[23] = 0.0f;
+}
+
+// ---------------------------------------------------------------------------------- INW
+std::pair<Vec3, Vec3> TransformData::bb_min_max() const {
+    Mat3 m = rotation_zxy(rotation) * Mat3::from_cols(scale.x, 0, 0, 0, scale.y, 0, 0, 0, scale.z);
+    float x = std::sqrt(m.at(0, 0) * m.at(0, 0) + m.at(1, 0) * m.at(1, 0) + m.at(2, 0) * m.at(2, 0));
+    float y = std::sqrt(m.at(0, 1) * m.at(0, 1) + m.at(1, 1) * m.at(1, 1) + m.at(2, 1) * m.at(2, 1));
+    float z = std::sqrt(m.at(0, 2) * m.at(0, 2) + m.at(1, 2) * m.at(1, 2) + m.at(2, 2) * m.at(2, 2));
+    Vec3 mn(rmin(position.x, last_position.x), rmin(position.y, last_position.y), rmin(position.z, last_position.z));
+    Vec3 mx(rmax(position.x, last_position.x), rmax(position.y, last_position.y), rmax(position.z, last_position.z));
+    return {Vec3(-x, -y, -z) + mn, Vec3(x, y, z) + mx};
+}
+void TransformData::fill_transform(float b[18]) const {
+    for (int i = 0; i < 3; i++) { b[i] = position[i]; b[15 + i] = position[i] - last_position[i]; }
+    Mat3 m = rotation_zxy(rotation);
+    for (int i = 0; i < 9; i++) b[3 + i] = m.at(i / 3, i % 3);
+    for (int i = 0; i < 3; i++) b[12 + i] = scale[i];
+}
+void GeometryData::fill_buffer(float b[28]) const {
+    fill_transform(b);
+    b[18] = float(type);
+    b[19] = 0.0f;  // _padding
+    b[20] = refractive_index; b[21] = refractivity; b[22] = reflectivity;
+    b[23] = scat[0]; b[24] = scat[1];
+    b[25] = color.x; b[26] = color.y; b[27] = color.z;
+}
+std::pair<Vec3, Vec3> GeometryData04::bb_min_max() const {
+    if (type == RT_INW_ELLIPSOID) return TransformData::bb_min_max();
+    if (type == RT_INW_CUBOID) {
+        Mat3 m = rotation_zxy(rotation);
+        Vec3 bmin(0, 0, 0), bmax(0, 0, 0);
+        for (int i = 0; i < 8; i++) {
+            Vec3 co;
+            int bit = 1;
+            for (int a = 0; a < 3; a++) { co[a] = (i & bit) ? 0.5f * scale[a] : -0.5f * scale[a]; bit <<= 1; }
+            co = m * co;
+            for (int a = 0; a < 3; a++) { bmin[a] = rmin(co[a], bmin[a]); bmax[a] = rmax(co[a], bmax[a]); }
+        }
+        Vec3 mn(rmin(position.x, last_position.x), rmin(position.y, last_position.y), rmin(position.z, last_position.z));
+        Vec3 mx(rmax(position.x, last_position.x), rmax(position.y, last_position.y), rmax(position.z, last_position.z));
+        return {bmin + mn, bmax + mx};
+    }
+    return {Vec3(0, 0, 0), Vec3(0, 0, 0)};
+}
+void GeometryData04::fill_buffer(float b[28]) const {
+    fill_transform(b);
+    b[18] = float(type);
+    b[27] = float(texture_index);
+    if (!emissive) {
+        b[24] = color.x; b[25] = color.y; b[26] = color.z;
+        b[19] = refractive_index; b[21] = reflectivity; b[20] = refractivity;
+    } else {  // lights.h:134-139: emissive objects are white, RI 1, no reflect/refract
+        b[24] = 1.0f; b[25] = 1.0f; b[26] = 1.0f;
+        b[19] = 1.0f; b[21] = 0.0f; b[20] = 0.0f;
+    }
+    b[22] = scat[0]; b[23] = scat[1];
+}
+
+static Vec3 v3(const float *f) { return Vec3(f[0], f[1], f[2]); }
+IowGeometry to_iow(const rt_geom_desc &d) {
+    IowGeometry g;
+    g.type = d.type;
+    g.position = v3(d.position); g.rotation = v3(d.rotation_deg); g.scale = v3(d.scale);
+    g.color = v3(d.color);
+    g.material = Vec3(d.refractivity, d.reflectivity, d.refractive_index);
+    g.scatteritivity = Vec3(d.scat_refract, d.scat_reflect, 0.0f);
+    // the default inverse is glm::mat3(1); ImGui edits call ResetInvRotationMatrix
+    if (d.rotation_deg[0] != 0 || d.rotation_deg[1] != 0 || d.rotation_deg[2] != 0) g.reset_inv_rotation();
+    return g;
+}
+template <class G> static void fill_common(G &g, const rt_geom_desc &d) {
+    g.type = d.type;
+    g.position = v3(d.position); g.last_position = v3(d.last_position);
+    g.rotation = v3(d.rotation_deg); g.scale = v3(d.scale); g.color = v3(d.color);
+    g.refractive_index = d.refractive_index; g.refractivity = d.refractivity; g.reflectivity = d.reflectivity;
+    g.scat[0] = d.scat_refract; g.scat[1] = d.scat_reflect;
+}
+GeometryData to_inw01(const rt_geom_desc &d) { GeometryData g; fill_common(g, d); return g; }
+GeometryData04 to_inw04(const rt_geom_desc &d) {
+    GeometryData04 g;
+    fill_common(g, d);
+    g.emissive = d.emissive != 0;
+    g.texture_index = d.texture_index;
+    return g;
+}
+
+// --------------------------------------------------------------------------------- LBVH
+// The reference merges adjacent leaf clusters level by level: every internal node i sits
+// between sorted leaves i and i+1 and is solved in the pass whose level reaches its
+// "highest differing bit" (lbvh.h:162-210); within a pass the FIFO keeps index order and
+// a solved node adopts the current top-most ancestors of leaves i and i+1.  That is the
+// same as merging nodes in (bit, index) order while tracking each contiguous leaf
+// cluster's root, which this does with a disjoint-set in O(N log N).
+static inline uint32_t expand_bits(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+static inline uint32_t morton30(Vec3 p) {
+    const float res = 1024.0f;
+    auto q = [&](float f) { return static_cast<uint32_t>(std::fmin(std::fmax(f * res, 0.0f), res - 1.0f)); };
+    return expand_bits(q(p.x)) * 4 + expand_bits(q(p.y)) * 2 + expand_bits(q(p.z));
+}
+
+std::vector<float> lbvh_build(const float *aabbs, uint32_t n) {
+    std::vector<float> out(size_t(2 * n - 1) * 8, 0.0f);
+    if (n == 1) {
+        std::memcpy(out.data(), aabbs, 6 * sizeof(float));
+        out[6] = -float(0u);
+        out[7] = 0.0f;
+        return out;
+    }
+    Vec3 smin = v3(aabbs), smax = v3(aabbs + 3);
+    for (uint32_t i = 1; i < n; i++)
+        for (int a = 0; a < 3; a++) {
+            smin[a] = rmin(smin[a], aabbs[size_t(i) * 6 + a]);
+            smax[a] = rmax(smax[a], aabbs[size_t(i) * 6 + 3 + a]);
+        }
+    struct Key { uint32_t code, id; float diag2; };
+    std::vector<Key> keys(n);
+    for (uint32_t i = 0; i < n; i++) {
+        const float *b = aabbs + size_t(i) * 6;
+        Vec3 p((b[0] + b[3]) * 0.5f, (b[1] + b[4]) * 0.5f, (b[2] + b[5]) * 0.5f);
+        p = p - smin;
+        p.x /= (smax.x - smin.x);
+        p.y /= (smax.y - smin.y);
+        p.z /= (smax.z - smin.z);
+        Vec3 d(b[3] - b[0], b[4] - b[1], b[5] - b[2]);
+        keys[i] = {morton30(p), i, d.x * d.x + d.y * d.y + d.z * d.z};
+    }
+    std::sort(keys.begin(), keys.end(), [](const Key &a, const Key &b) {
+        if (a.code != b.code) return a.code < b.code;
+        if (a.diag2 < b.diag2) return true;
+        if (b.diag2 < a.diag2) return false;
+        return a.id < b.id;  // contract tie-break (std::sort order of equal keys is unspecified)
+    });
+    std::vector<uint8_t> bit(n - 1);
+    for (uint32_t i = 1; i < n; i++) {
+        uint32_t x = keys[i - 1].code ^ keys[i].code;
+        uint8_t h = 0;
+        while (x) { x >>= 1; h++; }
+        bit[i - 1] = h;
+    }
+    const uint32_t total = 2 * n - 1;
+    struct Node { int32_t left = -1, right = -1; uint32_t obj = 0; Vec3 mn, mx; };
+    std::vector<Node> nd(total);
+    for (uint32_t i = 0; i < n; i++) {
+        nd[i].obj = keys[i].id;
+        nd[i].mn = v3(aabbs + size_t(keys[i].id) * 6);
+        nd[i].mx = v3(aabbs + size_t(keys[i].id) * 6 + 3);
+    }
+    // disjoint set over leaves; croot[rep] = tree node at the top of that cluster
+    std::vector<uint32_t> dsu(n), croot(n);
+    std::iota(dsu.begin(), dsu.end(), 0u);
+    std::iota(croot.begin(), croot.end(), 0u);
+    auto find = [&](uint32_t x) {
+        while (dsu[x] != x) { dsu[x] = dsu[dsu[x]]; x = dsu[x]; }
+        return x;
+    };
+    std::vector<uint32_t> order(n - 1);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return bit[a] < bit[b]; });
+    uint32_t last = 0;
+    for (uint32_t i : order) {
+        uint32_t ra = find(i), rb = find(i + 1);
+        uint32_t L = croot[ra], R = croot[rb], me = n + i;
+        nd[me].left = int32_t(L);
+        nd[me].right = int32_t(R);
+        for (int a = 0; a < 3; a++) {
+            nd[me].mn[a] = rmin(nd[L].mn[a], nd[R].mn[a]);
+            nd[me].mx[a] = rmax(nd[L].mx[a], nd[R].mx[a]);
+        }
+        dsu[rb] = ra;
+        croot[ra] = me;
+        last = me;
+    }
+    // ConstructLBVH_Buff: breadth-first write, children contiguous, rightData = parent
+    std::vector<std::pair<uint32_t, uint32_t>> q;
+    q.reserve(total);
+    q.push_back({last, 0u});
+    for (size_t head = 0, index = 0; head < q.size(); head++, index++) {
+        auto [cn, parent] = q[head];
+        uint32_t L = 0;
+        if (nd[cn].left >= 0) {
+            q.push_back({uint32_t(nd[cn].left), uint32_t(index)});
+            L = uint32_t(index + (q.size() - head - 1));
+            q.push_back({uint32_t(nd[cn].right), uint32_t(index)});
+        }
+        float *o = out.data() + index * 8;
+        o[0] = nd[cn].mn.x; o[1] = nd[cn].mn.y; o[2] = nd[cn].mn.z;
+        o[3] = nd[cn].mx.x; o[4] = nd[cn].mx.y; o[5] = nd[cn].mx.z;
+        o[6] = (L == 0) ? -float(nd[cn].obj) : float(L);
+        o[7] = float(parent);
+    }
+    return out;
+}
+
+// ------------------------------------------------------------------------------- camera
+Vec3 front_from_pitch_yaw(float pitch, float yaw, bool normalize) {
+    Vec3 f;
+    f.x = std::cos(radians(yaw)) * std::cos(radians(pitch));
+    f.y = std::sin(radians(pitch));
+    f.z = std::sin(radians(yaw)) * std::cos(radians(pitch));
+    if (!normalize) return f;  // RT_Base::m_Camera.Front(), base.h:274-281
+    float k = 1.0f / std::sqrt(f.x * f.x + f.y * f.y + f.z * f.z);  // glm::normalize
+    return f * k;
+}
+
+// ------------------------------------------------------------------------ sample tables
+void sample_tables(int spp, float *sunflower, float *fib, int *ring) {
+    const double kPI = 3.1415926538;              // the shaders' #define PI
+    const double kPHI = kPI * (3.0 - std::sqrt(5.0));
+    const double b = std::floor(2.0 * std::sqrt(double(spp)) + 0.5);
+    for (int i = 0; i < spp; i++) {
+        const double th = kPHI * double(i);
+        if (sunflower) {
+            if (i == 0) { sunflower[0] = 0.0f; sunflower[1] = 0.0f; }
+            else {
+                double rho = (double(i) > double(spp) - b) ? 1.0
+                             : std::sqrt((double(i) - 0.5) / (double(spp) - (b + 1.0) / 2.0));
+                sunflower[2 * i] = float(rho * std::cos(th));
+                sunflower[2 * i + 1] = float(rho * std::sin(th));
+            }
+        }
+        if (fib) {
+            double y = 1.0 - (double(i) / double(spp - 1));
+            double radius = std::sqrt(1.0 - y * y);
+            fib[3 * i] = float(std::cos(th) * radius);
+            fib[3 * i + 1] = float(y);
+            fib[3 * i + 2] = float(std::sin(th) * radius);
+        }
+    }
+    if (ring) {  // closed-form walk of the ring schedule (03...glsl:383-397)
+        int grid = 1;
+        while (grid * grid < spp) grid++;
+        int focus = 0, x = 0, y = 0;
+        for (int s = 0; s < spp; s++) {
+            int *o = ring + 2 * s;
+            if (focus >= grid) { o[0] = o[1] = -1; continue; }
+            if (x == 0 && y == 0) { ++focus; x = y = focus; o[0] = o[1] = focus; }
+            else if (x < y) { --y; o[0] = focus; o[1] = y; }
+            else { --x; o[0] = x; o[1] = focus; }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ presets
+namespace {
+struct Rng {  // mt19937 raw words -> 24-bit uniform floats (portable, no std::distribution)
+    std::mt19937 g;
+    explicit Rng(uint32_t s) : g(s) {}
+    float u() { return float(g() >> 8) * (1.0f / 16777216.0f); }
+    float u(float a, float b) { return a + (b - a) * u(); }
+};
+rt_geom_desc blank() {
+    rt_geom_desc d;
+    std::memset(&d, 0, sizeof(d));
+    d.scale[0] = d.scale[1] = d.scale[2] = 1.0f;
+    d.refractive_index = 1.5f;
+    return d;
+}
+void set3(float *f, float a, float b, float c) { f[0] = a; f[1] = b; f[2] = c; }
+rt_cam_desc cam_at(float px, float py, float pz, float pitch, float yaw, float fov, float ap, float focus) {
+    rt_cam_desc c;
+    set3(c.position, px, py, pz);
+    c.pitch_deg = pitch; c.yaw_deg = yaw; c.fov_y_deg = fov; c.aperture = ap; c.focus_dist = focus;
+    return c;
+}
+rt_params params_of(int w, int h, int spp, int bounces) {
+    rt_params p;
+    std::memset(&p, 0, sizeof(p));
+    p.width = w; p.height = h; p.spp = spp; p.max_bounces = bounces; p.device = -1;
+    return p;
+}
+// pitch/yaw (degrees) of the direction from `from` to `to`, inverse of FrontFromPitchYaw
+void look(const float from[3], const float to[3], float &pitch, float &yaw) {
+    double dx = to[0] - from[0], dy = to[1] - from[1], dz = to[2] - from[2];
+    double l = std::sqrt(dx * dx + dy * dy + dz * dz);
+    pitch = float(std::asin(dy / l) * 180.0 / 3.14159265358979323846);
+    yaw = float(std::atan2(dz, dx) * 180.0 / 3.14159265358979323846);
+}
+}  // namespace
+
+int scene_preset(int preset, uint32_t seed, int n_hint, std::vector<rt_geom_desc> &out,
+                 rt_cam_desc &cam, rt_params &params) {
+    out.clear();
+    switch (preset) {
+    case RT_PRESET_IOW03_REF3: {  // materials.cpp:46-65 on top of Geometry defaults (materials.h:89-95)
+        for (int i = 0; i < 3; i++) {
+            rt_geom_desc d = blank();
+            d.type = RT_IOW_CUBOID;
+            set3(d.color, 1, 0, 0);
+            d.refractivity = 0.2f; d.reflectivity = 0.3f; d.refractive_index = 1.5f;
+            out.push_back(d);
+        }
+        out[0].type = RT_IOW_ELLIPSOID; set3(out[0].color, 0, 0, 0); set3(out[0].scale, 2, 2, 2);
+        out[0].position[1] = 1; out[0].refractivity = 1; out[0].reflectivity = 0; out[0].refractive_index = 1.5f;
+        out[1].type = RT_IOW_CUBOID; out[1].position[1] = -1.5f; out[1].scale[0] = 12; out[1].scale[2] = 11;
+        set3(out[1].color, 0.02f, 0.0125f, 0.08f);
+        out[2].type = RT_IOW_ELLIPSOID; set3(out[2].position, -1, -.5f, 1.75f); set3(out[2].scale, .5f, .5f, .5f);
+        out[2].reflectivity = 0.8f; out[2].scat_reflect = 0.8f; set3(out[2].color, 0, 0, 0);
+        cam = cam_at(3, 2, 10, -13, -120, 90.0f, 2.0f, 10.0f);  // materials.h:140-145
+        params = params_of(300, 300, 36, 5);                    // materials.h:137-149
+        return int(out.size());
+    }
+    case RT_PRESET_IOW03_FINAL: {  // config C2: the "final scene" as IOW records
+        Rng r(seed);
+        rt_geom_desc g = blank();
+        g.type = RT_IOW_CUBOID;
+        set3(g.position, 0, -0.5f, 0); set3(g.scale, 100, 1, 100); set3(g.color, 0.1f, 0.1f, 0.1f);
+        g.reflectivity = 0.5f; g.scat_reflect = 1.0f;
+        out.push_back(g);
+        for (int a = -11; a < 11; a++)
+            for (int b = -11; b < 11; b++) {
+                float choose = r.u();
+                float cx = float(a) + 0.9f * r.u(), cz = float(b) + 0.9f * r.u();
+                float dx = cx - 4.0f, dz = cz;
+                if (std::sqrt(dx * dx + dz * dz) <= 0.9f) continue;
+                rt_geom_desc d = blank();
+                d.type = RT_IOW_ELLIPSOID;
+                set3(d.position, cx, 0.2f, cz); set3(d.scale, 0.2f, 0.2f, 0.2f);
+                if (choose < 0.8f) {  // "diffuse": broad-cone reflector
+                    float c0 = r.u() * r.u(), c1 = r.u() * r.u(), c2 = r.u() * r.u();
+                    set3(d.color, c0, c1, c2);
+                    d.reflectivity = 0.5f; d.scat_reflect = 1.0f;
+                } else if (choose < 0.95f) {  // "metal": fuzzed mirror
+                    float c0 = r.u(0.25f, 0.5f), c1 = r.u(0.25f, 0.5f), c2 = r.u(0.25f, 0.5f);
+                    set3(d.color, c0, c1, c2);
+                    d.reflectivity = 0.8f; d.scat_reflect = r.u(0.0f, 0.5f);
+                } else {  // "dielectric"
+                    d.refractivity = 1.0f; d.refractive_index = 1.5f;
+                }
+                out.push_back(d);
+            }
+        rt_geom_desc s1 = blank(); s1.type = RT_IOW_ELLIPSOID; set3(s1.position, 0, 1, 0);
+        s1.refractivity = 1.0f; s1.refractive_index = 1.5f; out.push_back(s1);
+        rt_geom_desc s2 = blank(); s2.type = RT_IOW_ELLIPSOID; set3(s2.position, -4, 1, 0);
+        set3(s2.color, 0.4f, 0.2f, 0.1f); s2.reflectivity = 0.5f; s2.scat_reflect = 1.0f; out.push_back(s2);
+        rt_geom_desc s3 = blank(); s3.type = RT_IOW_ELLIPSOID; set3(s3.position, 4, 1, 0);
+        set3(s3.color, 0.35f, 0.3f, 0.25f); s3.reflectivity = 0.8f; out.push_back(s3);
+        float from[3] = {13, 2, 3}, to[3] = {0, 0, 0}, pitch, yaw;
+        look(from, to, pitch, yaw);
+        cam = cam_at(13, 2, 3, pitch, yaw, 20.0f, 0.1f, 10.0f);
+        params = params_of(1200, 800, 100, 50);
+        return int(out.size());
+    }
+    case RT_PRESET_INW01_GRID: {  // BVH.cpp:83-112 ('R' key) over GeometryData defaults
+        int n = n_hint > 0 ? n_hint : 4;
+        uint32_t grid = 1;
+        while (grid * grid < uint32_t(n)) grid++;
+        grid /= 2;
+        int x = -int(grid), y = -int(grid);
+        for (int i = 0; i < n; i++) {
+            rt_geom_desc d = blank();
+            d.type = RT_INW_ELLIPSOID;
+            d.refractivity = 0.65f; d.reflectivity = 0.15f; d.refractive_index = 1.5f;
+            d.position[0] = float(x) * 1.0f; d.position[1] = float(y) * 1.0f; d.position[2] = 0.0f;
+            d.scale[0] = 1.0f + 0.2f * float(x) * (1.0f / float(grid));
+            d.scale[1] = 1.0f + 0.2f * float(y) * (1.0f / float(grid));
+            d.scale[2] = 1.0f;
+            std::memcpy(d.last_position, d.position, sizeof(d.position));
+            out.push_back(d);
+            if (++x > int(grid)) { x = -int(grid); y++; }
+        }
+        cam = cam_at(-3, 6.5f, -3, -30, 45, 60.0f, 1.0f, 10.0f);  // BVH.cpp:50-52, base.h:268-272, :590
+        params = params_of(100, 100, 1, 5);                       // base.h:249-255
+        return int(out.size());
+    }
+    case RT_PRESET_INW01_RANDOM: {  // config C3
+        int n = n_hint > 0 ? n_hint : 10000;
+        Rng r(seed);
+        for (int i = 0; i < n; i++) {
+            rt_geom_desc d = blank();
+            d.type = RT_INW_ELLIPSOID;
+            float px = r.u(-50, 50), py = r.u(-5, 5), pz = r.u(-50, 50);
+            float rad = r.u(0.1f, 0.4f);
+            float mx = r.u(-0.2f, 0.2f), my = r.u(-0.2f, 0.2f), mz = r.u(-0.2f, 0.2f);
+            set3(d.position, px, py, pz);
+            set3(d.last_position, px - mx, py - my, pz - mz);
+            set3(d.scale, rad, rad, rad);
+            if (r.u() < 0.7f) {
+                d.refractivity = 0.0f; d.reflectivity = r.u(0.5f, 0.9f); d.scat_reflect = r.u(0.0f, 0.3f);
+                float c0 = r.u(0, 0.6f), c1 = r.u(0, 0.6f), c2 = r.u(0, 0.6f);
+                set3(d.color, c0, c1, c2);
+            } else {
+                d.refractivity = 0.65f; d.reflectivity = 0.15f; d.refractive_index = r.u(1.3f, 1.7f);
+                d.scat_refract = r.u(0.0f, 0.3f);
+                float c0 = r.u(0, 0.2f), c1 = r.u(0, 0.2f), c2 = r.u(0, 0.2f);
+                set3(d.color, c0, c1, c2);
+            }
+            out.push_back(d);
+        }
+        cam = cam_at(-60, 15, -60, -12, 45, 60.0f, 0.1f, 40.0f);
+        params = params_of(1920, 1080, 500, 50);
+        return int(out.size());
+    }
+    case RT_PRESET_INW04_REFSET: {  // lights.cpp:116-146 over GeometryData_04 defaults (lights.h:194-201)
+        for (int i = 0; i < 5; i++) {
+            rt_geom_desc d = blank();
+            d.type = RT_INW_ELLIPSOID;
+            d.refractivity = 0.65f; d.reflectivity = 0.15f; d.refractive_index = 1.5f;
+            set3(d.position, 3, 3, 3);
+            out.push_back(d);
+        }
+        out[0].emissive = 1;
+        set3(out[1].position, -1.52f, 3.0f, 1.4f); out[1].emissive = 1;
+        set3(out[2].position, 9, 0, 9); set3(out[2].color, 0.3f, 0.4f, 1.0f);
+        set3(out[3].position, 7, 0, 8); set3(out[3].color, 0.3f, 0.4f, 1.0f);
+        set3(out[4].position, 0, -2, 0); set3(out[4].scale, 100, 1, 100); set3(out[4].color, 0.3f, 0.4f, 1.0f);
+        out[4].refractivity = 0.1f; out[4].reflectivity = 0.6f; out[4].type = RT_INW_CUBOID;
+        for (auto &d : out) std::memcpy(d.last_position, d.position, sizeof(d.position));
+        cam = cam_at(-6.1f, 6.2f, -0.2f, -30, 45, 60.0f, 1.0f, 10.0f);
+        params = params_of(100, 100, 1, 5);
+        return int(out.size());
+    }
+    case RT_PRESET_INW04_CORNELL: {  // config C5; deterministic, seed unused
+        (void)seed;
+        auto wall = [&](float px, float py, float pz, float sx, float sy, float sz, float r, float g, float b) {
+            rt_geom_desc d = blank();
+            d.type = RT_INW_CUBOID;
+            set3(d.position, px, py, pz); set3(d.scale, sx, sy, sz); set3(d.color, r, g, b);
+            d.refractivity = 0.0f; d.reflectivity = 0.5f; d.scat_reflect = 1.0f;
+            out.push_back(d);
+            return out.size() - 1;
+        };
+        const float S = 5.55f, h = S * 0.5f;
+        wall(h, -0.05f, h, S, 0.1f, S, .73f, .73f, .73f);          // floor
+        wall(h, S + 0.05f, h, S, 0.1f, S, .73f, .73f, .73f);       // ceiling
+        wall(h, h, S + 0.05f, S, S, 0.1f, .73f, .73f, .73f);       // back
+        wall(-0.05f, h, h, 0.1f, S, S, .65f, .05f, .05f);          // left (red)
+        wall(S + 0.05f, h, h, 0.1f, S, S, .12f, .45f, .15f);       // right (green)
+        size_t li = wall(2.78f, S - 0.01f, 2.795f, 1.3f, 0.02f, 1.05f, 1, 1, 1);
+        out[li].emissive = 1;                                       // ceiling light
+        size_t tb = wall(3.68f, 1.65f, 3.51f, 1.65f, 3.30f, 1.65f, .73f, .73f, .73f);
+        out[tb].rotation_deg[1] = 15.0f;                           // tall block
+        size_t sb = wall(1.85f, 0.825f, 1.69f, 1.65f, 1.65f, 1.65f, .73f, .73f, .73f);
+        out[sb].rotation_deg[1] = -18.0f;                          // short block
+        rt_geom_desc gl = blank();
+        gl.type = RT_INW_ELLIPSOID;
+        set3(gl.position, 1.85f, 2.25f, 1.69f); set3(gl.scale, 0.6f, 0.6f, 0.6f);
+        gl.refractivity = 0.9f; gl.reflectivity = 0.1f; gl.refractive_index = 1.5f;
+        out.push_back(gl);
+        for (auto &d : out) std::memcpy(d.last_position, d.position, sizeof(d.position));
+        cam = cam_at(2.78f, 2.78f, -8.0f, 0, 90, 40.0f, 0.05f, 10.0f);
+        params = params_of(4096, 4096, 2000, 50);
+        return int(out.size());
+    }
+    default:
+        return RT_E_ARG;
+    }
+}
+
+}  // namespace rtamd

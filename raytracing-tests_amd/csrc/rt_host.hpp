@@ -1,0 +1,109 @@
+// rt_host.hpp -- host-side C++ of the MI355X render path: the scene-description surface
+// the reference stages keep on the CPU (Geometry / Transform_Data / GeometryData /
+// GeometryData_04 / camera), their record packers, the LBVH builder and the sample tables.
+// Everything here is product code (it is what librt_hip.so ships); the CPU oracle under
+// oracle/ is an independent restatement used only by tests to check these bytes.
+//
+// Reference files (relative to /root/reference/Raytracing-Sandbox/Src/):
+//   Utilities/utility.cpp:489-516    Helper::MATH::MakeRotation{X,Y,Z}
+//   In-One-Weekend/03_Shadows_and_Materials/materials.h:43-98   IOW-03 Geometry
+//   In-Next-Week/base.h:12-81        Transform_Buff / Transform_Data
+//   In-Next-Week/01_BoundingVolumeHierarchy/BVH.h:6-76           GeometryBuff / GeometryData
+//   In-Next-Week/04_Lights_Camera_And_Action/lights.h:6-207      GeometryBuff_04 / GeometryData_04
+//   In-Next-Week/LBVH/lbvh.h:11-269  LBVH::ConstructLBVH(_Buff)
+#pragma once
+#include <array>
+#include <cstdint>
+#include <utility>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+#include "../../include/rt_scene.h"
+
+namespace rtamd {
+
+// ---- the slice of glm the reference's host code relies on (column-major mat3) ----------
+struct Vec3 {
+    float x = 0, y = 0, z = 0;
+    Vec3() = default;
+    Vec3(float a, float b, float c) : x(a), y(b), z(c) {}
+    float &operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+    float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+};
+inline Vec3 operator+(Vec3 a, Vec3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline Vec3 operator-(Vec3 a, Vec3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline Vec3 operator*(Vec3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+
+struct Mat3 {
+    Vec3 col[3];  // glm::mat3 m; m[c][r]
+    static Mat3 identity() { Mat3 m; m.col[0] = {1, 0, 0}; m.col[1] = {0, 1, 0}; m.col[2] = {0, 0, 1}; return m; }
+    // glm::mat3(x0,y0,z0, x1,y1,z1, x2,y2,z2) -- nine scalars fill the columns
+    static Mat3 from_cols(float a, float b, float c, float d, float e, float f, float g, float h, float i) {
+        Mat3 m; m.col[0] = {a, b, c}; m.col[1] = {d, e, f}; m.col[2] = {g, h, i}; return m;
+    }
+    float at(int c, int r) const { return col[c][r]; }
+};
+Mat3 operator*(const Mat3 &a, const Mat3 &b);  // glm mat3 product
+Vec3 operator*(const Mat3 &m, Vec3 v);         // glm mat3 * vec3
+Mat3 inverse(const Mat3 &m);                   // glm::inverse (adjugate form)
+float radians(float deg);                      // glm::radians
+Mat3 make_rotation_x(float rad);               // utility.cpp:491-498
+Mat3 make_rotation_y(float rad);               // utility.cpp:500-507
+Mat3 make_rotation_z(float rad);               // utility.cpp:508-515
+Mat3 rotation_zxy(const Vec3 &deg);            // Rz * Rx * Ry (materials.h:80-84, base.h:26-29)
+
+// ---- IOW-03 stage scene description (materials.h:43-98) --------------------------------
+struct IowGeometry {
+    int type = RT_IOW_CUBOID;                     // Typ
+    Vec3 position{0, 0, 0}, rotation{0, 0, 0}, scale{1, 1, 1};
+    Vec3 color{1, 0, 0};
+    Vec3 material{0.2f, 0.3f, 1.5f};              // refractivity, reflectivity, refractive index
+    Vec3 scatteritivity{0, 0, 0};                 // (refract, reflect)
+    Mat3 inv_rotation = Mat3::identity();         // _inv_rotation_matrix
+    void reset_inv_rotation();                    // ResetInvRotationMatrix
+    void fill_buffer(float rec[24]) const;        // FillBuffer
+};
+
+// ---- INW scene description (base.h:19-81, BVH.h:26-76, lights.h:28-207) -----------------
+struct TransformData {
+    Vec3 position{3, 3, 3}, last_position{0, 0, 0}, rotation{0, 0, 0}, scale{1, 1, 1};
+    std::pair<Vec3, Vec3> bb_min_max() const;     // CalculateBBMinMax (base version)
+    void fill_transform(float buf[18]) const;     // FillTransformBuff
+};
+struct GeometryData : TransformData {               // layout 1
+    int type = RT_INW_ELLIPSOID;
+    Vec3 color{0, 0, 0};
+    float refractive_index = 1.5f, refractivity = 0.65f, reflectivity = 0.15f;
+    float scat[2] = {0, 0};
+    void fill_buffer(float buf[28]) const;
+};
+struct GeometryData04 : TransformData {             // layout 4
+    int type = RT_INW_ELLIPSOID;
+    bool emissive = false;
+    Vec3 color{0, 0, 0};
+    int texture_index = 0;
+    float refractive_index = 1.5f, refractivity = 0.65f, reflectivity = 0.15f;
+    float scat[2] = {0, 0};
+    std::pair<Vec3, Vec3> bb_min_max() const;     // override: corner-exact cuboid
+    void fill_buffer(float buf[28]) const;
+};
+
+IowGeometry to_iow(const rt_geom_desc &d);
+GeometryData to_inw01(const rt_geom_desc &d);
+GeometryData04 to_inw04(const rt_geom_desc &d);
+
+// ---- LBVH (lbvh.h) --------------------------------------------------------------------
+// aabbs: N x (min xyz, max xyz).  Returns (2N-1) x 8 floats in the reference's BFS layout.
+std::vector<float> lbvh_build(const float *aabbs, uint32_t n);
+
+// ---- camera (materials.cpp:321-328, base.h:274-281) ------------------------------------
+Vec3 front_from_pitch_yaw(float pitch_deg, float yaw_deg, bool normalize);
+
+// ---- sample tables ----------------------------------------------------------------------
+void sample_tables(int spp, float *sunflower, float *fib, int *ring);
+
+// ---- presets ----------------------------------------------------------------------------
+int scene_preset(int preset, uint32_t seed, int n_hint, std::vector<rt_geom_desc> &out,
+                 rt_cam_desc &cam, rt_params &params);
+
+}  // namespace rtamd

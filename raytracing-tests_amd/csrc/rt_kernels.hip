@@ -1,0 +1,600 @@
+// rt_kernels.hip -- the render hot path for gfx950 (CDNA4, wave64).
+//
+// One thread renders one pixel and walks its samples in order, exactly like the
+// reference's invocation (IOW) or workgroup (INW) does, so the per-pixel reduction order
+// is the reference's sequential one.  A 256-thread block covers a 16x16 pixel tile with
+// each wave on an 8x8 quadrant (coherent camera rays).  Per-thread ray / node stacks live
+// in LDS in a [slot][thread] layout: lane l of a wave touches bank (l mod 32) whatever the
+// stack depth, so divergent stack pointers never conflict.
+//
+// Kernels and the shaders they replace (paths relative to /root/reference/Raytracing-Sandbox/Src/):
+//   k_iow01 <- In-One-Weekend/01_Adding_Sphere/computeShaderSrc.glsl:98-146
+//   k_iow03 <- In-One-Weekend/03_Shadows_and_Materials/computeShaderSrc.glsl:196-430
+//   k_inw   <- In-Next-Week/01_BoundingVolumeHierarchy/computeShaderSrc.glsl:230-675 (LIGHTS=false)
+//              In-Next-Week/04_Lights_Camera_And_Action/computeShaderSrc.glsl:243-773 (LIGHTS=true)
+#include "rt_kernels.hpp"
+#include "rt_math.hpp"
+
+namespace rtk {
+
+constexpr int kBlock = 256;
+
+// ----------------------------------------------------------------------- pixel mapping
+struct Pix { int x, y; bool in_image; size_t out; bool valid; };
+
+__device__ __forceinline__ Pix map_pixel(const Frame &f) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lx = ((wave & 1) << 3) | (lane & 7), ly = ((wave >> 1) << 3) | (lane >> 3);
+    Pix p;
+    if (f.tiles == nullptr) {
+        const int nbx = (f.tw + 15) >> 4;
+        const int bx = blockIdx.x % nbx, by = blockIdx.x / nbx;
+        const int rx = bx * 16 + lx, ry = by * 16 + ly;
+        p.x = f.x0 + rx; p.y = f.y0 + ry;
+        p.valid = rx < f.tw && ry < f.th && p.x >= 0 && p.y >= 0 && p.x < f.W && p.y < f.H;
+        p.in_image = p.valid;
+        p.out = (size_t)p.y * f.W + p.x;
+    } else {
+        const int per = f.tile_size >> 4, sub = per * per;
+        const int tile = blockIdx.x / sub, s = blockIdx.x % sub;
+        const int ix = (s % per) * 16 + lx, iy = (s / per) * 16 + ly;
+        p.x = f.tiles[2 * tile] * f.tile_size + ix;
+        p.y = f.tiles[2 * tile + 1] * f.tile_size + iy;
+        p.in_image = p.x < f.W && p.y < f.H;
+        p.valid = true;  // packed slots outside the image are written as zero
+        p.out = (size_t)tile * f.tile_size * f.tile_size + (size_t)iy * f.tile_size + ix;
+    }
+    return p;
+}
+
+struct Ctr { uint32_t seg = 0, nodes = 0, prims = 0, shadow = 0, drops = 0, nans = 0; };
+
+__device__ __forceinline__ void flush(const Frame &f, const Ctr &c) {
+    if (!f.counters) return;
+    unsigned long long v[6] = {c.seg, c.nodes, c.prims, c.shadow, c.drops, c.nans};
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        unsigned long long s = wave_sum(v[i]);
+        if ((threadIdx.x & 63) == 0 && s) atomicAdd(f.counters + i, s);
+    }
+}
+
+// ============================================================================ IOW-01
+__global__ __launch_bounds__(kBlock) void k_iow01(Frame f) {
+    Pix px = map_pixel(f);
+    if (!px.valid) return;  // no cross-lane work in this kernel
+    f3 color = f3{0, 0, 0};
+    if (px.in_image) {
+        const f3 D = mk(f.dir[0], f.dir[1], f.dir[2]), P = mk(f.pos[0], f.pos[1], f.pos[2]);
+        const f3 C = mk(f.sphere[0], f.sphere[1], f.sphere[2]);
+        const float R = f.sphere[3];
+        float aspect = (float)f.W * rcp((float)f.H);
+        f3 cr = cross(D, f3{0, 1, 0}), cu = cross(cr, D);
+        float sx = ((float)px.x * 2.0f - (float)f.W) * rcp(2.0f * (float)f.W);
+        sx *= aspect;
+        float sy = ((float)px.y * 2.0f - (float)f.H) * rcp(2.0f * (float)f.H);
+        f3 pis = ((P + D * f.focus) + cr * sx) + cu * sy;
+        // CreatePlane((0,-2,0),(0,-2,1),(1,-2,0))
+        const f3 p1 = f3{0, -2, 0};
+        f3 pn = normalize(cross(f3{0, -2, 1} - p1, f3{1, -2, 0} - p1));
+        float pw = -(pn.x * p1.x + pn.y * p1.y + pn.z * p1.z);
+        f3 ro = P, rd = normalize(pis - P);
+        color = background(rd, false);
+        float min_depth = 10000.0f;
+        float t = -(pn.x * ro.x + pn.y * ro.y + pn.z * ro.z + pw) * rcp(pn.x * rd.x + pn.y * rd.y + pn.z * rd.z);
+        if (min_depth > t && t > 0.0f) { color = f3{0.8f, 0.1f, 0.7f}; min_depth = t; }
+        f3 rs = ro - C;
+        float hb = dot(rd, rs), a = dot(rd, rd), c = dot(rs, rs) - R * R;
+        float det = hb * hb - a * c;
+        t = (det > 0.0f && hb < 0.0f) ? ((-hb - __builtin_sqrtf(det)) * rcp(a)) : -1.0f;
+        if (min_depth > t && t > 0.0f) {
+            f3 ip = ro + rd * t;
+            color = f.show_normal ? normalize(ip - C) : f3{1, 0, 0};
+        }
+    }
+    reinterpret_cast<float4 *>(f.out_rgba)[px.out] = make_float4(color.x, color.y, color.z, px.in_image ? 1.0f : 0.0f);
+}
+
+// ============================================================================ IOW-03
+struct RayRet { f3 point, normal, reflected, color, material; float scat0, scat1; };
+
+struct IowObj { f3 pos; int type; m3 M; f3 scale, is; };
+
+__device__ __forceinline__ IowObj iow_obj(const float *__restrict__ h) {
+    IowObj o;
+    o.pos = mk(h[0], h[1], h[2]);
+    o.type = (int)h[3];
+    o.M.c0 = mk(h[4], h[5], h[6]); o.M.c1 = mk(h[7], h[8], h[9]); o.M.c2 = mk(h[10], h[11], h[12]);
+    o.scale = mk(h[13], h[14], h[15]);
+    o.is = mk(h[16], h[17], h[18]);
+    return o;
+}
+
+// LaunchRay 03...glsl:196-256.  The closest hit's normal and attributes are evaluated once
+// after the loop from the winning object (same pure functions of the same inputs).
+__device__ RayRet iow_launch_ray(const IowScene &S, f3 go, f3 gd, float max_t, float contrib, Ctr &c) {
+    float min_t = max_t;
+    int best = -1;
+    f3 best_to = f3{0, 0, 0}, best_nd = f3{0, 0, 0}, best_td = f3{0, 0, 0};
+    c.seg++;
+    c.prims += S.n;
+    for (uint32_t j = 0; j < S.n; j++) {
+        const IowObj ob = iow_obj(S.hot + (size_t)j * kIowHot);
+        f3 to = mul(ob.M, go - ob.pos);
+        f3 td = mul(ob.M, gd);
+        f3 nd = normalize(td);
+        float t = -1.0f;
+        if (ob.type == 2) t = t_ellipsoid(to, nd, ob.is);
+        else if (ob.type == 1) t = t_cuboid(to, nd, ob.scale);
+        if (min_t > t && t > 0.0f) { min_t = t; best = (int)j; best_to = to; best_nd = nd; best_td = td; }
+    }
+    RayRet r;
+    if (min_t < max_t) {
+        const IowObj ob = iow_obj(S.hot + (size_t)best * kIowHot);
+        const float *cold = S.cold + (size_t)best * kIowCold;
+        f3 h = best_to + best_nd * min_t;
+        f3 n = ob.type == 2 ? f3{h.x * ob.is.x * ob.scale.x, h.y * ob.is.y * ob.scale.y, h.z * ob.is.z * ob.scale.z}
+                            : (ob.type == 1 ? cuboid_normal(h, ob.scale) : f3{0, 0, 0});
+        r.color = mk(cold[0], cold[1], cold[2]);
+        r.material = mk(cold[3], cold[4], cold[5]);
+        r.scat0 = cold[6]; r.scat1 = cold[7];
+        const bool inside = dot(n, best_td) > 0.0f;
+        f3 n_ = inside ? -n : n;
+        f3 refl = reflect(best_td, n_);
+        if (!inside) {
+            f3 nir = normalize(cross(n_, best_td));
+            f3 nn = normalize(cross(nir, n_));
+            float s = r.scat1;
+            float k = 1.0f / __builtin_sqrtf(1.0f + s * s);
+            f3 mr = n_ * (s * k) + nn * k;
+            refl = (dot(refl, n_) > dot(mr, n_)) ? refl : mr;
+        }
+        m3 inv = inverse(ob.M);
+        r.point = go + gd * min_t;
+        r.normal = normalize(mul(inv, n));
+        r.reflected = normalize(mul(inv, refl));
+        r.color = r.color * contrib;
+    } else {
+        r.point = f3{0, 0, 0}; r.normal = f3{0, 0, 0};
+        r.reflected = r.color = r.material = f3{0, 0, 0};
+        r.scat0 = r.scat1 = 0.0f;
+    }
+    return r;
+}
+
+__device__ __forceinline__ f3 fib_dir(const IowScene &S, int idx, float s, f3 focus) {
+    const float *t = S.fib + 4 * idx;
+    float x = t[0] * s, y = t[1] * s, z = t[2] * s;
+    f3 yc = focus;
+    f3 zc = normalize(cross(f3{0, 1.0f, 0}, yc));
+    f3 xc = normalize(cross(yc, zc));
+    return normalize(focus + ((xc * x + yc * y) + zc * z));
+}
+
+__device__ __forceinline__ float schlick(float cosine, float ri) {
+    float r0 = (1.0f - ri) * rcp(1.0f + ri);
+    r0 = r0 * r0;
+    float q = 1.0f - cosine;
+    return r0 + (1.0f - r0) * (q * q * q * q * q);
+}
+
+// IOW ray stack (03...glsl:258-283): 4 entries of {orig, dirn, contribution, RI, bounces}
+constexpr int kIowStack = 4, kIowSlot = 9;
+struct IowStack {
+    float *base;  // LDS, [slot][thread]
+    int size;
+    __device__ __forceinline__ float &at(int entry, int k) { return base[(entry * kIowSlot + k) * kBlock]; }
+    __device__ __forceinline__ void push(f3 o, f3 d, float contrib, float ri, int b, Ctr &c) {
+        if (size < kIowStack) {
+            at(size, 0) = o.x; at(size, 1) = o.y; at(size, 2) = o.z;
+            at(size, 3) = d.x; at(size, 4) = d.y; at(size, 5) = d.z;
+            at(size, 6) = contrib; at(size, 7) = ri; at(size, 8) = (float)b;
+            size++;
+        } else c.drops++;
+    }
+};
+
+// LaunchRays 03...glsl:285-358
+__device__ f3 iow_launch_rays(const IowScene &S, const Frame &F, IowStack &K, f3 ro, f3 rd, int sidx, Ctr &c) {
+    K.push(ro, rd, 1.0f, 1.0f, 0, c);
+    f3 sample = f3{0, 0, 0};
+    int skip = 0;
+    while (K.size > 0) {
+        K.size--;
+        const int e = K.size;
+        f3 co = mk(K.at(e, 0), K.at(e, 1), K.at(e, 2)), cd = mk(K.at(e, 3), K.at(e, 4), K.at(e, 5));
+        float contribution = K.at(e, 6), ri = K.at(e, 7);
+        int bounced = (int)K.at(e, 8);
+        RayRet data = iow_launch_ray(S, co, cd, 32000.0f, contribution, c);
+        const bool hit = dot(data.normal, data.normal) > 0.9f;
+        sample = sample + (hit ? data.color : background(cd, false)) * contribution;
+        if (bounced < F.max_bounces && hit) {
+            bounced++;
+            bool spawnRefl = false, spawnRefr = false;
+            f3 refr_dir = f3{0, 0, 0}, refl_dir = f3{0, 0, 0};
+            float cos_t = dot(data.normal, cd);
+            float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+            float target_ri;
+            {
+                int pi = K.size - 1 - skip;
+                float parent = (pi < 0) ? 1.0f : (pi < kIowStack ? K.at(pi, 7) : 0.0f);
+                target_ri = cos_t > 0.0f ? parent : data.material.z;
+            }
+            float rr = (ri * rcp(target_ri)) * sin_t;
+            float refr_c = data.material.x, refl_c = data.material.y;
+            f3 n_ = cos_t > 0.0f ? data.normal : -data.normal;
+            if (cos_t < 0.0f) {
+                refl_dir = fib_dir(S, sidx, data.scat1, data.reflected); spawnRefl = true;
+                float inc = refr_c * schlick(-cos_t, ri * rcp(target_ri));
+                refr_c -= inc; refl_c += inc;
+            } else if (rr > 1.0f) {
+                refr_dir = data.reflected; spawnRefl = true; refl_c = 1.0f;  // sic (03...glsl:332)
+            }
+            if (rr <= 1.0f) {
+                f3 yc = n_ * cos_t, xc = cd - yc;
+                spawnRefr = true;
+                refr_dir = n_ * rr + xc * __builtin_sqrtf(1.0f - rr * rr);
+                refr_dir = fib_dir(S, sidx, data.scat0, refr_dir);
+            }
+            skip = (spawnRefl && spawnRefr) ? skip - 1 : (spawnRefl ? skip : (spawnRefr ? skip + 1 : 0));
+            if (spawnRefl) {
+                if (__builtin_isnan(dot(refl_dir, refl_dir))) c.nans++;
+                K.push(data.point - n_ * 0.000015f, refl_dir, contribution * refl_c, ri, bounced, c);
+            }
+            if (spawnRefr) {
+                if (__builtin_isnan(dot(refr_dir, refr_dir))) c.nans++;
+                K.push(data.point + n_ * 0.000015f, refr_dir, contribution * refr_c, target_ri, bounced, c);
+            }
+        } else skip = 0;
+    }
+    return sample;
+}
+
+__global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S) {
+    __shared__ float lds[kIowStack * kIowSlot * kBlock];
+    Pix px = map_pixel(f);
+    Ctr c;
+    f3 fc = f3{0, 0, 0};
+    if (px.in_image) {
+        IowStack K{lds + threadIdx.x, 0};
+        for (int e = 0; e < kIowStack; e++) K.at(e, 7) = 0.0f;  // stale RI slots start at 0
+        const f3 D = mk(f.dir[0], f.dir[1], f.dir[2]), P = mk(f.pos[0], f.pos[1], f.pos[2]);
+        const int W = f.W, H = f.H, spp = f.spp;
+        int grid = 1;
+        while (grid * grid < spp) grid++;
+        float aspect = (float)W * rcp((float)H);
+        float sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
+        float sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
+        float dsx = aspect * rcp((float)(W * grid));
+        float dsy = 1.0f * rcp((float)(H * grid));
+        f3 look_at = P + D * f.focus;
+        const f3 up = f3{0, 1, 0};
+        f3 cr = cross(D, up), cu = cross(cr, D);
+        bool done = false;
+        for (int s = 0; s < spp; s++) {
+            const int ix = S.ring[2 * s], iy = S.ring[2 * s + 1];
+            if (ix < 0) { fc = fc * rcp((float)s); done = true; break; }
+            float rx = (S.sunflower[2 * s] * f.aperture) * 0.5f, ry = (S.sunflower[2 * s + 1] * f.aperture) * 0.5f;
+            f3 ro = (P + cr * rx) + cu * ry;
+            f3 ld = normalize(look_at - ro);
+            f3 r_ = cross(ld, up), u_ = cross(cr, ld);
+            f3 rd = normalize((ld * f.screen_dist + r_ * (sx + dsx * (float)ix)) + u_ * (sy + dsy * (float)iy));
+            if (!f.show_normal) fc = fc + iow_launch_rays(S, f, K, ro, rd, s, c);
+            else fc = fc + iow_launch_ray(S, ro, rd, 32000.0f, 1.0f, c).normal;
+        }
+        if (!done) fc = fc * rcp((float)spp);
+    }
+    if (px.valid) reinterpret_cast<float4 *>(f.out_rgba)[px.out] = make_float4(fc.x, fc.y, fc.z, px.in_image ? 1.0f : 0.0f);
+    flush(f, c);  // every lane of the wave takes part in the shuffle reduction
+}
+
+// ============================================================================ INW
+constexpr int kFStack = 40;  // stack_capacity, 01_BVH...glsl:80
+constexpr float kMaxT = 32000.0f;
+
+struct FStack {  // FLT_STACK (01_BVH...glsl:81-107) in LDS, [slot][thread]
+    float *base;
+    uint32_t size;
+    __device__ __forceinline__ float &at(uint32_t k) { return base[k * kBlock]; }
+    __device__ __forceinline__ void push(float v, Ctr &c) {
+        if (size < kFStack) { at(size) = v; size++; } else c.drops++;
+    }
+    __device__ __forceinline__ void push_ray(f3 o, f3 d, float contrib, float bounced, Ctr &c) {
+        if (size < kFStack - 7) {
+            at(size) = o.x; at(size + 1) = o.y; at(size + 2) = o.z;
+            at(size + 3) = d.x; at(size + 4) = d.y; at(size + 5) = d.z;
+            at(size + 6) = contrib; at(size + 7) = bounced;
+            size += 8;
+        } else c.drops++;
+    }
+};
+
+struct Xf { f3 pos, scale, delta, is, is2; m3 R; int type; float extra, ri_acc; };
+
+__device__ __forceinline__ Xf load_xf(const InwScene &S, int g) {
+    const float4 *h = S.hot + (size_t)g * 7;
+    float4 a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], q = h[6];
+    Xf x;
+    x.pos = mk(a.x, a.y, a.z);
+    x.R.c0 = mk(a.w, b.x, b.y); x.R.c1 = mk(b.z, b.w, c.x); x.R.c2 = mk(c.y, c.z, c.w);
+    x.scale = mk(d.x, d.y, d.z);
+    x.delta = mk(d.w, e.x, e.y);
+    x.type = (int)(e.z + 0.1f);
+    x.extra = e.w;
+    x.is = mk(f.x, f.y, f.z);
+    x.is2 = mk(f.w, q.x, q.y);
+    x.ri_acc = q.z;
+    return x;
+}
+
+// TestIntersectAABB 01_BVH...glsl:187-208 (reciprocals of the ray direction hoisted)
+__device__ __forceinline__ bool test_aabb(float4 n0, float4 n1, f3 o, f3 id, float tlim) {
+    float a = (n0.x - o.x) * id.x, b = (n0.w - o.x) * id.x;
+    float tmin = fminf(a, b), tmax = fmaxf(a, b);
+    if (tmax <= tmin) return false;  // axis 0 re-applied by the loop is idempotent
+    a = (n0.y - o.y) * id.y; b = (n1.x - o.y) * id.y;
+    tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
+    if (tmax <= tmin) return false;
+    a = (n0.z - o.z) * id.z; b = (n1.y - o.z) * id.z;
+    tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
+    if (tmax <= tmin) return false;
+    return tlim > 0.0f ? tlim > tmin : true;
+}
+
+// closest-hit LBVH DFS (01_BVH...glsl:431-473, 04...glsl:524-563, shadow 620-657)
+template <bool WANT_NORMAL>
+__device__ float inw_traverse(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
+                              float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c) {
+    float final_geom = init_geom;
+    const uint32_t I = K.size;
+    const f3 id = f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    K.push(0.0f, c);
+    for (;;) {
+        float geom = -1.0f;
+        while (K.size > I) {
+            K.size--;
+            const int node = (int)K.at(K.size);
+            const float4 n0 = S.nodes[2 * node], n1 = S.nodes[2 * node + 1];
+            c.nodes++;
+            if (test_aabb(n0, n1, o, id, tlim)) {
+                const float left = n1.z;
+                if (left > 0.1f) {
+                    const float right = left + 1.0f;
+                    K.push(invert ? right : left, c);
+                    K.push(invert ? left : right, c);
+                } else { geom = -left; break; }
+            }
+        }
+        if (!(geom > -0.9f)) break;
+        c.prims++;
+        // IntersectRay / IntersectRayMinimal
+        const Xf x = load_xf(S, (int)geom);
+        f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+        f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+        float t = -1.0f;
+        if (x.type == 1) t = t_ellipsoid(to, td, x.is);
+        else if (x.type == 2) t = t_cuboid(to, td, x.scale);
+        if (t > 0.0f && t < tlim) {
+            tlim = t;
+            final_geom = geom;
+            if (WANT_NORMAL) {
+                f3 h = to + td * t, nl;
+                if (x.type == 1) nl = normalize(f3{h.x * x.is2.x, h.y * x.is2.y, h.z * x.is2.z});
+                else if (x.type == 2) nl = cuboid_normal(h, x.scale);
+                else nl = f3{0, 0, 0};
+                normal = mul(x.R, nl);
+                extra = x.extra;
+            }
+        }
+    }
+    K.size = I;
+    return final_geom;
+}
+
+// Surrounding refractive index (01_BVH...glsl:272-345, 486-502)
+__device__ float inw_surrounding_ri(const InwScene &S, FStack &K, f3 hp, float ratio, Ctr &c) {
+    float acc = 0.0f;
+    uint32_t cnt = 0;
+    const uint32_t I = K.size;
+    K.push(0.0f, c);
+    while (K.size > I) {
+        K.size--;
+        const int node = (int)K.at(K.size);
+        const float4 n0 = S.nodes[2 * node], n1 = S.nodes[2 * node + 1];
+        c.nodes++;
+        if (hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z) {
+            const float left = n1.z;
+            if (left < 0.1f) {
+                c.prims++;
+                const Xf x = load_xf(S, (int)(-left));
+                f3 v = (hp - x.pos) + x.delta * (1.0f - ratio);
+                v = tmul(x.R, v);
+                v.x *= x.is.x; v.y *= x.is.y; v.z *= x.is.z;
+                bool inside;
+                if (x.type == 1) inside = dot(v, v) <= 1.0f;
+                else if (x.type == 2) inside = fabsf(v.x) <= 0.5f && fabsf(v.y) <= 0.5f && fabsf(v.z) <= 0.5f;
+                else inside = false;
+                if (inside) { acc += x.ri_acc; cnt++; }
+            } else {
+                K.push(left, c);
+                K.push(left + 1.0f, c);
+            }
+        }
+    }
+    if (acc > 1.0f) acc *= rcp((float)cnt);
+    else acc = 1.0f;
+    return acc;
+}
+
+__device__ __forceinline__ bool is_lit_geom(const InwScene &S, uint32_t in) {  // 04...glsl:468-474
+    bool r = false;
+    for (uint32_t i = 0; i < S.n_lights && !r; i++) r = in == __float_as_uint(S.lights[i * 7 + 6]);
+    return r;
+}
+__device__ __forceinline__ uint32_t f2u(float f) { return f <= 0.0f ? 0u : (uint32_t)f; }
+
+// deviateWithLinmit90deg 01_BVH...glsl:28-46, power = 1
+__device__ __forceinline__ f3 deviate(const InwScene &S, f3 dir, float tan_theta, int s) {
+    float ap = (2.0f * tan_theta) * 0.5f;
+    float nx = S.sunflower[2 * s] * ap, ny = S.sunflower[2 * s + 1] * ap;
+    f3 right = cross(dir, f3{0, 1, 0});
+    f3 up = cross(right, dir);
+    return normalize(dir + (right * nx + up * ny) * 0.1f);
+}
+
+template <bool LIGHTS>
+__device__ void inw_sample(const InwScene &S, const Frame &F, FStack &K, int px, int py, int s, f3 &out_color,
+                           float &out_depth, Ctr &c) {
+    K.size = 0;
+    f3 color = f3{0, 0, 0};
+    float depth = 0.0f;
+    const f3 D = mk(F.dir[0], F.dir[1], F.dir[2]);
+    const float ratio = (float)s * F.inv_spp;
+    const bool invert = dot(D, f3{1, 1, 1}) > 0.0f;
+    {
+        float aspect = (float)F.W * rcp((float)F.H);
+        float srx = (float)px * rcp((float)F.W) - 0.5f;
+        float sry = (float)py * rcp((float)F.H) - 0.5f;
+        srx *= aspect;
+        const f3 up = f3{0, 1, 0};
+        f3 cr = cross(D, up), cu = cross(cr, D);
+        f3 co = mk(F.pos[0], F.pos[1], F.pos[2]);
+        f3 cd = normalize((D * F.screen_dist + cr * srx) + cu * sry);
+        float ox = S.sunflower[2 * s] * (F.aperture * 0.5f), oy = S.sunflower[2 * s + 1] * (F.aperture * 0.5f);
+        f3 rr = cross(cd, up), ru = cross(rr, cd);
+        f3 tip = ((co + cd) + rr * ox) + ru * oy;
+        f3 la = normalize((co + cd * F.focus) - tip);
+        K.push_ray(tip - la, la, 1.0f, 0.0f, c);
+    }
+    while (K.size > 0) {
+        K.size -= 8;
+        const uint32_t b = K.size;
+        f3 co = mk(K.at(b), K.at(b + 1), K.at(b + 2)), cd = mk(K.at(b + 3), K.at(b + 4), K.at(b + 5));
+        float contribution = K.at(b + 6), bounced = (float)(int)K.at(b + 7);
+        c.seg++;
+        float tlim = kMaxT, extra = 0.0f;
+        f3 normal = f3{0, 0, 0};
+        float fg = inw_traverse<true>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
+        const f3 hitpoint = co + cd * tlim;
+        if (!(tlim < kMaxT)) {
+            color = color + background(cd, LIGHTS && S.n_lights > 0) * contribution;
+            depth = tlim;
+            continue;
+        }
+        const float4 m0 = S.cold[2 * (int)fg], m1 = S.cold[2 * (int)fg + 1];
+        const float m_refr = m0.x, m_refl = m0.y, m_srfr = m0.z, m_srfl = m0.w;
+        const f3 m_color = mk(m1.x, m1.y, m1.z);
+        const float m_ri = LIGHTS ? extra : m1.w;
+        const float surr = inw_surrounding_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
+        if (LIGHTS) {  // 04...glsl:604-665
+            uint32_t is_lit = S.n_lights > 0 ? 0u : (uint32_t)is_lit_geom(S, f2u(fg + 0.1f));
+            if (is_lit == 0) {
+                for (uint32_t i = 0; i < S.n_lights; i++) {
+                    const float *lt = S.lights + i * 7;
+                    f3 bmin = mk(lt[0], lt[1], lt[2]), bmax = mk(lt[3], lt[4], lt[5]);
+                    f3 so = hitpoint + normal * 0.0001f;
+                    float sl = len((bmax + bmin) * 0.5f - so) + len(bmax - bmin);
+                    f3 sd = normalize((bmin + (bmax - bmin) * ratio) - so);
+                    c.shadow++;
+                    f3 dummy_n; float dummy_e;
+                    float sg = inw_traverse<false>(S, K, so, sd, ratio, invert, sl, dummy_n, dummy_e, -1.0f, c);
+                    is_lit += (uint32_t)is_lit_geom(S, f2u(sg + 0.1f));
+                }
+                const uint32_t nl = S.n_lights > 1 ? S.n_lights : 1u;
+                contribution *= (float)is_lit * rcp((float)nl);
+            } else {
+                color = f3{1, 1, 1};
+                K.size = 0;
+                break;
+            }
+        }
+        bool ok;
+        if (!LIGHTS) { bounced += 1.0f; ok = bounced < (float)F.max_bounces; }
+        else ok = bounced < (float)F.max_bounces;
+        if ((m_refl > 0.002f || m_refr > 0.002f) && contribution > 0.01f && ok) {
+            if (LIGHTS) bounced += 1.0f;
+            f3 refl = f3{0, 0, 0}, refr = f3{0, 0, 0};
+            f3 nrm = normal;
+            if (!(dot(nrm, cd) > 0.0f)) {
+                if (m_refl > 0.002f) {
+                    refl = normalize(reflect(cd, nrm));
+                    if (m_srfl > 0.001f) refl = deviate(S, refl, m_srfl, s);
+                }
+                if (m_refr > 0.002f) {
+                    refr = normalize(refract(cd, nrm, surr * rcp(m_ri)));
+                    if (m_srfr > 0.001f) refr = deviate(S, refr, m_srfr, s);
+                }
+            } else {
+                nrm = nrm * -1.0f;
+                refr = refract(cd, nrm, m_ri * rcp(surr));
+                if (dot(refr, refr) < 0.1f) refl = reflect(cd, nrm);
+            }
+            float carried = 0.0f;
+            const float rr2 = dot(refr, refr);
+            if (__builtin_isnan(rr2)) c.nans++;
+            if (rr2 > 0.1f) {
+                carried += m_refr;
+                K.push_ray(hitpoint - nrm * 0.0001f, refr, contribution * m_refr, bounced, c);
+            }
+            if (dot(refl, refl) > 0.1f) {
+                carried += m_refl;
+                K.push_ray(hitpoint + nrm * 0.0001f, refl, contribution * m_refl, bounced, c);
+            }
+            contribution *= (1.0f - 0.5f * carried);
+        }
+        color = color + m_color * contribution;
+    }
+    out_color = color;
+    out_depth = depth;
+}
+
+template <bool LIGHTS>
+__global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S) {
+    __shared__ float lds[kFStack * kBlock];
+    Pix px = map_pixel(f);
+    Ctr c;
+    f3 acc = f3{0, 0, 0};
+    float dmid = 0.0f;
+    if (px.in_image) {
+        FStack K{lds + threadIdx.x, 0};
+        for (int s = 0; s < f.spp; s++) {
+            f3 col; float dep;
+            inw_sample<LIGHTS>(S, f, K, px.x, px.y, s, col, dep, c);
+            f3 g = f3{__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z)};
+            acc = (s == 0) ? g : acc + g;
+            if (s == f.spp / 2) dmid = dep;
+        }
+        acc = acc * rcp((float)f.spp);
+    }
+    if (px.valid) {
+        reinterpret_cast<float4 *>(f.out_rgba)[px.out] = make_float4(acc.x, acc.y, acc.z, px.in_image ? 1.0f : 0.0f);
+        if (f.out_depth) f.out_depth[px.out] = dmid;
+    }
+    flush(f, c);
+}
+
+// ============================================================================ launch
+static dim3 grid_of(const Frame &f) {
+    if (f.tiles) {
+        const int per = f.tile_size >> 4;
+        return dim3((unsigned)(f.n_tiles * per * per));
+    }
+    const int nbx = (f.tw + 15) >> 4, nby = (f.th + 15) >> 4;
+    return dim3((unsigned)(nbx * nby));
+}
+
+hipError_t launch_iow01(const Frame &f, hipStream_t s) {
+    hipLaunchKernelGGL(k_iow01, grid_of(f), dim3(kBlock), 0, s, f);
+    return hipGetLastError();
+}
+hipError_t launch_iow03(const Frame &f, const IowScene &sc, hipStream_t s) {
+    hipLaunchKernelGGL(k_iow03, grid_of(f), dim3(kBlock), 0, s, f, sc);
+    return hipGetLastError();
+}
+hipError_t launch_inw(const Frame &f, const InwScene &sc, hipStream_t s) {
+    if (sc.layout == 4) hipLaunchKernelGGL(k_inw<true>, grid_of(f), dim3(kBlock), 0, s, f, sc);
+    else hipLaunchKernelGGL(k_inw<false>, grid_of(f), dim3(kBlock), 0, s, f, sc);
+    return hipGetLastError();
+}
+
+}  // namespace rtk

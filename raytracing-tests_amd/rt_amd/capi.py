@@ -1,0 +1,258 @@
+"""ctypes binding of librt_hip.so (include/rt_hip.h + include/rt_scene.h).
+
+This is the Python side of the drop-in boundary: a thin mirror of the C ABI with numpy
+arrays in and out.  It loads the in-tree HIP library and fails loudly if it is missing --
+there is no CPU fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "librt_hip.so")
+
+RT_OK, RT_E_ARG, RT_E_HIP, RT_E_NODEVICE, RT_E_UNSUPPORTED = 0, -1, -2, -3, -4
+
+RT_STAGE_IOW01, RT_STAGE_IOW03, RT_STAGE_INW01, RT_STAGE_INW04 = 1, 3, 11, 14
+RT_IOW_CUBOID, RT_IOW_ELLIPSOID = 1, 2
+RT_INW_ELLIPSOID, RT_INW_CUBOID = 1, 2
+
+PRESET_IOW03_REF3 = 1
+PRESET_IOW03_FINAL = 2
+PRESET_INW01_GRID = 3
+PRESET_INW01_RANDOM = 4
+PRESET_INW04_REFSET = 5
+PRESET_INW04_CORNELL = 6
+
+
+class RtCamera(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("dir", C.c_float * 3), ("fov_y_rad", C.c_float),
+                ("aperture", C.c_float), ("focus_dist", C.c_float)]
+
+
+class RtParams(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("spp", C.c_int), ("max_bounces", C.c_int),
+                ("tile_x0", C.c_int), ("tile_y0", C.c_int), ("tile_w", C.c_int), ("tile_h", C.c_int),
+                ("show_normal", C.c_int), ("device", C.c_int)]
+
+
+class RtStats(C.Structure):
+    _fields_ = [("segments", C.c_uint64), ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
+                ("shadow_queries", C.c_uint64), ("stack_drops", C.c_uint64), ("nan_drops", C.c_uint64),
+                ("ms", C.c_double)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class RtGeomDesc(C.Structure):
+    _fields_ = [("type", C.c_int), ("position", C.c_float * 3), ("last_position", C.c_float * 3),
+                ("rotation_deg", C.c_float * 3), ("scale", C.c_float * 3), ("color", C.c_float * 3),
+                ("refractivity", C.c_float), ("reflectivity", C.c_float), ("refractive_index", C.c_float),
+                ("scat_refract", C.c_float), ("scat_reflect", C.c_float), ("emissive", C.c_int),
+                ("texture_index", C.c_int)]
+
+
+class RtCamDesc(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("pitch_deg", C.c_float), ("yaw_deg", C.c_float),
+                ("fov_y_deg", C.c_float), ("aperture", C.c_float), ("focus_dist", C.c_float)]
+
+
+_FP = C.POINTER(C.c_float)
+_IP = C.POINTER(C.c_int)
+_U32P = C.POINTER(C.c_uint32)
+_U64P = C.POINTER(C.c_uint64)
+
+# name -> (restype, argtypes); every symbol include/*.h declares
+SIGNATURES = {
+    "rt_abi_version": (C.c_int, []),
+    "rt_device_info": (C.c_int, [C.c_int, C.c_char_p, C.c_int, _IP]),
+    "rt_render_iow01": (C.c_int, [C.POINTER(RtCamera), _FP, C.POINTER(RtParams), _FP, C.POINTER(RtStats)]),
+    "rt_render_iow03": (C.c_int, [_FP, _FP, C.c_uint32, C.POINTER(RtCamera), C.POINTER(RtParams), _FP,
+                                  C.POINTER(RtStats)]),
+    "rt_render_inw": (C.c_int, [_FP, C.c_uint32, C.c_int, _FP, _FP, C.c_uint32, C.POINTER(RtCamera),
+                                C.POINTER(RtParams), _FP, _FP, C.POINTER(RtStats)]),
+    "rt_lbvh_build": (C.c_int, [_FP, C.c_uint32, _FP]),
+    "rt_dev_scene_iow03": (C.c_void_p, [_FP, _FP, C.c_uint32, C.c_int, C.c_int]),
+    "rt_dev_scene_inw": (C.c_void_p, [_FP, C.c_uint32, C.c_int, _FP, _FP, C.c_uint32, C.c_int, C.c_int]),
+    "rt_dev_scene_free": (None, [C.c_void_p]),
+    "rt_render_tiles_async": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.POINTER(RtParams), C.c_void_p,
+                                        C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_render_image_async": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.POINTER(RtParams), C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_scene_preset": (C.c_int, [C.c_int, C.c_uint32, C.c_int, C.POINTER(RtGeomDesc), C.c_int,
+                                  C.POINTER(RtCamDesc), C.POINTER(RtParams)]),
+    "rt_camera_from_desc": (C.c_int, [C.POINTER(RtCamDesc), C.c_int, C.POINTER(RtCamera)]),
+    "rt_pack_iow03": (C.c_int, [C.POINTER(RtGeomDesc), C.c_uint32, _FP, _FP]),
+    "rt_pack_inw": (C.c_int, [C.POINTER(RtGeomDesc), C.c_uint32, C.c_int, _FP, _FP, _FP, _U32P]),
+    "rt_sample_tables": (C.c_int, [C.c_int, _FP, _FP, _IP]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load librt_hip.so.  Raises (never falls back) if the HIP library is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"librt_hip.so not built at {path}: run __graft_entry__.build() "
+                           "(there is no CPU fallback for the render path)")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def fptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_FP)
+
+
+def check(rc: int, what: str) -> None:
+    if rc != RT_OK:
+        raise RuntimeError(f"{what} failed with status {rc}")
+
+
+# ----------------------------------------------------------------------------- scenes
+@dataclass
+class Scene:
+    """A packed scene in the reference's record layouts (what the GL textures held)."""
+    stage: int
+    desc: object            # ctypes array of RtGeomDesc
+    n: int
+    camera: RtCamera
+    params: RtParams
+    types: np.ndarray | None = None    # IOW-03
+    records: np.ndarray | None = None  # IOW-03 (N,24)
+    geom: np.ndarray | None = None     # INW (N,28)
+    aabbs: np.ndarray | None = None    # INW (N,6)
+    nodes: np.ndarray | None = None    # INW (2N-1,8)
+    lights: np.ndarray | None = None   # INW-04 (L,7)
+    n_lights: int = 0
+
+    @property
+    def layout(self) -> int:
+        return 4 if self.stage == RT_STAGE_INW04 else 1
+
+
+PRESET_STAGE = {PRESET_IOW03_REF3: RT_STAGE_IOW03, PRESET_IOW03_FINAL: RT_STAGE_IOW03,
+                 PRESET_INW01_GRID: RT_STAGE_INW01, PRESET_INW01_RANDOM: RT_STAGE_INW01,
+                 PRESET_INW04_REFSET: RT_STAGE_INW04, PRESET_INW04_CORNELL: RT_STAGE_INW04}
+
+
+def preset_desc(preset: int, seed: int = 0, n_hint: int = 0):
+    lib = load()
+    n = lib.rt_scene_preset(preset, seed, n_hint, None, 0, None, None)
+    if n < 0:
+        raise RuntimeError(f"unknown preset {preset}")
+    arr = (RtGeomDesc * max(n, 1))()
+    cam, par = RtCamDesc(), RtParams()
+    check(lib.rt_scene_preset(preset, seed, n_hint, arr, n, C.byref(cam), C.byref(par)) - n, "rt_scene_preset")
+    return arr, n, cam, par
+
+
+def camera_from_desc(cd: RtCamDesc, stage: int) -> RtCamera:
+    cam = RtCamera()
+    check(load().rt_camera_from_desc(C.byref(cd), stage, C.byref(cam)), "rt_camera_from_desc")
+    return cam
+
+
+def pack(desc, n: int, stage: int, build_lbvh: bool = True) -> dict:
+    lib = load()
+    out: dict = {}
+    if stage == RT_STAGE_IOW03:
+        types = np.zeros(n, np.float32)
+        rec = np.zeros((n, 24), np.float32)
+        check(lib.rt_pack_iow03(desc, n, fptr(types), fptr(rec)), "rt_pack_iow03")
+        out.update(types=types, records=rec)
+    else:
+        layout = 4 if stage == RT_STAGE_INW04 else 1
+        geom = np.zeros((n, 28), np.float32)
+        aabbs = np.zeros((n, 6), np.float32)
+        lights = np.zeros((max(n, 1), 7), np.float32)
+        nl = C.c_uint32(0)
+        check(lib.rt_pack_inw(desc, n, layout, fptr(geom), fptr(aabbs), fptr(lights), C.byref(nl)), "rt_pack_inw")
+        out.update(geom=geom, aabbs=aabbs, lights=lights[: nl.value].copy(), n_lights=nl.value)
+        if build_lbvh:
+            out["nodes"] = lbvh_build(aabbs)
+    return out
+
+
+def make_scene(preset: int, seed: int = 0, n_hint: int = 0, **param_overrides) -> Scene:
+    stage = PRESET_STAGE[preset]
+    arr, n, cd, par = preset_desc(preset, seed, n_hint)
+    for k, v in param_overrides.items():
+        setattr(par, k, v)
+    cam = camera_from_desc(cd, stage)
+    sc = Scene(stage=stage, desc=arr, n=n, camera=cam, params=par)
+    for k, v in pack(arr, n, stage).items():
+        setattr(sc, k, v)
+    return sc
+
+
+def lbvh_build(aabbs: np.ndarray) -> np.ndarray:
+    aabbs = np.ascontiguousarray(aabbs, np.float32)
+    n = aabbs.shape[0]
+    nodes = np.zeros((2 * n - 1, 8), np.float32)
+    check(load().rt_lbvh_build(fptr(aabbs), n, fptr(nodes)), "rt_lbvh_build")
+    return nodes
+
+
+def sample_tables(spp: int):
+    sf = np.zeros((spp, 2), np.float32)
+    fib = np.zeros((spp, 3), np.float32)
+    ring = np.zeros((spp, 2), np.int32)
+    check(load().rt_sample_tables(spp, fptr(sf), fptr(fib), ring.ctypes.data_as(_IP)), "rt_sample_tables")
+    return sf, fib, ring
+
+
+# ---------------------------------------------------------------------------- render
+def render(sc: Scene, params: RtParams | None = None, sphere=None):
+    """Blocking GPU render of a packed scene; returns (rgba (H,W,4), depth or None, stats dict)."""
+    lib = load()
+    p = params or sc.params
+    rgba = np.zeros((p.height, p.width, 4), np.float32)
+    st = RtStats()
+    depth = None
+    if sc.stage == RT_STAGE_IOW01:
+        sph = np.asarray(sphere, np.float32)
+        rc = lib.rt_render_iow01(C.byref(sc.camera), fptr(sph), C.byref(p), fptr(rgba), C.byref(st))
+    elif sc.stage == RT_STAGE_IOW03:
+        rc = lib.rt_render_iow03(fptr(sc.types), fptr(sc.records), sc.n, C.byref(sc.camera), C.byref(p),
+                                 fptr(rgba), C.byref(st))
+    else:
+        depth = np.zeros((p.height, p.width), np.float32)
+        lights = sc.lights if sc.lights is not None and len(sc.lights) else None
+        rc = lib.rt_render_inw(fptr(sc.geom), sc.n, sc.layout, fptr(sc.nodes), fptr(lights), sc.n_lights,
+                               C.byref(sc.camera), C.byref(p), fptr(rgba), fptr(depth), C.byref(st))
+    check(rc, "render")
+    return rgba, depth, st.as_dict()
+
+
+def render_iow01(camera: RtCamera, sphere, params: RtParams):
+    sc = Scene(stage=RT_STAGE_IOW01, desc=None, n=0, camera=camera, params=params)
+    rgba, _, st = render(sc, params, sphere=sphere)
+    return rgba, st
+
+
+def iow01_defaults(width: int = 400, height: int = 225) -> tuple[RtCamera, np.ndarray, RtParams]:
+    """IOW-01 stage defaults (Sphere.h:26,34-37): camera (0,1,10), pitch 0 / yaw -90, focus 1,
+    sphere (0,3,-1) r 3, ShowNormal = true."""
+    cd = RtCamDesc()
+    cd.position[:] = (0.0, 1.0, 10.0)
+    cd.pitch_deg, cd.yaw_deg, cd.fov_y_deg, cd.aperture, cd.focus_dist = 0.0, -90.0, 0.0, 0.0, 1.0
+    cam = camera_from_desc(cd, RT_STAGE_IOW01)
+    p = RtParams()
+    p.width, p.height, p.spp, p.max_bounces, p.show_normal, p.device = width, height, 1, 1, 1, -1
+    return cam, np.array([0.0, 3.0, -1.0, 3.0], np.float32), p
