@@ -103,6 +103,13 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     if not os.path.exists(path):
         raise RuntimeError(f"librt_hip.so not built at {path}: run __graft_entry__.build() "
                            "(there is no CPU fallback for the render path)")
+    # torch bundles its own libamdhip64 (SONAME libamdhip64.so.7).  Loading torch first makes
+    # the dynamic linker resolve our NEEDED libamdhip64.so.7 to that same runtime, so device
+    # pointers, streams and RCCL from torch and our kernels share one HIP runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

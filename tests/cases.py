@@ -1,0 +1,69 @@
+"""Parity cases shared by the CPU (oracle vs golden) and GPU (HIP vs oracle) tests.
+
+Each case is a reference stage + scene + reduced render parameters, sized so the CPU oracle
+finishes in about a second on a few cores.  The full BASELINE configs are covered on the GPU
+through size-independent properties (tests/test_gpu_properties.py).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import rt_amd as R
+
+
+def _scene(preset, seed=0, n_hint=0, **over):
+    return R.make_scene(preset, seed, n_hint, **over)
+
+
+def _no_lights(sc):
+    """INW-04 with zero light sources: exercises the `contribution *= 0/1` quirk (04...glsl:660)."""
+    arr = sc.desc
+    for i in range(sc.n):
+        arr[i].emissive = 0
+    for k, v in R.pack(arr, sc.n, sc.stage).items():
+        setattr(sc, k, v)
+    return sc
+
+
+CASES = {
+    # name: callable -> Scene (IOW-01 handled separately)
+    "iow03_ref3": lambda: _scene(R.PRESET_IOW03_REF3, spp=4),
+    "iow03_ref3_normals": lambda: _scene(R.PRESET_IOW03_REF3, spp=9, show_normal=1),
+    "iow03_ref3_spp1": lambda: _scene(R.PRESET_IOW03_REF3, spp=1),
+    "iow03_ref3_tile": lambda: _scene(R.PRESET_IOW03_REF3, spp=4, tile_x0=100, tile_y0=100, tile_w=100, tile_h=100),
+    "iow03_final": lambda: _scene(R.PRESET_IOW03_FINAL, 20250131, 0, width=32, height=20, spp=2),
+    "iow03_final_b8": lambda: _scene(R.PRESET_IOW03_FINAL, 20250131, 0, width=96, height=64, spp=3, max_bounces=8),
+    "inw01_grid": lambda: _scene(R.PRESET_INW01_GRID, 0, 9, spp=16),
+    "inw01_random": lambda: _scene(R.PRESET_INW01_RANDOM, 1234, 10000, width=96, height=54, spp=8),
+    "inw01_random_spp37": lambda: _scene(R.PRESET_INW01_RANDOM, 1234, 3000, width=64, height=36, spp=37),
+    "inw04_refset": lambda: _scene(R.PRESET_INW04_REFSET, spp=16),
+    "inw04_nolights": lambda: _no_lights(_scene(R.PRESET_INW04_REFSET, spp=8)),
+    "inw04_cornell": lambda: _scene(R.PRESET_INW04_CORNELL, 7, 0, width=64, height=64, spp=8),
+}
+
+GOLDEN_CASES = ["iow01_c1", "iow03_ref3", "iow03_ref3_normals", "iow03_final", "inw01_grid",
+                "inw01_random", "inw04_refset", "inw04_cornell"]
+
+
+def iow01_c1():
+    """Config C1 exactly: IOW-01 400x225, 1 spp, primary rays only, stage defaults."""
+    return R.iow01_defaults(400, 225)
+
+
+def compare(a: np.ndarray, b: np.ndarray) -> dict:
+    """Per-channel comparison that treats NaN == NaN (the reference can produce NaN)."""
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    na, nb = np.isnan(a), np.isnan(b)
+    both = ~(na | nb)
+    d = np.abs(a[both].astype(np.float64) - b[both].astype(np.float64))
+    bits_equal = (a.view(np.uint32) == b.view(np.uint32)) | (na & nb)
+    return {
+        "nan_mismatch": int((na != nb).sum()),
+        "max_abs": float(d.max()) if d.size else 0.0,
+        "n_over_1e-3": int((d > 1e-3).sum()),
+        "exact_frac": float(bits_equal.mean()),
+    }
+
+
+TOL = 1e-3  # north_star: per-channel |delta| <= 1e-3
