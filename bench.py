@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""bench.py -- Mrays/s of the MI355X render path on BASELINE.json's headline configuration.
+
+Workload (BASELINE.json configs[1]): In-One-Weekend 03_Adding_Materials "final scene"
+(~500 spheres + ground cuboid), 1200x800, 100 spp, 50 bounces.  One step = one full frame:
+every pixel, every sample, every bounce of the reference's IOW-03 render loop.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Multi-GPU: the frame is cut into 64x64 tiles dealt round-robin to the ranks (one process per
+GPU); each rank renders its tiles into a packed buffer and the tiles are gathered to rank 0
+with one RCCL gather over xGMI, where the image is assembled.  Total work is fixed, so the
+scaling mode is "strong".
+
+Metric: Mrays/s = W*H*spp*mean_bounces / t = (rays cast, counted by the kernels) / t, summed
+over ranks, t = max over ranks of the timed region (barrier + synchronize on both sides).
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "raytracing-tests_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import rt_amd as R  # noqa: E402
+
+TILE = 64
+FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (= f32 MFMA rate), MI355X_MICROARCH.md
+HBM_PEAK_GBPS = 8000.0     # MI355X HBM3E peak, MI355X_MICROARCH.md
+WORKLOAD = ("In-One-Weekend 03_Adding_Materials final scene (~500 random spheres + ground cuboid), "
+            "1200x800, 100 spp, 50 bounces")
+
+
+def algorithmic_flops(st: dict) -> float:
+    """SURVEY.md 8d contract: F_alg = 40*node_visits + 70*prim_tests + 60*segments."""
+    return 40.0 * st["node_visits"] + 70.0 * st["prim_tests"] + 60.0 * st["segments"]
+
+
+def algorithmic_bytes(st: dict, pixels: int) -> float:
+    """SURVEY.md 8d contract: B_alg = 32*node_visits + 96*prim_tests (IOW records) + 16*W*H."""
+    return 32.0 * st["node_visits"] + 96.0 * st["prim_tests"] + 16.0 * pixels
+
+
+def tiles_for_rank(W: int, H: int, world: int, rank: int):
+    nx, ny = math.ceil(W / TILE), math.ceil(H / TILE)
+    allt = [(tx, ty) for ty in range(ny) for tx in range(nx)]
+    return allt, allt[rank::world], math.ceil(len(allt) / world)
+
+
+def cpu_baseline(sc, threads: int, px: int) -> dict:
+    """The CPU oracle (C restatement of the reference shader, OpenMP) on a bounded sample of the
+    same frame: the central px x px block at the full spp and bounce count."""
+    from oracle import oracle as O
+    O.set_threads(threads)
+    p = R.RtParams()
+    C.memmove(C.addressof(p), C.addressof(sc.params), C.sizeof(p))
+    p.tile_x0, p.tile_y0 = sc.params.width // 2 - px // 2, sc.params.height // 2 - px // 2
+    p.tile_w = p.tile_h = px
+    t0 = time.perf_counter()
+    _, _, st = O.render(sc, p)
+    dt = time.perf_counter() - t0
+    return {"value": st["segments"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"central {px}x{px} pixel block of the same frame at {sc.params.spp} spp / "
+                      f"{sc.params.max_bounces} bounces ({st['segments']} rays, {dt:.1f} s, oracle/librt_oracle.so)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--spp", type=int, default=0, help="override spp (default: the config's 100)")
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--cpu-px", type=int, default=12, help="CPU baseline sample block size")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="host cores for the CPU baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    lib = R.load()
+    over = {}
+    if args.spp:
+        over["spp"] = args.spp
+    if args.width:
+        over["width"] = args.width
+    if args.height:
+        over["height"] = args.height
+    sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0, **over)
+    W, H, spp = sc.params.width, sc.params.height, sc.params.spp
+    allt, mine, per_rank = tiles_for_rank(W, H, world, rank)
+
+    scene = lib.rt_dev_scene_iow03(R.fptr(sc.types), R.fptr(sc.records), sc.n, spp, local)
+    if not scene:
+        raise RuntimeError("rt_dev_scene_iow03 failed (no gfx950 device?)")
+    d_tiles = torch.tensor(mine, dtype=torch.int32, device=dev).reshape(-1, 2).contiguous()
+    packed = torch.zeros((per_rank, TILE, TILE, 4), dtype=torch.float32, device=dev)
+    counters = torch.zeros(6, dtype=torch.int64, device=dev)
+    gathered = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
+    nx, ny = math.ceil(W / TILE), math.ceil(H / TILE)
+    image = torch.empty((ny * TILE, nx * TILE, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        stream = torch.cuda.current_stream()
+        if i is not None:
+            ev[i][0].record(stream)
+        if mine:
+            rc = lib.rt_render_tiles_async(scene, C.byref(sc.camera), C.byref(sc.params), d_tiles.data_ptr(),
+                                           len(mine), TILE, packed.data_ptr(), None, counters.data_ptr(),
+                                           stream.cuda_stream)
+            if rc != 0:
+                raise RuntimeError(f"rt_render_tiles_async -> {rc}")
+        if i is not None:
+            ev[i][1].record(stream)
+        if world > 1:  # the one exchange step: RCCL gather of the packed tiles to rank 0
+            dist.gather(packed, gathered, dst=0)
+        if rank == 0:  # assemble the frame: tile t of rank r is allt[r + world*t]
+            src = torch.stack(gathered, 0) if world > 1 else packed.unsqueeze(0)
+            order = src.permute(1, 0, 2, 3, 4).reshape(-1, TILE, TILE, 4)[: len(allt)]
+            image.copy_(order.view(ny, nx, TILE, TILE, 4).permute(0, 2, 1, 3, 4).reshape(ny * TILE, nx * TILE, 4))
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    counters.zero_()
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    ctr = counters.clone()
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ctr, op=dist.ReduceOp.SUM)
+    elapsed, kernel_ms = float(t[0]), float(t[1])
+    c = [int(v) for v in ctr.cpu().tolist()]
+    st = dict(zip(("segments", "node_visits", "prim_tests", "shadow_queries", "stack_drops", "nan_drops"), c))
+    per_step = {k: v / args.steps for k, v in st.items()}
+
+    if rank == 0:
+        value = st["segments"] / elapsed / 1e6
+        flops = algorithmic_flops(per_step)
+        achieved = flops / (kernel_ms * 1e-3) / 1e12
+        balg = algorithmic_bytes(per_step, W * H / world)
+        traffic = None
+        prof = os.path.join(ROOT, "profiles", "pmc_iow03.json")
+        if os.path.exists(prof):
+            try:
+                pm = json.load(open(prof))
+                if pm.get("config") == [W, H, spp]:
+                    traffic = pm.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(sc, args.cpu_threads, args.cpu_px)
+        out = {
+            "metric": "Mrays/s (W*H*spp*mean_bounces/t)",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded final-scene generator, SURVEY 8d seed 20250131)",
+            "config": {"workload": WORKLOAD, "width": W, "height": H, "spp": spp,
+                       "max_bounces": sc.params.max_bounces, "objects": sc.n, "tile": TILE,
+                       "parallelism": f"tiles_rr{world}" + ("+rccl_gather" if world > 1 else "")},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                         "traffic": traffic, "kernel": "k_iow03", "kernel_ms": round(kernel_ms, 3),
+                         "note": "VALU fp32 kernel (no MFMA on this path); peak = FP32 vector peak"},
+            "hbm": {"achieved_GBps": round(balg / (kernel_ms * 1e-3) / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
+                    "algorithmic_bytes_per_launch": balg},
+            "mean_bounces": round(st["segments"] / (W * H * spp * args.steps), 3),
+            "rays_per_step": int(per_step["segments"]),
+            "counters_per_step": {k: int(v) for k, v in per_step.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    lib.rt_dev_scene_free(scene)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

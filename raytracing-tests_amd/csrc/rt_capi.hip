@@ -8,6 +8,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
+#include <algorithm>
 #include <memory>
 #include <new>
 #include <string>
@@ -93,7 +95,9 @@ struct rt_dev_scene {
     int spp = 0;
     uint32_t n = 0, n_lights = 0;
     int layout = 0;
-    DevBuf hot, cold, nodes, lights, sunflower, fib, ring;
+    int s_stop = 0;      // IOW-03: samples before the ring schedule's early return (== spp in practice)
+    int blocks_cap = 0;  // persistent grid size: resident blocks the device can hold
+    DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
 };
 
 namespace {
@@ -108,6 +112,13 @@ int build_tables(rt_dev_scene *s, int spp) {
     HIP_OK(s->fib.upload(fib4.data(), fib4.size() * sizeof(float)));
     HIP_OK(s->ring.upload(ring.data(), ring.size() * sizeof(int)));
     s->spp = spp;
+    s->s_stop = spp;
+    for (int i = 0; i < spp; i++)
+        if (ring[size_t(i) * 2] < 0) { s->s_stop = i; break; }
+    HIP_OK(s->counter.alloc(64));
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    s->blocks_cap = cus * 8;  // more than can be resident; late blocks find the queue empty and exit
     return RT_OK;
 }
 
@@ -127,6 +138,38 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
     s->kind = 3; s->n = n;
     HIP_OK(s->hot.upload(hot.data(), hot.size() * sizeof(float)));
     HIP_OK(s->cold.upload(cold.data(), cold.size() * sizeof(float)));
+    // Culling BVH over the objects (the reference loops linearly; rtk::iow_launch_ray keeps its
+    // exact result).  World box = |M^T| * local half extents, inflated so it is conservative.
+    const char *force_linear = std::getenv("RT_IOW_LINEAR");  // A/B switch: the reference's linear loop
+    if (n >= 2 && !(force_linear && force_linear[0] == '1')) {
+        std::vector<float> boxes(size_t(n) * 6);
+        for (uint32_t j = 0; j < n; j++) {
+            const float *r = rec + size_t(j) * 24;
+            const bool ell = int(types[j]) == RT_IOW_ELLIPSOID;
+            float h[3];
+            for (int k = 0; k < 3; k++) h[k] = std::fabs(r[12 + k]) * (ell ? 1.0f : 0.5f);
+            float big = std::fmax(std::fabs(r[0]), std::fmax(std::fabs(r[1]), std::fabs(r[2])));
+            for (int k = 0; k < 3; k++) {
+                const float *col = r + 3 + 3 * k;  // column k of M: M_{row j, col k} = col[j]
+                float e = std::fabs(col[0]) * h[0] + std::fabs(col[1]) * h[1] + std::fabs(col[2]) * h[2];
+                e = e * 1.001f + 1e-3f + big * 1e-5f;
+                boxes[size_t(j) * 6 + k] = r[k] - e;
+                boxes[size_t(j) * 6 + 3 + k] = r[k] + e;
+            }
+        }
+        std::vector<float> nodes = rtamd::lbvh_build(boxes.data(), n);
+        // deepest stack the ordered walk can need = tree depth
+        int depth = 0;
+        std::vector<std::pair<uint32_t, int>> st{{0u, 0}};
+        while (!st.empty()) {
+            auto [i, d] = st.back();
+            st.pop_back();
+            depth = std::max(depth, d);
+            float left = nodes[size_t(i) * 8 + 6];
+            if (left > 0.1f) { st.push_back({uint32_t(left), d + 1}); st.push_back({uint32_t(left) + 1, d + 1}); }
+        }
+        if (depth < rtk::kIowBvhStack && n < 65535) HIP_OK(s->nodes.upload(nodes.data(), nodes.size() * sizeof(float)));
+    }
     return build_tables(s, spp);
 }
 
@@ -164,13 +207,13 @@ int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const f
 int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     hipError_t e;
     if (s->kind == 3) {
-        rtk::IowScene sc{s->hot.as<float>(), s->cold.as<float>(), s->n, s->sunflower.as<float>(),
-                         s->fib.as<float>(), s->ring.as<int>()};
-        e = rtk::launch_iow03(f, sc, st);
+        rtk::IowScene sc{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
+                         s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>()};
+        e = rtk::launch_iow03(f, sc, s->counter.as<unsigned>(), s->s_stop, s->blocks_cap, st);
     } else {
         rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
                          s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>()};
-        e = rtk::launch_inw(f, sc, st);
+        e = rtk::launch_inw(f, sc, s->counter.as<unsigned>(), s->blocks_cap, st);
     }
     if (e != hipSuccess) {
         std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));

@@ -110,15 +110,32 @@ __device__ __forceinline__ IowObj iow_obj(const float *__restrict__ h) {
     return o;
 }
 
-// LaunchRay 03...glsl:196-256.  The closest hit's normal and attributes are evaluated once
-// after the loop from the winning object (same pure functions of the same inputs).
-__device__ RayRet iow_launch_ray(const IowScene &S, f3 go, f3 gd, float max_t, float contrib, Ctr &c) {
+// Culling-only slab test for the IOW BVH (never decides a hit: the exact object test does).
+// Boxes are inflated on the host and the limit carries relative slack, so an object whose
+// exact t can win is never culled.  (plane - o) * (1/d) keeps a small relative error in t;
+// the fused form plane*(1/d) - o*(1/d) would cancel catastrophically for large o/d.
+__device__ __forceinline__ bool cull_slab(float4 n0, float4 n1, f3 o, f3 id, float lim, float &te) {
+    const float x0 = (n0.x - o.x) * id.x, x1 = (n0.w - o.x) * id.x;
+    const float y0 = (n0.y - o.y) * id.y, y1 = (n1.x - o.y) * id.y;
+    const float z0 = (n0.z - o.z) * id.z, z1 = (n1.y - o.z) * id.z;
+    te = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    const float tx = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    return te <= tx && tx >= -1e-3f && te <= lim;
+}
+
+// LaunchRay 03...glsl:196-256.  The reference loops over every object and keeps the first
+// strictly nearer hit, i.e. the minimum t with the lowest index among exact ties.  The BVH
+// walk visits a superset of the objects that can attain that minimum and applies the same
+// (t, index) rule, so it returns the same object and the same t bits.  The closest hit's
+// normal and attributes are evaluated once after the search from the winning object.
+__device__ RayRet iow_launch_ray(const IowScene &S, f3 go, f3 gd, float max_t, float contrib, Ctr &c,
+                                 unsigned short *bstk) {
     float min_t = max_t;
     int best = -1;
     f3 best_to = f3{0, 0, 0}, best_nd = f3{0, 0, 0}, best_td = f3{0, 0, 0};
     c.seg++;
-    c.prims += S.n;
-    for (uint32_t j = 0; j < S.n; j++) {
+    auto test = [&](int j) {
+        c.prims++;
         const IowObj ob = iow_obj(S.hot + (size_t)j * kIowHot);
         f3 to = mul(ob.M, go - ob.pos);
         f3 td = mul(ob.M, gd);
@@ -126,7 +143,41 @@ __device__ RayRet iow_launch_ray(const IowScene &S, f3 go, f3 gd, float max_t, f
         float t = -1.0f;
         if (ob.type == 2) t = t_ellipsoid(to, nd, ob.is);
         else if (ob.type == 1) t = t_cuboid(to, nd, ob.scale);
-        if (min_t > t && t > 0.0f) { min_t = t; best = (int)j; best_to = to; best_nd = nd; best_td = td; }
+        if (t > 0.0f && (t < min_t || (t == min_t && j < best))) {
+            min_t = t; best = j; best_to = to; best_nd = nd; best_td = td;
+        }
+    };
+    const float dl2 = dot(gd, gd);
+    if (S.nodes != nullptr && dl2 > 0.998f && dl2 < 1.002f) {
+        const f3 id = f3{__builtin_amdgcn_rcpf(gd.x), __builtin_amdgcn_rcpf(gd.y), __builtin_amdgcn_rcpf(gd.z)};
+        int sp = 0, cur = 0;
+        for (;;) {
+            const float4 n1 = S.nodes[2 * cur + 1];
+            if (n1.z > 0.1f) {
+                const int L = (int)n1.z;
+                const float4 a0 = S.nodes[2 * L], a1 = S.nodes[2 * L + 1];
+                const float4 b0 = S.nodes[2 * L + 2], b1 = S.nodes[2 * L + 3];
+                c.nodes += 2;
+                const float lim = min_t * 1.0001f + 1e-3f;
+                float ta, tb;
+                const bool ha = cull_slab(a0, a1, go, id, lim, ta);
+                const bool hb = cull_slab(b0, b1, go, id, lim, tb);
+                if (ha && hb) {
+                    const bool a_first = ta <= tb;
+                    bstk[(sp++) * kBlock] = (unsigned short)(a_first ? L + 1 : L);
+                    cur = a_first ? L : L + 1;
+                    continue;
+                }
+                if (ha) { cur = L; continue; }
+                if (hb) { cur = L + 1; continue; }
+            } else {
+                test((int)(-n1.z));
+            }
+            if (sp == 0) break;
+            cur = bstk[(--sp) * kBlock];
+        }
+    } else {
+        for (uint32_t j = 0; j < S.n; j++) test((int)j);  // also the path for zero / NaN directions
     }
     RayRet r;
     if (min_t < max_t) {
@@ -178,7 +229,10 @@ __device__ __forceinline__ float schlick(float cosine, float ri) {
     return r0 + (1.0f - r0) * (q * q * q * q * q);
 }
 
-// IOW ray stack (03...glsl:258-283): 4 entries of {orig, dirn, contribution, RI, bounces}
+// IOW ray stack (03...glsl:258-283): 4 entries of {orig, dirn, contribution, RI, bounces}.
+// The entries outlive a sample: the parent-RI lookup (03...glsl:316-319) may read slots above
+// the stack top that an earlier sample of the same pixel wrote, so a pixel's samples stay in
+// order on one lane and the LDS slots persist across them.
 constexpr int kIowStack = 4, kIowSlot = 9;
 struct IowStack {
     float *base;  // LDS, [slot][thread]
@@ -194,98 +248,186 @@ struct IowStack {
     }
 };
 
-// LaunchRays 03...glsl:285-358
-__device__ f3 iow_launch_rays(const IowScene &S, const Frame &F, IowStack &K, f3 ro, f3 rd, int sidx, Ctr &c) {
-    K.push(ro, rd, 1.0f, 1.0f, 0, c);
-    f3 sample = f3{0, 0, 0};
-    int skip = 0;
-    while (K.size > 0) {
-        K.size--;
-        const int e = K.size;
-        f3 co = mk(K.at(e, 0), K.at(e, 1), K.at(e, 2)), cd = mk(K.at(e, 3), K.at(e, 4), K.at(e, 5));
-        float contribution = K.at(e, 6), ri = K.at(e, 7);
-        int bounced = (int)K.at(e, 8);
-        RayRet data = iow_launch_ray(S, co, cd, 32000.0f, contribution, c);
-        const bool hit = dot(data.normal, data.normal) > 0.9f;
-        sample = sample + (hit ? data.color : background(cd, false)) * contribution;
-        if (bounced < F.max_bounces && hit) {
-            bounced++;
-            bool spawnRefl = false, spawnRefr = false;
-            f3 refr_dir = f3{0, 0, 0}, refl_dir = f3{0, 0, 0};
-            float cos_t = dot(data.normal, cd);
-            float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
-            float target_ri;
-            {
-                int pi = K.size - 1 - skip;
-                float parent = (pi < 0) ? 1.0f : (pi < kIowStack ? K.at(pi, 7) : 0.0f);
-                target_ri = cos_t > 0.0f ? parent : data.material.z;
-            }
-            float rr = (ri * rcp(target_ri)) * sin_t;
-            float refr_c = data.material.x, refl_c = data.material.y;
-            f3 n_ = cos_t > 0.0f ? data.normal : -data.normal;
-            if (cos_t < 0.0f) {
-                refl_dir = fib_dir(S, sidx, data.scat1, data.reflected); spawnRefl = true;
-                float inc = refr_c * schlick(-cos_t, ri * rcp(target_ri));
-                refr_c -= inc; refl_c += inc;
-            } else if (rr > 1.0f) {
-                refr_dir = data.reflected; spawnRefl = true; refl_c = 1.0f;  // sic (03...glsl:332)
-            }
-            if (rr <= 1.0f) {
-                f3 yc = n_ * cos_t, xc = cd - yc;
-                spawnRefr = true;
-                refr_dir = n_ * rr + xc * __builtin_sqrtf(1.0f - rr * rr);
-                refr_dir = fib_dir(S, sidx, data.scat0, refr_dir);
-            }
-            skip = (spawnRefl && spawnRefr) ? skip - 1 : (spawnRefl ? skip : (spawnRefr ? skip + 1 : 0));
-            if (spawnRefl) {
-                if (__builtin_isnan(dot(refl_dir, refl_dir))) c.nans++;
-                K.push(data.point - n_ * 0.000015f, refl_dir, contribution * refl_c, ri, bounced, c);
-            }
-            if (spawnRefr) {
-                if (__builtin_isnan(dot(refr_dir, refr_dir))) c.nans++;
-                K.push(data.point + n_ * 0.000015f, refr_dir, contribution * refr_c, target_ri, bounced, c);
-            }
-        } else skip = 0;
-    }
-    return sample;
+// One iteration of LaunchRays' while loop (03...glsl:294-356): pop, cast, shade, push.
+__device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, IowStack &K, int &skip, f3 &sample,
+                                            int sidx, Ctr &c, unsigned short *bstk) {
+    K.size--;
+    const int e = K.size;
+    f3 co = mk(K.at(e, 0), K.at(e, 1), K.at(e, 2)), cd = mk(K.at(e, 3), K.at(e, 4), K.at(e, 5));
+    float contribution = K.at(e, 6), ri = K.at(e, 7);
+    int bounced = (int)K.at(e, 8);
+    RayRet data = iow_launch_ray(S, co, cd, 32000.0f, contribution, c, bstk);
+    const bool hit = dot(data.normal, data.normal) > 0.9f;
+    sample = sample + (hit ? data.color : background(cd, false)) * contribution;
+    if (bounced < F.max_bounces && hit) {
+        bounced++;
+        bool spawnRefl = false, spawnRefr = false;
+        f3 refr_dir = f3{0, 0, 0}, refl_dir = f3{0, 0, 0};
+        float cos_t = dot(data.normal, cd);
+        float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+        float target_ri;
+        {
+            int pi = K.size - 1 - skip;
+            float parent = (pi < 0) ? 1.0f : (pi < kIowStack ? K.at(pi, 7) : 0.0f);
+            target_ri = cos_t > 0.0f ? parent : data.material.z;
+        }
+        float rr = (ri * rcp(target_ri)) * sin_t;
+        float refr_c = data.material.x, refl_c = data.material.y;
+        f3 n_ = cos_t > 0.0f ? data.normal : -data.normal;
+        if (cos_t < 0.0f) {
+            refl_dir = fib_dir(S, sidx, data.scat1, data.reflected); spawnRefl = true;
+            float inc = refr_c * schlick(-cos_t, ri * rcp(target_ri));
+            refr_c -= inc; refl_c += inc;
+        } else if (rr > 1.0f) {
+            refr_dir = data.reflected; spawnRefl = true; refl_c = 1.0f;  // sic (03...glsl:332)
+        }
+        if (rr <= 1.0f) {
+            f3 yc = n_ * cos_t, xc = cd - yc;
+            spawnRefr = true;
+            refr_dir = n_ * rr + xc * __builtin_sqrtf(1.0f - rr * rr);
+            refr_dir = fib_dir(S, sidx, data.scat0, refr_dir);
+        }
+        skip = (spawnRefl && spawnRefr) ? skip - 1 : (spawnRefl ? skip : (spawnRefr ? skip + 1 : 0));
+        if (spawnRefl) {
+            if (__builtin_isnan(dot(refl_dir, refl_dir))) c.nans++;
+            K.push(data.point - n_ * 0.000015f, refl_dir, contribution * refl_c, ri, bounced, c);
+        }
+        if (spawnRefr) {
+            if (__builtin_isnan(dot(refr_dir, refr_dir))) c.nans++;
+            K.push(data.point + n_ * 0.000015f, refr_dir, contribution * refr_c, target_ri, bounced, c);
+        }
+    } else skip = 0;
 }
 
-__global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S) {
-    __shared__ float lds[kIowStack * kIowSlot * kBlock];
-    Pix px = map_pixel(f);
-    Ctr c;
-    f3 fc = f3{0, 0, 0};
-    if (px.in_image) {
-        IowStack K{lds + threadIdx.x, 0};
-        for (int e = 0; e < kIowStack; e++) K.at(e, 7) = 0.0f;  // stale RI slots start at 0
-        const f3 D = mk(f.dir[0], f.dir[1], f.dir[2]), P = mk(f.pos[0], f.pos[1], f.pos[2]);
-        const int W = f.W, H = f.H, spp = f.spp;
-        int grid = 1;
-        while (grid * grid < spp) grid++;
-        float aspect = (float)W * rcp((float)H);
-        float sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
-        float sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
-        float dsx = aspect * rcp((float)(W * grid));
-        float dsy = 1.0f * rcp((float)(H * grid));
-        f3 look_at = P + D * f.focus;
-        const f3 up = f3{0, 1, 0};
-        f3 cr = cross(D, up), cu = cross(cr, D);
-        bool done = false;
-        for (int s = 0; s < spp; s++) {
-            const int ix = S.ring[2 * s], iy = S.ring[2 * s + 1];
-            if (ix < 0) { fc = fc * rcp((float)s); done = true; break; }
-            float rx = (S.sunflower[2 * s] * f.aperture) * 0.5f, ry = (S.sunflower[2 * s + 1] * f.aperture) * 0.5f;
-            f3 ro = (P + cr * rx) + cu * ry;
-            f3 ld = normalize(look_at - ro);
-            f3 r_ = cross(ld, up), u_ = cross(cr, ld);
-            f3 rd = normalize((ld * f.screen_dist + r_ * (sx + dsx * (float)ix)) + u_ * (sy + dsy * (float)iy));
-            if (!f.show_normal) fc = fc + iow_launch_rays(S, f, K, ro, rd, s, c);
-            else fc = fc + iow_launch_ray(S, ro, rd, 32000.0f, 1.0f, c).normal;
-        }
-        if (!done) fc = fc * rcp((float)spp);
+// ---------------------------------------------------------------- persistent work queue
+// Work unit = one pixel.  A wave keeps all 64 lanes busy: a lane that finishes its pixel
+// takes the next one with a wave-aggregated atomic (ballot -> popcount -> one atomicAdd ->
+// per-lane rank by masked popcount), so divergent path lengths never idle the wave.
+struct UnitPix { int x, y; bool in_image; size_t out; };
+
+__device__ __forceinline__ UnitPix unit_pixel(const Frame &f, uint32_t u) {
+    UnitPix p;
+    const int l = (int)(u & 63u);
+    if (f.tiles == nullptr) {
+        const int b = (int)(u >> 6), nbx = (f.tw + 7) >> 3;
+        const int rx = (b % nbx) * 8 + (l & 7), ry = (b / nbx) * 8 + (l >> 3);
+        p.x = f.x0 + rx; p.y = f.y0 + ry;
+        p.in_image = rx < f.tw && ry < f.th && p.x >= 0 && p.y >= 0 && p.x < f.W && p.y < f.H;
+        p.out = p.in_image ? (size_t)p.y * f.W + p.x : (size_t)-1;
+    } else {
+        const uint32_t area = (uint32_t)f.tile_size * f.tile_size;
+        const int t = (int)(u / area), r = (int)(u % area), per = f.tile_size >> 3;
+        const int b = r >> 6;
+        const int ix = (b % per) * 8 + (l & 7), iy = (b / per) * 8 + (l >> 3);
+        p.x = f.tiles[2 * t] * f.tile_size + ix;
+        p.y = f.tiles[2 * t + 1] * f.tile_size + iy;
+        p.in_image = p.x < f.W && p.y < f.H;
+        p.out = (size_t)t * area + (size_t)iy * f.tile_size + ix;
     }
-    if (px.valid) reinterpret_cast<float4 *>(f.out_rgba)[px.out] = make_float4(fc.x, fc.y, fc.z, px.in_image ? 1.0f : 0.0f);
-    flush(f, c);  // every lane of the wave takes part in the shuffle reduction
+    return p;
+}
+
+__device__ __forceinline__ uint32_t units_total(const Frame &f) {
+    if (f.tiles) return (uint32_t)f.n_tiles * f.tile_size * f.tile_size;
+    return (uint32_t)(((f.tw + 7) >> 3) * ((f.th + 7) >> 3)) * 64u;
+}
+
+// wave-aggregated fetch: lanes with `need` get consecutive unit ids
+__device__ __forceinline__ uint32_t fetch_unit(unsigned *counter, bool need) {
+    const unsigned long long mask = __ballot(need);
+    if (mask == 0) return 0xffffffffu;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((long long)mask) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (unsigned)__popcll(mask));
+    base = __shfl(base, leader, 64);
+    const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    return need ? base + rank : 0xffffffffu;
+}
+
+__device__ __forceinline__ void write_px(const Frame &f, const UnitPix &p, f3 c, float depth) {
+    if (p.out == (size_t)-1) return;
+    reinterpret_cast<float4 *>(f.out_rgba)[p.out] = make_float4(c.x, c.y, c.z, p.in_image ? 1.0f : 0.0f);
+    if (f.out_depth) f.out_depth[p.out] = depth;
+}
+
+// Camera ray of sample s of a pixel, out_Pixel 03...glsl:370-406
+struct IowPixelCam { float sx, sy; };
+__device__ __forceinline__ void iow_camera_ray(const IowScene &S, const Frame &f, float sx, float sy, float dsx,
+                                               float dsy, int s, f3 &ro, f3 &rd) {
+    const f3 D = mk(f.dir[0], f.dir[1], f.dir[2]), P = mk(f.pos[0], f.pos[1], f.pos[2]);
+    const f3 up = f3{0, 1, 0};
+    f3 look_at = P + D * f.focus;
+    f3 cr = cross(D, up), cu = cross(cr, D);
+    const int ix = S.ring[2 * s], iy = S.ring[2 * s + 1];
+    float rx = (S.sunflower[2 * s] * f.aperture) * 0.5f, ry = (S.sunflower[2 * s + 1] * f.aperture) * 0.5f;
+    ro = (P + cr * rx) + cu * ry;
+    f3 ld = normalize(look_at - ro);
+    f3 r_ = cross(ld, up), u_ = cross(cr, ld);
+    rd = normalize((ld * f.screen_dist + r_ * (sx + dsx * (float)ix)) + u_ * (sy + dsy * (float)iy));
+}
+
+__global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, unsigned *counter, int s_stop) {
+    __shared__ float lds[kIowStack * kIowSlot * kBlock];
+    __shared__ unsigned short lds_bvh[kIowBvhStack * kBlock];
+    unsigned short *bstk = lds_bvh + threadIdx.x;
+    Ctr c;
+    IowStack K{lds + threadIdx.x, 0};
+    const uint32_t total = units_total(f);
+    const int W = f.W, H = f.H, spp = f.spp;
+    int grid = 1;
+    while (grid * grid < spp) grid++;
+    const float aspect = (float)W * rcp((float)H);
+    const float dsx = aspect * rcp((float)(W * grid));
+    const float dsy = 1.0f * rcp((float)(H * grid));
+    bool live = true;     // lane may still find work
+    bool busy = false;    // lane owns a pixel
+    UnitPix px{};
+    float sx = 0, sy = 0;
+    f3 fc = f3{0, 0, 0}, sample = f3{0, 0, 0};
+    int s = 0, skip = 0;
+    for (;;) {
+        const uint32_t u = fetch_unit(counter, live && !busy);
+        if (live && !busy) {
+            if (u >= total) live = false;
+            else {
+                px = unit_pixel(f, u);
+                if (!px.in_image) write_px(f, px, f3{0, 0, 0}, 0.0f);
+                else {
+                    busy = true;
+                    for (int e = 0; e < kIowStack; e++) K.at(e, 7) = 0.0f;  // stale RI slots start at 0
+                    sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
+                    sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
+                    fc = f3{0, 0, 0};
+                    s = 0;
+                    K.size = 0;
+                }
+            }
+        }
+        if (__ballot(live) == 0) break;
+        if (!busy) continue;
+        if (K.size == 0) {  // start sample s
+            f3 ro, rd;
+            iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
+            if (f.show_normal) {
+                fc = fc + iow_launch_ray(S, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
+                s++;
+            } else {
+                K.push(ro, rd, 1.0f, 1.0f, 0, c);
+                sample = f3{0, 0, 0};
+                skip = 0;
+            }
+        }
+        if (K.size > 0) {
+            iow_segment(S, f, K, skip, sample, s, c, bstk);
+            if (K.size == 0) { fc = fc + sample; s++; }
+        }
+        if (K.size == 0 && s >= s_stop) {
+            write_px(f, px, fc * rcp((float)s_stop), 0.0f);
+            busy = false;
+        }
+    }
+    flush(f, c);
 }
 
 // ============================================================================ INW
@@ -442,31 +584,34 @@ __device__ __forceinline__ f3 deviate(const InwScene &S, f3 dir, float tan_theta
     return normalize(dir + (right * nx + up * ny) * 0.1f);
 }
 
-template <bool LIGHTS>
-__device__ void inw_sample(const InwScene &S, const Frame &F, FStack &K, int px, int py, int s, f3 &out_color,
-                           float &out_depth, Ctr &c) {
+// Camera ray of sample s (out_Pixel prologue, 01_BVH...glsl:366-410): push it, reset the sample.
+__device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame &F, FStack &K, int px, int py, int s,
+                                                 Ctr &c) {
     K.size = 0;
-    f3 color = f3{0, 0, 0};
-    float depth = 0.0f;
+    const f3 D = mk(F.dir[0], F.dir[1], F.dir[2]);
+    float aspect = (float)F.W * rcp((float)F.H);
+    float srx = (float)px * rcp((float)F.W) - 0.5f;
+    float sry = (float)py * rcp((float)F.H) - 0.5f;
+    srx *= aspect;
+    const f3 up = f3{0, 1, 0};
+    f3 cr = cross(D, up), cu = cross(cr, D);
+    f3 co = mk(F.pos[0], F.pos[1], F.pos[2]);
+    f3 cd = normalize((D * F.screen_dist + cr * srx) + cu * sry);
+    float ox = S.sunflower[2 * s] * (F.aperture * 0.5f), oy = S.sunflower[2 * s + 1] * (F.aperture * 0.5f);
+    f3 rr = cross(cd, up), ru = cross(rr, cd);
+    f3 tip = ((co + cd) + rr * ox) + ru * oy;
+    f3 la = normalize((co + cd * F.focus) - tip);
+    K.push_ray(tip - la, la, 1.0f, 0.0f, c);
+}
+
+// One iteration of out_Pixel's ray loop (01_BVH...glsl:414-597 / 04...glsl:510-713):
+// pop a ray, closest hit, surrounding RI, shadow rays, push reflect/refract, accumulate.
+template <bool LIGHTS>
+__device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s, f3 &color, float &depth, Ctr &c) {
     const f3 D = mk(F.dir[0], F.dir[1], F.dir[2]);
     const float ratio = (float)s * F.inv_spp;
     const bool invert = dot(D, f3{1, 1, 1}) > 0.0f;
-    {
-        float aspect = (float)F.W * rcp((float)F.H);
-        float srx = (float)px * rcp((float)F.W) - 0.5f;
-        float sry = (float)py * rcp((float)F.H) - 0.5f;
-        srx *= aspect;
-        const f3 up = f3{0, 1, 0};
-        f3 cr = cross(D, up), cu = cross(cr, D);
-        f3 co = mk(F.pos[0], F.pos[1], F.pos[2]);
-        f3 cd = normalize((D * F.screen_dist + cr * srx) + cu * sry);
-        float ox = S.sunflower[2 * s] * (F.aperture * 0.5f), oy = S.sunflower[2 * s + 1] * (F.aperture * 0.5f);
-        f3 rr = cross(cd, up), ru = cross(rr, cd);
-        f3 tip = ((co + cd) + rr * ox) + ru * oy;
-        f3 la = normalize((co + cd * F.focus) - tip);
-        K.push_ray(tip - la, la, 1.0f, 0.0f, c);
-    }
-    while (K.size > 0) {
+    do {
         K.size -= 8;
         const uint32_t b = K.size;
         f3 co = mk(K.at(b), K.at(b + 1), K.at(b + 2)), cd = mk(K.at(b + 3), K.at(b + 4), K.at(b + 5));
@@ -479,7 +624,7 @@ __device__ void inw_sample(const InwScene &S, const Frame &F, FStack &K, int px,
         if (!(tlim < kMaxT)) {
             color = color + background(cd, LIGHTS && S.n_lights > 0) * contribution;
             depth = tlim;
-            continue;
+            break;
         }
         const float4 m0 = S.cold[2 * (int)fg], m1 = S.cold[2 * (int)fg + 1];
         const float m_refr = m0.x, m_refl = m0.y, m_srfr = m0.z, m_srfl = m0.w;
@@ -543,57 +688,79 @@ __device__ void inw_sample(const InwScene &S, const Frame &F, FStack &K, int px,
             contribution *= (1.0f - 0.5f * carried);
         }
         color = color + m_color * contribution;
-    }
-    out_color = color;
-    out_depth = depth;
+    } while (false);
 }
 
 template <bool LIGHTS>
-__global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S) {
+__global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S, unsigned *counter) {
     __shared__ float lds[kFStack * kBlock];
-    Pix px = map_pixel(f);
     Ctr c;
-    f3 acc = f3{0, 0, 0};
-    float dmid = 0.0f;
-    if (px.in_image) {
-        FStack K{lds + threadIdx.x, 0};
-        for (int s = 0; s < f.spp; s++) {
-            f3 col; float dep;
-            inw_sample<LIGHTS>(S, f, K, px.x, px.y, s, col, dep, c);
+    FStack K{lds + threadIdx.x, 0};
+    const uint32_t total = units_total(f);
+    bool live = true, busy = false;
+    UnitPix px{};
+    f3 acc = f3{0, 0, 0}, col = f3{0, 0, 0};
+    float dmid = 0.0f, dep = 0.0f;
+    int s = 0;
+    K.size = 0;
+    for (;;) {
+        const uint32_t u = fetch_unit(counter, live && !busy);
+        if (live && !busy) {
+            if (u >= total) live = false;
+            else {
+                px = unit_pixel(f, u);
+                if (!px.in_image) write_px(f, px, f3{0, 0, 0}, 0.0f);
+                else { busy = true; s = 0; acc = f3{0, 0, 0}; dmid = 0.0f; K.size = 0; }
+            }
+        }
+        if (__ballot(live) == 0) break;
+        if (!busy) continue;
+        // one ray segment per iteration (samples of a pixel are independent invocations)
+        if (K.size == 0) { inw_start_sample(S, f, K, px.x, px.y, s, c); col = f3{0, 0, 0}; dep = 0.0f; }
+        inw_segment<LIGHTS>(S, f, K, s, col, dep, c);
+        if (K.size == 0) {  // sample done: End() accumulates sqrt(colour) in sample order
             f3 g = f3{__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z)};
             acc = (s == 0) ? g : acc + g;
             if (s == f.spp / 2) dmid = dep;
+            s++;
+            if (s >= f.spp) {
+                write_px(f, px, acc * rcp((float)f.spp), dmid);
+                busy = false;
+            }
         }
-        acc = acc * rcp((float)f.spp);
-    }
-    if (px.valid) {
-        reinterpret_cast<float4 *>(f.out_rgba)[px.out] = make_float4(acc.x, acc.y, acc.z, px.in_image ? 1.0f : 0.0f);
-        if (f.out_depth) f.out_depth[px.out] = dmid;
     }
     flush(f, c);
 }
 
 // ============================================================================ launch
-static dim3 grid_of(const Frame &f) {
-    if (f.tiles) {
-        const int per = f.tile_size >> 4;
-        return dim3((unsigned)(f.n_tiles * per * per));
-    }
-    const int nbx = (f.tw + 15) >> 4, nby = (f.th + 15) >> 4;
-    return dim3((unsigned)(nbx * nby));
+static unsigned grid_of(const Frame &f, int blocks_cap) {
+    const uint64_t units = f.tiles ? (uint64_t)f.n_tiles * f.tile_size * f.tile_size
+                                   : (uint64_t)(((f.tw + 7) >> 3) * ((f.th + 7) >> 3)) * 64u;
+    uint64_t b = (units + kBlock - 1) / kBlock;
+    if (b > (uint64_t)blocks_cap) b = blocks_cap;
+    return (unsigned)(b ? b : 1);
+}
+static dim3 grid_iow01(const Frame &f) {
+    if (f.tiles) { const int per = f.tile_size >> 4; return dim3((unsigned)(f.n_tiles * per * per)); }
+    return dim3((unsigned)(((f.tw + 15) >> 4) * ((f.th + 15) >> 4)));
 }
 
 hipError_t launch_iow01(const Frame &f, hipStream_t s) {
-    hipLaunchKernelGGL(k_iow01, grid_of(f), dim3(kBlock), 0, s, f);
+    hipLaunchKernelGGL(k_iow01, grid_iow01(f), dim3(kBlock), 0, s, f);
     return hipGetLastError();
 }
-hipError_t launch_iow03(const Frame &f, const IowScene &sc, hipStream_t s) {
-    hipLaunchKernelGGL(k_iow03, grid_of(f), dim3(kBlock), 0, s, f, sc);
+hipError_t launch_iow03(const Frame &f, const IowScene &sc, unsigned *counter, int s_stop, int blocks_cap,
+                        hipStream_t s) {
+    hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_iow03, dim3(grid_of(f, blocks_cap)), dim3(kBlock), 0, s, f, sc, counter, s_stop);
     return hipGetLastError();
 }
-hipError_t launch_inw(const Frame &f, const InwScene &sc, hipStream_t s) {
-    if (sc.layout == 4) hipLaunchKernelGGL(k_inw<true>, grid_of(f), dim3(kBlock), 0, s, f, sc);
-    else hipLaunchKernelGGL(k_inw<false>, grid_of(f), dim3(kBlock), 0, s, f, sc);
+hipError_t launch_inw(const Frame &f, const InwScene &sc, unsigned *counter, int blocks_cap, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    if (sc.layout == 4) hipLaunchKernelGGL(k_inw<true>, dim3(grid_of(f, blocks_cap)), dim3(kBlock), 0, s, f, sc, counter);
+    else hipLaunchKernelGGL(k_inw<false>, dim3(grid_of(f, blocks_cap)), dim3(kBlock), 0, s, f, sc, counter);
     return hipGetLastError();
 }
 

@@ -28,9 +28,11 @@ constexpr int kIowCold = 8;   // color3 material3 scat2
 constexpr int kInwHot = 28;   // pos3 R9 scale3 delta3 type extra inv_scale3 inv_s2_3 ri_acc pad
 constexpr int kInwCold = 8;   // refr refl srfr srfl color3 ri
 
+constexpr int kIowBvhStack = 32;  // deepest IOW BVH the kernel walks; deeper trees use the linear loop
 struct IowScene {
     const float *hot, *cold;
     uint32_t n;
+    const float4 *nodes;     // conservative BVH over the objects ((2n-1)*2 float4) or null = linear loop
     const float *sunflower;  // spp*2
     const float *fib;        // spp*4 (xyz + pad)
     const int *ring;         // spp*2
@@ -46,7 +48,10 @@ struct InwScene {
 };
 
 hipError_t launch_iow01(const Frame &f, hipStream_t s);
-hipError_t launch_iow03(const Frame &f, const IowScene &sc, hipStream_t s);
-hipError_t launch_inw(const Frame &f, const InwScene &sc, hipStream_t s);
+// Persistent work-queue launches: `counter` (one u32, device) is zeroed on `s` before the
+// kernel; at most `blocks_cap` blocks are launched (they pull pixels until none are left).
+hipError_t launch_iow03(const Frame &f, const IowScene &sc, unsigned *counter, int s_stop, int blocks_cap,
+                        hipStream_t s);
+hipError_t launch_inw(const Frame &f, const InwScene &sc, unsigned *counter, int blocks_cap, hipStream_t s);
 
 }  // namespace rtk

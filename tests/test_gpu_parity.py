@@ -48,7 +48,10 @@ def test_render_matches_oracle(gpu, name):
         _check(name + ":depth", gd, od)
     print(name, "gpu", {k: gst[k] for k in COUNTERS}, "ms %.2f" % gst["ms"])
     print(name, "cpu", {k: ost[k] for k in COUNTERS}, "ms %.2f" % ost["ms"])
-    for k in COUNTERS:
+    # IOW-03 walks a culling BVH instead of the reference's linear object loop, so its node /
+    # primitive counts are its own; every ray-level counter must still match exactly.
+    exact = COUNTERS if sc.stage != R.RT_STAGE_IOW03 else ("segments", "shadow_queries", "stack_drops", "nan_drops")
+    for k in exact:
         assert gst[k] == ost[k], (k, gst[k], ost[k])
     assert c["exact_frac"] == 1.0, c
 
