@@ -87,6 +87,7 @@ def main():
     ap.add_argument("--cpu-px", type=int, default=12, help="CPU baseline sample block size")
     ap.add_argument("--cpu-threads", type=int, default=16, help="host cores for the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--occupancy", action="store_true", help="report per-phase lane occupancy (diagnostic)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -117,6 +118,9 @@ def main():
     d_tiles = torch.tensor(mine, dtype=torch.int32, device=dev).reshape(-1, 2).contiguous()
     packed = torch.zeros((per_rank, TILE, TILE, 4), dtype=torch.float32, device=dev)
     counters = torch.zeros(6, dtype=torch.int64, device=dev)
+    dbg = torch.zeros(8, dtype=torch.int64, device=dev)
+    if args.occupancy:
+        lib.rt_debug_counters(dbg.data_ptr())
     gathered = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
     nx, ny = math.ceil(W / TILE), math.ceil(H / TILE)
     image = torch.empty((ny * TILE, nx * TILE, 4), dtype=torch.float32, device=dev) if rank == 0 else None
@@ -213,6 +217,11 @@ def main():
             "counters_per_step": {k: int(v) for k, v in per_step.items()},
             "cpu_baseline": cpu,
         }
+        if args.occupancy:
+            d = [int(v) for v in dbg.cpu().tolist()]
+            out["lane_occupancy"] = {name: round(d[2 * i + 1] / max(d[2 * i], 1) / 64, 4)
+                                     for i, name in enumerate(("outer", "bvh_walk", "leaf_tests", "segments"))}
+            out["wave_iterations"] = {name: d[2 * i] for i, name in enumerate(("outer", "bvh_walk", "leaf_tests", "segments"))}
         print(json.dumps(out), flush=True)
     lib.rt_dev_scene_free(scene)
     if world > 1:

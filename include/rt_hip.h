@@ -138,6 +138,12 @@ int rt_render_tiles_async(rt_dev_scene *s, const rt_camera *cam, const rt_params
 int rt_render_image_async(rt_dev_scene *s, const rt_camera *cam, const rt_params *p,
                           float *d_rgba, float *d_depth, uint64_t *d_counters, void *stream);
 
+/* ---- diagnostics ---------------------------------------------------------------------
+ * d_buf: device array of 8 uint64 (or NULL to disable).  While set, the kernels add, per
+ * wave iteration of each phase (outer work loop, BVH walk, postponed-leaf tests, ray
+ * segments), 1 and the number of lanes taking part -- a direct lane-occupancy measure. */
+int rt_debug_counters(uint64_t *d_buf);
+
 #ifdef __cplusplus
 }
 #endif

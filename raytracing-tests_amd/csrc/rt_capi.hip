@@ -22,6 +22,8 @@
 
 namespace {
 
+unsigned long long *g_dbg = nullptr;  // rt_debug_counters(): lane-occupancy diagnostics
+
 #define HIP_OK(expr)                                             \
     do {                                                         \
         hipError_t e_ = (expr);                                  \
@@ -83,6 +85,7 @@ rtk::Frame make_frame(const rt_camera *cam, const rt_params *p) {
         f.screen_dist = 1.0f / (2.0f * (float)std::tan((double)(cam->fov_y_rad * 0.5f)));
     }
     f.inv_spp = 1.0f / (float)p->spp;
+    f.dbg = g_dbg;
     return f;
 }
 
@@ -98,6 +101,12 @@ struct rt_dev_scene {
     int s_stop = 0;      // IOW-03: samples before the ring schedule's early return (== spp in practice)
     int blocks_cap = 0;  // persistent grid size: resident blocks the device can hold
     DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
+    // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
+    uint32_t ws_units = 0;
+    size_t ws_temp_bytes = 0;
+    DevBuf ws_state, ws_cost, ws_keys, ws_iota, ws_order, ws_temp;
+    // tail-compaction continuation buffers (ping-pong), blocks_cap*kBlock slots each
+    DevBuf cont[2], cont_count;
 };
 
 namespace {
@@ -116,10 +125,15 @@ int build_tables(rt_dev_scene *s, int spp) {
     for (int i = 0; i < spp; i++)
         if (ring[size_t(i) * 2] < 0) { s->s_stop = i; break; }
     HIP_OK(s->counter.alloc(64));
+    return RT_OK;
+}
+
+// Persistent grid = the blocks the device keeps resident (a work-queue kernel gains nothing
+// from more: extra blocks would only start after the queue ran dry).
+void set_residency(rt_dev_scene *s) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    s->blocks_cap = cus * 8;  // more than can be resident; late blocks find the queue empty and exit
-    return RT_OK;
+    s->blocks_cap = cus * rtk::resident_blocks_per_cu(s->kind);
 }
 
 int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n, int spp) {
@@ -134,6 +148,10 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
         for (int k = 0; k < 3; k++) { h[13 + k] = r[12 + k]; h[16 + k] = 1.0f / r[12 + k]; }
         for (int k = 0; k < 3; k++) { c[k] = r[15 + k]; c[3 + k] = r[18 + k]; }
         c[6] = r[21]; c[7] = r[22];
+        // glm::mat3(1) bit pattern (+0 off-diagonal): the kernel may reuse the ray's
+        // identity-transformed direction, which is bit-identical to transforming it here
+        static const float kI[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        h[19] = std::memcmp(r + 3, kI, sizeof(kI)) == 0 ? 1.0f : 0.0f;
     }
     s->kind = 3; s->n = n;
     HIP_OK(s->hot.upload(hot.data(), hot.size() * sizeof(float)));
@@ -157,19 +175,11 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
                 boxes[size_t(j) * 6 + 3 + k] = r[k] + e;
             }
         }
-        std::vector<float> nodes = rtamd::lbvh_build(boxes.data(), n);
-        // deepest stack the ordered walk can need = tree depth
         int depth = 0;
-        std::vector<std::pair<uint32_t, int>> st{{0u, 0}};
-        while (!st.empty()) {
-            auto [i, d] = st.back();
-            st.pop_back();
-            depth = std::max(depth, d);
-            float left = nodes[size_t(i) * 8 + 6];
-            if (left > 0.1f) { st.push_back({uint32_t(left), d + 1}); st.push_back({uint32_t(left) + 1, d + 1}); }
-        }
+        std::vector<float> nodes = rtamd::sah_build(boxes.data(), n, &depth);
         if (depth < rtk::kIowBvhStack && n < 65535) HIP_OK(s->nodes.upload(nodes.data(), nodes.size() * sizeof(float)));
     }
+    set_residency(s);
     return build_tables(s, spp);
 }
 
@@ -201,19 +211,116 @@ int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const f
     HIP_OK(s->nodes.upload(nodes, size_t(2 * n - 1) * 8 * sizeof(float)));
     if (s->n_lights) HIP_OK(s->lights.upload(lights, size_t(s->n_lights) * 7 * sizeof(float)));
     else HIP_OK(s->lights.alloc(16));
+    set_residency(s);
     return build_tables(s, spp);
 }
 
+// Sample ranges of the render.  Default: one range (tail compaction keeps the SIMDs full).
+// RT_CHUNKS=lpt: a short first chunk measures every pixel's cost and the rest run
+// longest-first (LPT) -- kept as an A/B switch; with compaction it measured slower.
+std::vector<std::pair<int, int>> chunk_plan(int spp) {
+    std::vector<std::pair<int, int>> plan;
+    const char *env = std::getenv("RT_CHUNKS");
+    if (spp <= 2 || !(env && std::strcmp(env, "lpt") == 0)) { plan.push_back({0, spp}); return plan; }
+    const int first = std::max(1, spp / 20);
+    const int step = std::max(1, (spp - first + 7) / 8);
+    plan.push_back({0, first});
+    for (int b = first; b < spp; b += step) plan.push_back({b, std::min(spp, b + step)});
+    return plan;
+}
+
+int ensure_workspace(rt_dev_scene *s, uint32_t units) {
+    if (units <= s->ws_units) return RT_OK;
+    s->ws_state.~DevBuf(); new (&s->ws_state) DevBuf();
+    s->ws_cost.~DevBuf(); new (&s->ws_cost) DevBuf();
+    s->ws_keys.~DevBuf(); new (&s->ws_keys) DevBuf();
+    s->ws_iota.~DevBuf(); new (&s->ws_iota) DevBuf();
+    s->ws_order.~DevBuf(); new (&s->ws_order) DevBuf();
+    s->ws_temp.~DevBuf(); new (&s->ws_temp) DevBuf();
+    HIP_OK(s->ws_state.alloc(size_t(units) * 32));
+    HIP_OK(s->ws_cost.alloc(size_t(units) * 4));
+    HIP_OK(s->ws_keys.alloc(size_t(units) * 4));
+    HIP_OK(s->ws_order.alloc(size_t(units) * 4));
+    std::vector<unsigned> iota(units);
+    for (uint32_t i = 0; i < units; i++) iota[i] = i;
+    HIP_OK(s->ws_iota.upload(iota.data(), size_t(units) * 4));
+    s->ws_temp_bytes = rtk::sort_temp_bytes(units);
+    HIP_OK(s->ws_temp.alloc(s->ws_temp_bytes));
+    s->ws_units = units;
+    return RT_OK;
+}
+
+int env_int(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
+int ensure_cont(rt_dev_scene *s) {
+    if (s->cont_count.p) return RT_OK;
+    const size_t slots = size_t(s->blocks_cap) * rtk::kBlock;
+    for (auto &b : s->cont) HIP_OK(b.alloc(slots * rtk::kContSlots * sizeof(float4)));
+    HIP_OK(s->cont_count.alloc(128));  // two counts 64 B apart
+    return RT_OK;
+}
+
+// Enqueue a whole render (all chunks) on `st`.  The first call for a given frame size
+// allocates the chunk workspace; later calls allocate nothing.
 int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
-    hipError_t e;
-    if (s->kind == 3) {
-        rtk::IowScene sc{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
-                         s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>()};
-        e = rtk::launch_iow03(f, sc, s->counter.as<unsigned>(), s->s_stop, s->blocks_cap, st);
-    } else {
-        rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
-                         s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>()};
-        e = rtk::launch_inw(f, sc, s->counter.as<unsigned>(), s->blocks_cap, st);
+    const std::vector<std::pair<int, int>> plan = chunk_plan(f.spp);
+    const uint32_t units = rtk::units_of(f);
+    if (plan.size() > 1) {
+        int rc = ensure_workspace(s, units);
+        if (rc != RT_OK) return rc;
+    }
+    // Each chunk runs as 1 + `rounds` launches: the pixel launch, then launches that resume the
+    // lanes the previous one parked.  Counts stay on the device (no host round trip): a resume
+    // launch with nothing parked exits at once.  Parking stops below ~one wave per SIMD, where
+    // compaction can no longer shorten the critical path; the last round never parks.
+    const int rounds = std::max(0, env_int("RT_ROUNDS", 6));
+    const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", s->blocks_cap * rtk::kBlock / 8)));
+    if (rounds > 0) {
+        int rc = ensure_cont(s);
+        if (rc != RT_OK) return rc;
+    }
+    unsigned *cnt = s->cont_count.as<unsigned>();  // [0], [16]: ping-pong counts (separate cache lines)
+    hipError_t e = hipSuccess;
+    for (size_t k = 0; k < plan.size() && e == hipSuccess; k++) {
+        rtk::Chunk ch;
+        ch.s_begin = plan[k].first;
+        ch.s_end = plan[k].second;
+        ch.final_chunk = k + 1 == plan.size();
+        ch.state = plan.size() > 1 ? s->ws_state.as<float4>() : nullptr;
+        ch.order = k > 0 ? s->ws_order.as<unsigned>() : nullptr;
+        ch.cost = ch.final_chunk ? nullptr : s->ws_cost.as<unsigned>();
+        for (int r = 0; r <= rounds && e == hipSuccess; r++) {
+            rtk::Cont ct{};
+            uint32_t n_units = units;
+            if (r > 0) {
+                ct.in = s->cont[(r - 1) & 1].as<float4>();
+                ct.in_count = cnt + 16 * ((r - 1) & 1);
+                n_units = uint32_t(s->blocks_cap) * rtk::kBlock;
+            }
+            if (r < rounds) {
+                ct.out = s->cont[r & 1].as<float4>();
+                ct.out_count = cnt + 16 * (r & 1);
+                ct.park_min = park_min;
+                e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), st);
+                if (e != hipSuccess) break;
+            }
+            if (s->kind == 3) {
+                rtk::IowScene sc{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
+                                 s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>()};
+                e = rtk::launch_iow03(f, sc, ch, ct, n_units, s->counter.as<unsigned>(), s->s_stop, s->blocks_cap, st);
+            } else {
+                rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
+                                 s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>()};
+                e = rtk::launch_inw(f, sc, ch, ct, n_units, s->counter.as<unsigned>(), s->blocks_cap, st);
+            }
+        }
+        if (e == hipSuccess && !ch.final_chunk)
+            e = rtk::sort_units_by_cost(s->ws_cost.as<unsigned>(), s->ws_keys.as<unsigned>(),
+                                        s->ws_iota.as<unsigned>(), s->ws_order.as<unsigned>(), units,
+                                        s->ws_temp.p, s->ws_temp_bytes, st);
     }
     if (e != hipSuccess) {
         std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
@@ -276,6 +383,13 @@ bool inw_textured(const float *geom, uint32_t n, int layout) {
 extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+// Diagnostics (not part of the reference's surface): pass a device buffer of 8 u64 to make
+// the kernels tally lane occupancy per phase; NULL turns it off.
+int rt_debug_counters(uint64_t *d_buf) {
+    g_dbg = reinterpret_cast<unsigned long long *>(d_buf);
+    return RT_OK;
+}
 
 int rt_device_info(int device, char *name_out, int name_cap, int *cu_count) {
     int rc = check_device(device);

@@ -271,6 +271,84 @@ std::vector<float> lbvh_build(const float *aabbs, uint32_t n) {
     return out;
 }
 
+// ----------------------------------------------------------------------------- SAH BVH
+namespace {
+struct Box {
+    float mn[3] = {1e30f, 1e30f, 1e30f}, mx[3] = {-1e30f, -1e30f, -1e30f};
+    void grow(const Box &b) { for (int a = 0; a < 3; a++) { mn[a] = std::fmin(mn[a], b.mn[a]); mx[a] = std::fmax(mx[a], b.mx[a]); } }
+    float area() const {
+        float d[3];
+        for (int a = 0; a < 3; a++) d[a] = std::fmax(mx[a] - mn[a], 0.0f);
+        return d[0] * d[1] + d[1] * d[2] + d[2] * d[0];
+    }
+};
+struct SahBuilder {
+    std::vector<Box> prim;
+    std::vector<float> cen;  // 3 per prim
+    std::vector<uint32_t> ids;
+    std::vector<float> out;  // 8 floats per node
+    uint32_t next = 1;
+    int depth = 0;
+    void node(uint32_t at, uint32_t parent, uint32_t lo, uint32_t hi, int d) {
+        depth = std::max(depth, d);
+        Box b;
+        for (uint32_t i = lo; i < hi; i++) b.grow(prim[ids[i]]);
+        float *o = out.data() + size_t(at) * 8;
+        for (int a = 0; a < 3; a++) { o[a] = b.mn[a]; o[3 + a] = b.mx[a]; }
+        o[7] = float(parent);
+        const uint32_t cnt = hi - lo;
+        if (cnt == 1) { o[6] = -float(ids[lo]); return; }
+        // full sweep SAH over the three axes (N is small: hundreds to thousands)
+        float best = 1e38f;
+        int best_axis = 0;
+        uint32_t best_split = lo + cnt / 2;
+        std::vector<float> right_area(cnt);
+        for (int a = 0; a < 3; a++) {
+            std::sort(ids.begin() + lo, ids.begin() + hi, [&](uint32_t x, uint32_t y) {
+                return cen[3 * x + a] < cen[3 * y + a] || (cen[3 * x + a] == cen[3 * y + a] && x < y);
+            });
+            Box r;
+            for (uint32_t i = hi; i-- > lo + 1;) { r.grow(prim[ids[i]]); right_area[i - lo] = r.area(); }
+            Box l;
+            for (uint32_t i = lo; i + 1 < hi; i++) {
+                l.grow(prim[ids[i]]);
+                const uint32_t nl = i + 1 - lo, nr = hi - i - 1;
+                const float c = l.area() * float(nl) + right_area[i + 1 - lo] * float(nr);
+                if (c < best) { best = c; best_axis = a; best_split = i + 1; }
+            }
+        }
+        std::sort(ids.begin() + lo, ids.begin() + hi, [&](uint32_t x, uint32_t y) {
+            return cen[3 * x + best_axis] < cen[3 * y + best_axis] ||
+                   (cen[3 * x + best_axis] == cen[3 * y + best_axis] && x < y);
+        });
+        const uint32_t c0 = next;
+        next += 2;
+        o[6] = float(c0);
+        node(c0, at, lo, best_split, d + 1);
+        node(c0 + 1, at, best_split, hi, d + 1);
+    }
+};
+}  // namespace
+
+std::vector<float> sah_build(const float *aabbs, uint32_t n, int *depth) {
+    SahBuilder b;
+    b.prim.resize(n);
+    b.cen.resize(size_t(n) * 3);
+    b.ids.resize(n);
+    for (uint32_t i = 0; i < n; i++) {
+        for (int a = 0; a < 3; a++) {
+            b.prim[i].mn[a] = aabbs[size_t(i) * 6 + a];
+            b.prim[i].mx[a] = aabbs[size_t(i) * 6 + 3 + a];
+            b.cen[3 * i + a] = 0.5f * (b.prim[i].mn[a] + b.prim[i].mx[a]);
+        }
+        b.ids[i] = i;
+    }
+    b.out.assign(size_t(2 * n - 1) * 8, 0.0f);
+    b.node(0, 0, 0, n, 0);
+    if (depth) *depth = b.depth;
+    return b.out;
+}
+
 // ------------------------------------------------------------------------------- camera
 Vec3 front_from_pitch_yaw(float pitch, float yaw, bool normalize) {
     Vec3 f;

@@ -96,6 +96,11 @@ GeometryData04 to_inw04(const rt_geom_desc &d);
 // aabbs: N x (min xyz, max xyz).  Returns (2N-1) x 8 floats in the reference's BFS layout.
 std::vector<float> lbvh_build(const float *aabbs, uint32_t n);
 
+// Binned-SAH BVH over boxes (acceleration structure for IOW-03's closest-hit search; the
+// reference has none there).  Same node layout as the LBVH (children contiguous, leftData
+// = first child or -objectID, rightData = parent).  *depth receives the tree depth.
+std::vector<float> sah_build(const float *aabbs, uint32_t n, int *depth);
+
 // ---- camera (materials.cpp:321-328, base.h:274-281) ------------------------------------
 Vec3 front_from_pitch_yaw(float pitch_deg, float yaw_deg, bool normalize);
 

@@ -17,7 +17,6 @@
 
 namespace rtk {
 
-constexpr int kBlock = 256;
 
 // ----------------------------------------------------------------------- pixel mapping
 struct Pix { int x, y; bool in_image; size_t out; bool valid; };
@@ -47,9 +46,22 @@ __device__ __forceinline__ Pix map_pixel(const Frame &f) {
     return p;
 }
 
-struct Ctr { uint32_t seg = 0, nodes = 0, prims = 0, shadow = 0, drops = 0, nans = 0; };
+struct Ctr {
+    uint32_t seg = 0, nodes = 0, prims = 0, shadow = 0, drops = 0, nans = 0;
+    unsigned long long dbg[kDbgSlots] = {0, 0, 0, 0, 0, 0, 0, 0};  // wave-uniform tallies
+};
+// count one wave-iteration of a phase and how many lanes take part (diagnostic builds only)
+#define DBG_TALLY(f, c, slot, pred)                                                   \
+    do {                                                                              \
+        if ((f).dbg) {                                                                \
+            const unsigned long long m_ = __ballot(pred);                             \
+            (c).dbg[slot] += 1; (c).dbg[(slot) + 1] += (unsigned long long)__popcll(m_); \
+        }                                                                             \
+    } while (0)
 
 __device__ __forceinline__ void flush(const Frame &f, const Ctr &c) {
+    if (f.dbg && (threadIdx.x & 63) == 0)
+        for (int i = 0; i < kDbgSlots; i++) atomicAdd(f.dbg + i, c.dbg[i]);  // wave-uniform values
     if (!f.counters) return;
     unsigned long long v[6] = {c.seg, c.nodes, c.prims, c.shadow, c.drops, c.nans};
 #pragma unroll
@@ -128,18 +140,25 @@ __device__ __forceinline__ bool cull_slab(float4 n0, float4 n1, f3 o, f3 id, flo
 // walk visits a superset of the objects that can attain that minimum and applies the same
 // (t, index) rule, so it returns the same object and the same t bits.  The closest hit's
 // normal and attributes are evaluated once after the search from the winning object.
-__device__ RayRet iow_launch_ray(const IowScene &S, f3 go, f3 gd, float max_t, float contrib, Ctr &c,
-                                 unsigned short *bstk) {
+__device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 gd, float max_t, float contrib,
+                                 Ctr &c, unsigned short *bstk) {
     float min_t = max_t;
     int best = -1;
     f3 best_to = f3{0, 0, 0}, best_nd = f3{0, 0, 0}, best_td = f3{0, 0, 0};
     c.seg++;
+    // Objects whose matrix is glm::mat3(1) transform the direction identically, so M*gd and
+    // normalize(M*gd) are evaluated once per ray (same operations, same bits: 1*x folds to x,
+    // the 0*y terms are kept because IEEE forbids folding them).
+    const m3 I = m3{f3{1.0f, 0.0f, 0.0f}, f3{0.0f, 1.0f, 0.0f}, f3{0.0f, 0.0f, 1.0f}};
+    const f3 td_id = mul(I, gd);
+    const f3 nd_id = normalize(td_id);
     auto test = [&](int j) {
         c.prims++;
-        const IowObj ob = iow_obj(S.hot + (size_t)j * kIowHot);
-        f3 to = mul(ob.M, go - ob.pos);
-        f3 td = mul(ob.M, gd);
-        f3 nd = normalize(td);
+        const float *h = S.hot + (size_t)j * kIowHot;
+        const IowObj ob = iow_obj(h);
+        f3 to, td, nd;
+        if (h[19] != 0.0f) { to = mul(I, go - ob.pos); td = td_id; nd = nd_id; }
+        else { to = mul(ob.M, go - ob.pos); td = mul(ob.M, gd); nd = normalize(td); }
         float t = -1.0f;
         if (ob.type == 2) t = t_ellipsoid(to, nd, ob.is);
         else if (ob.type == 1) t = t_cuboid(to, nd, ob.scale);
@@ -148,33 +167,50 @@ __device__ RayRet iow_launch_ray(const IowScene &S, f3 go, f3 gd, float max_t, f
         }
     };
     const float dl2 = dot(gd, gd);
-    if (S.nodes != nullptr && dl2 > 0.998f && dl2 < 1.002f) {
+    if (!(dl2 > 0.0f)) {
+        // zero or NaN direction (the TIR branch pushes the uninitialised reflection_dirn,
+        // 03...glsl:331-332): normalize(M*gd) is NaN for every object, so every t is -1 and
+        // the reference's loop finds no hit -- skip it.
+        c.prims += S.n;
+    } else if (S.nodes != nullptr && dl2 > 0.998f && dl2 < 1.002f) {
+        // Ordered walk with postponed leaves (speculative traversal): a lane that reaches a
+        // leaf parks it and keeps walking inner nodes; primitive tests run when every lane
+        // of the wave holds one (or has finished), so they execute with full lanes.
         const f3 id = f3{__builtin_amdgcn_rcpf(gd.x), __builtin_amdgcn_rcpf(gd.y), __builtin_amdgcn_rcpf(gd.z)};
-        int sp = 0, cur = 0;
+        int sp = 0, cur = 0, pend = -1;
+        bool walking = true;
         for (;;) {
-            const float4 n1 = S.nodes[2 * cur + 1];
-            if (n1.z > 0.1f) {
-                const int L = (int)n1.z;
-                const float4 a0 = S.nodes[2 * L], a1 = S.nodes[2 * L + 1];
-                const float4 b0 = S.nodes[2 * L + 2], b1 = S.nodes[2 * L + 3];
-                c.nodes += 2;
-                const float lim = min_t * 1.0001f + 1e-3f;
-                float ta, tb;
-                const bool ha = cull_slab(a0, a1, go, id, lim, ta);
-                const bool hb = cull_slab(b0, b1, go, id, lim, tb);
-                if (ha && hb) {
-                    const bool a_first = ta <= tb;
-                    bstk[(sp++) * kBlock] = (unsigned short)(a_first ? L + 1 : L);
-                    cur = a_first ? L : L + 1;
-                    continue;
+            DBG_TALLY(F_, c, kDbgTrav, walking);
+            if (walking) {
+                const float4 n1 = S.nodes[2 * cur + 1];
+                if (n1.z > 0.1f) {
+                    const int L = (int)n1.z;
+                    const float4 a0 = S.nodes[2 * L], a1 = S.nodes[2 * L + 1];
+                    const float4 b0 = S.nodes[2 * L + 2], b1 = S.nodes[2 * L + 3];
+                    c.nodes += 2;
+                    const float lim = min_t * 1.0001f + 1e-3f;
+                    float ta, tb;
+                    const bool ha = cull_slab(a0, a1, go, id, lim, ta);
+                    const bool hb = cull_slab(b0, b1, go, id, lim, tb);
+                    if (ha && hb) {
+                        const bool a_first = ta <= tb;
+                        bstk[(sp++) * kBlock] = (unsigned short)(a_first ? L + 1 : L);
+                        cur = a_first ? L : L + 1;
+                    } else if (ha) cur = L;
+                    else if (hb) cur = L + 1;
+                    else if (sp == 0) walking = false;
+                    else cur = bstk[(--sp) * kBlock];
+                } else if (pend < 0) {
+                    pend = (int)(-n1.z);
+                    if (sp == 0) walking = false;
+                    else cur = bstk[(--sp) * kBlock];
                 }
-                if (ha) { cur = L; continue; }
-                if (hb) { cur = L + 1; continue; }
-            } else {
-                test((int)(-n1.z));
             }
-            if (sp == 0) break;
-            cur = bstk[(--sp) * kBlock];
+            if (__all(!walking || pend >= 0)) {
+                DBG_TALLY(F_, c, kDbgLeaf, pend >= 0);
+                if (pend >= 0) { test(pend); pend = -1; }
+                if (__all(!walking)) break;
+            }
         }
     } else {
         for (uint32_t j = 0; j < S.n; j++) test((int)j);  // also the path for zero / NaN directions
@@ -256,7 +292,7 @@ __device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, I
     f3 co = mk(K.at(e, 0), K.at(e, 1), K.at(e, 2)), cd = mk(K.at(e, 3), K.at(e, 4), K.at(e, 5));
     float contribution = K.at(e, 6), ri = K.at(e, 7);
     int bounced = (int)K.at(e, 8);
-    RayRet data = iow_launch_ray(S, co, cd, 32000.0f, contribution, c, bstk);
+    RayRet data = iow_launch_ray(S, F, co, cd, 32000.0f, contribution, c, bstk);
     const bool hit = dot(data.normal, data.normal) > 0.9f;
     sample = sample + (hit ? data.color : background(cd, false)) * contribution;
     if (bounced < F.max_bounces && hit) {
@@ -367,14 +403,30 @@ __device__ __forceinline__ void iow_camera_ray(const IowScene &S, const Frame &f
     rd = normalize((ld * f.screen_dist + r_ * (sx + dsx * (float)ix)) + u_ * (sy + dsy * (float)iy));
 }
 
-__global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, unsigned *counter, int s_stop) {
+// wave-aggregated slot allocation for parking (same ballot / popcount / rank scheme)
+__device__ __forceinline__ uint32_t park_slot(unsigned *count, bool need) {
+    const unsigned long long mask = __ballot(need);
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((long long)mask) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (unsigned)__popcll(mask));
+    base = __shfl(base, leader, 64);
+    return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+}
+__device__ __forceinline__ float ibits(int v) { return __int_as_float(v); }
+__device__ __forceinline__ float ubits(uint32_t v) { return __uint_as_float(v); }
+
+__global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, Chunk ch, Cont ct, unsigned *counter,
+                                                  int s_stop) {
     __shared__ float lds[kIowStack * kIowSlot * kBlock];
     __shared__ unsigned short lds_bvh[kIowBvhStack * kBlock];
     unsigned short *bstk = lds_bvh + threadIdx.x;
     Ctr c;
     IowStack K{lds + threadIdx.x, 0};
-    const uint32_t total = units_total(f);
+    const uint32_t total = ct.in ? *ct.in_count : units_total(f);
+    const bool may_park = ct.out != nullptr && total >= ct.park_min;
     const int W = f.W, H = f.H, spp = f.spp;
+    const int s_end = ch.s_end < s_stop ? ch.s_end : s_stop;
     int grid = 1;
     while (grid * grid < spp) grid++;
     const float aspect = (float)W * rcp((float)H);
@@ -383,47 +435,97 @@ __global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, unsigned 
     bool live = true;     // lane may still find work
     bool busy = false;    // lane owns a pixel
     UnitPix px{};
+    uint32_t unit = 0, urays = 0;
     float sx = 0, sy = 0;
     f3 fc = f3{0, 0, 0}, sample = f3{0, 0, 0};
     int s = 0, skip = 0;
     for (;;) {
-        const uint32_t u = fetch_unit(counter, live && !busy);
+        const uint32_t q = fetch_unit(counter, live && !busy);
         if (live && !busy) {
-            if (u >= total) live = false;
-            else {
-                px = unit_pixel(f, u);
-                if (!px.in_image) write_px(f, px, f3{0, 0, 0}, 0.0f);
-                else {
+            if (q >= total) live = false;
+            else if (ct.in) {  // resume a parked lane
+                const float4 *p = ct.in + (size_t)q * kContSlots;
+                const float4 m = p[0], a = p[1], b = p[2];
+                unit = __float_as_uint(m.x); s = __float_as_int(m.y); skip = __float_as_int(m.z);
+                K.size = __float_as_int(m.w);
+                fc = f3{a.x, a.y, a.z}; urays = __float_as_uint(a.w);
+                sample = f3{b.x, b.y, b.z};
+                const float *fl = reinterpret_cast<const float *>(p + 3);
+                for (int k = 0; k < kIowStack * kIowSlot; k++) K.base[k * kBlock] = fl[k];
+                px = unit_pixel(f, unit);
+                sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
+                sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
+                busy = true;
+            } else {
+                unit = ch.order ? ch.order[q] : q;
+                px = unit_pixel(f, unit);
+                if (!px.in_image) {
+                    if (ch.final_chunk) write_px(f, px, f3{0, 0, 0}, 0.0f);
+                    if (ch.cost) ch.cost[unit] = 0;
+                } else {
                     busy = true;
-                    for (int e = 0; e < kIowStack; e++) K.at(e, 7) = 0.0f;  // stale RI slots start at 0
                     sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
                     sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
-                    fc = f3{0, 0, 0};
-                    s = 0;
+                    s = ch.s_begin;
                     K.size = 0;
+                    urays = 0;
+                    if (s == 0) {
+                        fc = f3{0, 0, 0};
+                        for (int e = 0; e < kIowStack; e++) K.at(e, 7) = 0.0f;  // stale RI slots start at 0
+                    } else {  // resume the pixel where the previous chunk parked it
+                        const float4 a0 = ch.state[2 * (size_t)unit], a1 = ch.state[2 * (size_t)unit + 1];
+                        fc = f3{a0.x, a0.y, a0.z};
+                        K.at(0, 7) = a1.x; K.at(1, 7) = a1.y; K.at(2, 7) = a1.z; K.at(3, 7) = a1.w;
+                    }
                 }
             }
         }
         if (__ballot(live) == 0) break;
+        if (may_park && __ballot(!live) != 0 && __popcll(__ballot(busy)) < kParkBelow) {
+            // queue drained and the wave is under half busy: park the busy lanes, free the SIMD
+            const uint32_t slot = park_slot(ct.out_count, busy);
+            if (busy) {
+                float4 *p = ct.out + (size_t)slot * kContSlots;
+                p[0] = make_float4(ubits(unit), ibits(s), ibits(skip), ibits(K.size));
+                p[1] = make_float4(fc.x, fc.y, fc.z, ubits(urays));
+                p[2] = make_float4(sample.x, sample.y, sample.z, 0.0f);
+                float *fl = reinterpret_cast<float *>(p + 3);
+                for (int k = 0; k < kIowStack * kIowSlot; k++) fl[k] = K.base[k * kBlock];
+            }
+            break;
+        }
+        DBG_TALLY(f, c, kDbgOuter, busy);
         if (!busy) continue;
-        if (K.size == 0) {  // start sample s
+        if (K.size == 0 && s < s_end) {  // start sample s
             f3 ro, rd;
             iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
             if (f.show_normal) {
-                fc = fc + iow_launch_ray(S, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
+                fc = fc + iow_launch_ray(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
                 s++;
+                urays++;
             } else {
                 K.push(ro, rd, 1.0f, 1.0f, 0, c);
                 sample = f3{0, 0, 0};
                 skip = 0;
             }
         }
+        DBG_TALLY(f, c, kDbgSeg, K.size > 0);
         if (K.size > 0) {
             iow_segment(S, f, K, skip, sample, s, c, bstk);
+            urays++;
             if (K.size == 0) { fc = fc + sample; s++; }
         }
-        if (K.size == 0 && s >= s_stop) {
-            write_px(f, px, fc * rcp((float)s_stop), 0.0f);
+        if (K.size == 0 && s >= s_end) {
+            if (s_end >= s_stop) {
+                if (ch.final_chunk) write_px(f, px, fc * rcp((float)s_stop), 0.0f);
+                else if (ch.state) {  // early-return pixels: keep the final colour for the last launch
+                    ch.state[2 * (size_t)unit] = make_float4(fc.x, fc.y, fc.z, 0.0f);
+                }
+            } else if (ch.state) {
+                ch.state[2 * (size_t)unit] = make_float4(fc.x, fc.y, fc.z, 0.0f);
+                ch.state[2 * (size_t)unit + 1] = make_float4(K.at(0, 7), K.at(1, 7), K.at(2, 7), K.at(3, 7));
+            }
+            if (ch.cost) ch.cost[unit] = urays;
             busy = false;
         }
     }
@@ -692,39 +794,84 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
 }
 
 template <bool LIGHTS>
-__global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S, unsigned *counter) {
+__global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S, Chunk ch, Cont ct, unsigned *counter) {
     __shared__ float lds[kFStack * kBlock];
     Ctr c;
     FStack K{lds + threadIdx.x, 0};
-    const uint32_t total = units_total(f);
+    const uint32_t total = ct.in ? *ct.in_count : units_total(f);
+    const bool may_park = ct.out != nullptr && total >= ct.park_min;
+    const int s_end = ch.s_end < f.spp ? ch.s_end : f.spp;
     bool live = true, busy = false;
     UnitPix px{};
+    uint32_t unit = 0, urays = 0;
     f3 acc = f3{0, 0, 0}, col = f3{0, 0, 0};
     float dmid = 0.0f, dep = 0.0f;
     int s = 0;
     K.size = 0;
     for (;;) {
-        const uint32_t u = fetch_unit(counter, live && !busy);
+        const uint32_t q = fetch_unit(counter, live && !busy);
         if (live && !busy) {
-            if (u >= total) live = false;
-            else {
-                px = unit_pixel(f, u);
-                if (!px.in_image) write_px(f, px, f3{0, 0, 0}, 0.0f);
-                else { busy = true; s = 0; acc = f3{0, 0, 0}; dmid = 0.0f; K.size = 0; }
+            if (q >= total) live = false;
+            else if (ct.in) {  // resume a parked lane
+                const float4 *p = ct.in + (size_t)q * kContSlots;
+                const float4 m = p[0], a = p[1], b = p[2];
+                unit = __float_as_uint(m.x); s = __float_as_int(m.y); K.size = __float_as_uint(m.z);
+                urays = __float_as_uint(m.w);
+                acc = f3{a.x, a.y, a.z}; dmid = a.w;
+                col = f3{b.x, b.y, b.z}; dep = b.w;
+                const float *fl = reinterpret_cast<const float *>(p + 3);
+                for (int k = 0; k < kFStack; k++) K.base[k * kBlock] = fl[k];
+                px = unit_pixel(f, unit);
+                busy = true;
+            } else {
+                unit = ch.order ? ch.order[q] : q;
+                px = unit_pixel(f, unit);
+                if (!px.in_image) {
+                    if (ch.final_chunk) write_px(f, px, f3{0, 0, 0}, 0.0f);
+                    if (ch.cost) ch.cost[unit] = 0;
+                } else {
+                    busy = true;
+                    s = ch.s_begin;
+                    K.size = 0;
+                    urays = 0;
+                    if (s == 0) { acc = f3{0, 0, 0}; dmid = 0.0f; }
+                    else {
+                        const float4 a0 = ch.state[2 * (size_t)unit];
+                        acc = f3{a0.x, a0.y, a0.z};
+                        dmid = a0.w;
+                    }
+                }
             }
         }
         if (__ballot(live) == 0) break;
+        if (may_park && __ballot(!live) != 0 && __popcll(__ballot(busy)) < kParkBelow) {
+            const uint32_t slot = park_slot(ct.out_count, busy);
+            if (busy) {
+                float4 *p = ct.out + (size_t)slot * kContSlots;
+                p[0] = make_float4(ubits(unit), ibits(s), ubits(K.size), ubits(urays));
+                p[1] = make_float4(acc.x, acc.y, acc.z, dmid);
+                p[2] = make_float4(col.x, col.y, col.z, dep);
+                float *fl = reinterpret_cast<float *>(p + 3);
+                for (int k = 0; k < kFStack; k++) fl[k] = K.base[k * kBlock];
+            }
+            break;
+        }
+        DBG_TALLY(f, c, kDbgOuter, busy);
         if (!busy) continue;
         // one ray segment per iteration (samples of a pixel are independent invocations)
         if (K.size == 0) { inw_start_sample(S, f, K, px.x, px.y, s, c); col = f3{0, 0, 0}; dep = 0.0f; }
+        DBG_TALLY(f, c, kDbgSeg, true);
         inw_segment<LIGHTS>(S, f, K, s, col, dep, c);
+        urays++;
         if (K.size == 0) {  // sample done: End() accumulates sqrt(colour) in sample order
             f3 g = f3{__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z)};
             acc = (s == 0) ? g : acc + g;
             if (s == f.spp / 2) dmid = dep;
             s++;
-            if (s >= f.spp) {
-                write_px(f, px, acc * rcp((float)f.spp), dmid);
+            if (s >= s_end) {
+                if (ch.final_chunk) write_px(f, px, acc * rcp((float)f.spp), dmid);
+                else ch.state[2 * (size_t)unit] = make_float4(acc.x, acc.y, acc.z, dmid);
+                if (ch.cost) ch.cost[unit] = urays;
                 busy = false;
             }
         }
@@ -733,10 +880,12 @@ __global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S, unsigned *c
 }
 
 // ============================================================================ launch
-static unsigned grid_of(const Frame &f, int blocks_cap) {
-    const uint64_t units = f.tiles ? (uint64_t)f.n_tiles * f.tile_size * f.tile_size
-                                   : (uint64_t)(((f.tw + 7) >> 3) * ((f.th + 7) >> 3)) * 64u;
-    uint64_t b = (units + kBlock - 1) / kBlock;
+uint32_t units_of(const Frame &f) {
+    return f.tiles ? (uint32_t)f.n_tiles * f.tile_size * f.tile_size
+                   : (uint32_t)(((f.tw + 7) >> 3) * ((f.th + 7) >> 3)) * 64u;
+}
+static unsigned grid_of(uint32_t units, int blocks_cap) {
+    uint64_t b = ((uint64_t)units + kBlock - 1) / kBlock;
     if (b > (uint64_t)blocks_cap) b = blocks_cap;
     return (unsigned)(b ? b : 1);
 }
@@ -745,22 +894,33 @@ static dim3 grid_iow01(const Frame &f) {
     return dim3((unsigned)(((f.tw + 15) >> 4) * ((f.th + 15) >> 4)));
 }
 
+int resident_blocks_per_cu(int kind) {
+    int nb = 0;
+    hipError_t e;
+    if (kind == 3) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03, kBlock, 0);
+    else if (kind == 14) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<true>, kBlock, 0);
+    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<false>, kBlock, 0);
+    return (e == hipSuccess && nb > 0) ? nb : 2;
+}
+
 hipError_t launch_iow01(const Frame &f, hipStream_t s) {
     hipLaunchKernelGGL(k_iow01, grid_iow01(f), dim3(kBlock), 0, s, f);
     return hipGetLastError();
 }
-hipError_t launch_iow03(const Frame &f, const IowScene &sc, unsigned *counter, int s_stop, int blocks_cap,
-                        hipStream_t s) {
+hipError_t launch_iow03(const Frame &f, const IowScene &sc, const Chunk &ch, const Cont &ct, uint32_t n_units,
+                        unsigned *counter, int s_stop, int blocks_cap, hipStream_t s) {
     hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_iow03, dim3(grid_of(f, blocks_cap)), dim3(kBlock), 0, s, f, sc, counter, s_stop);
+    hipLaunchKernelGGL(k_iow03, dim3(grid_of(n_units, blocks_cap)), dim3(kBlock), 0, s, f, sc, ch, ct, counter, s_stop);
     return hipGetLastError();
 }
-hipError_t launch_inw(const Frame &f, const InwScene &sc, unsigned *counter, int blocks_cap, hipStream_t s) {
+hipError_t launch_inw(const Frame &f, const InwScene &sc, const Chunk &ch, const Cont &ct, uint32_t n_units,
+                      unsigned *counter, int blocks_cap, hipStream_t s) {
     hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    if (sc.layout == 4) hipLaunchKernelGGL(k_inw<true>, dim3(grid_of(f, blocks_cap)), dim3(kBlock), 0, s, f, sc, counter);
-    else hipLaunchKernelGGL(k_inw<false>, dim3(grid_of(f, blocks_cap)), dim3(kBlock), 0, s, f, sc, counter);
+    const dim3 g(grid_of(n_units, blocks_cap));
+    if (sc.layout == 4) hipLaunchKernelGGL(k_inw<true>, g, dim3(kBlock), 0, s, f, sc, ch, ct, counter);
+    else hipLaunchKernelGGL(k_inw<false>, g, dim3(kBlock), 0, s, f, sc, ch, ct, counter);
     return hipGetLastError();
 }
 

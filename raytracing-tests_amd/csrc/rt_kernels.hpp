@@ -19,7 +19,11 @@ struct Frame {
     float pos[3], dir[3];
     float aperture, focus, screen_dist, inv_spp;
     float sphere[4];    // IOW-01 only
+    unsigned long long *dbg;  // optional lane-occupancy counters (kDbg* slots), null in production
 };
+// lane-occupancy counters (per wave-iteration: 1 and popcount of the participating lanes)
+enum { kDbgOuter = 0, kDbgOuterLanes, kDbgTrav, kDbgTravLanes, kDbgLeaf, kDbgLeafLanes, kDbgSeg, kDbgSegLanes,
+       kDbgSlots = 8 };
 
 // IOW-03 device scene: "hot" records walked by the linear loop + "cold" hit attributes.
 constexpr int kIowHot = 20;   // pos3 type M9 scale3 inv_scale3 pad
@@ -47,11 +51,49 @@ struct InwScene {
     const float *sunflower;  // spp*2
 };
 
+// One launch of a chunked render: samples [s_begin, s_end) of every pixel unit.  A pixel's
+// samples must run in order (IOW-03 reads stale stack slots of earlier samples), so the
+// per-pixel state (accumulator + the IOW stack's RI slots) is parked in `state` between
+// launches, `cost` records the rays each unit spent, and `order` (a permutation of unit ids,
+// longest first) lets the next launch schedule the expensive pixels first.
+struct Chunk {
+    int s_begin, s_end;      // sample range of this launch
+    int final_chunk;         // write the image (else park the state)
+    float4 *state;           // 2 float4 per unit (may be null for a single-chunk render)
+    const unsigned *order;   // unit permutation or null (natural order)
+    unsigned *cost;          // rays per unit in this launch, or null
+};
+
+// Tail compaction between launches.  Once the work queue is empty, a wave whose busy lanes
+// fall below kParkBelow parks them (state at a ray-segment boundary) in `out`, slot ids from
+// a wave-aggregated atomic on `out_count`, and exits; the next launch resumes the parked
+// lanes from `in` in full waves.  in == null: the launch's units are pixels.  out == null or
+// fewer than park_min units in the launch: lanes run to completion (the final round).
+constexpr int kBlock = 256;      // threads per block of every render kernel
+constexpr int kParkBelow = 32;    // park when fewer than half the wave's lanes are busy
+constexpr int kContSlots = 13;    // float4 per parked lane
+struct Cont {
+    const float4 *in;
+    const unsigned *in_count;
+    float4 *out;
+    unsigned *out_count;
+    uint32_t park_min;
+};
+
 hipError_t launch_iow01(const Frame &f, hipStream_t s);
 // Persistent work-queue launches: `counter` (one u32, device) is zeroed on `s` before the
 // kernel; at most `blocks_cap` blocks are launched (they pull pixels until none are left).
-hipError_t launch_iow03(const Frame &f, const IowScene &sc, unsigned *counter, int s_stop, int blocks_cap,
-                        hipStream_t s);
-hipError_t launch_inw(const Frame &f, const InwScene &sc, unsigned *counter, int blocks_cap, hipStream_t s);
+// n_units: pixel units (cont.in == null) or parked lanes to resume (host-known count)
+hipError_t launch_iow03(const Frame &f, const IowScene &sc, const Chunk &ch, const Cont &ct, uint32_t n_units,
+                        unsigned *counter, int s_stop, int blocks_cap, hipStream_t s);
+hipError_t launch_inw(const Frame &f, const InwScene &sc, const Chunk &ch, const Cont &ct, uint32_t n_units,
+                      unsigned *counter, int blocks_cap, hipStream_t s);
+uint32_t units_of(const Frame &f);
+// resident 256-thread blocks per CU for the persistent kernels (occupancy query)
+int resident_blocks_per_cu(int kind);
+// order[i] = unit ids sorted by cost, most expensive first (hipcub radix sort)
+hipError_t sort_units_by_cost(const unsigned *cost, unsigned *keys_tmp, const unsigned *iota, unsigned *order,
+                              uint32_t n, void *temp, size_t temp_bytes, hipStream_t s);
+size_t sort_temp_bytes(uint32_t n);
 
 }  // namespace rtk

@@ -90,6 +90,7 @@ SIGNATURES = {
     "rt_pack_iow03": (C.c_int, [C.POINTER(RtGeomDesc), C.c_uint32, _FP, _FP]),
     "rt_pack_inw": (C.c_int, [C.POINTER(RtGeomDesc), C.c_uint32, C.c_int, _FP, _FP, _FP, _U32P]),
     "rt_sample_tables": (C.c_int, [C.c_int, _FP, _FP, _IP]),
+    "rt_debug_counters": (C.c_int, [C.c_void_p]),
 }
 
 _lib = None
