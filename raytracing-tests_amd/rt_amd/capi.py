@@ -21,6 +21,8 @@ RT_STAGE_IOW01, RT_STAGE_IOW03, RT_STAGE_INW01, RT_STAGE_INW04 = 1, 3, 11, 14
 RT_IOW_CUBOID, RT_IOW_ELLIPSOID = 1, 2
 RT_INW_ELLIPSOID, RT_INW_CUBOID = 1, 2
 
+ABI_VERSION = 1  # RT_ABI_VERSION, include/rt_hip.h
+
 PRESET_IOW03_REF3 = 1
 PRESET_IOW03_FINAL = 2
 PRESET_INW01_GRID = 3

@@ -1,0 +1,78 @@
+"""Multi-GPU partition + exchange, rehearsed on the CPU with gloo (world size 2 and 3).
+
+bench.py deals 64x64 tiles round-robin to ranks, each rank packs its tiles, one gather brings
+them to rank 0, and rank 0 assembles the frame.  Here every rank "renders" a
+deterministic per-pixel pattern into its packed tiles; the assembled frame must equal the
+pattern everywhere, and the tile lists must cover every tile exactly once.
+"""
+import math
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+
+
+def _pattern(W, H):
+    y, x = torch.meshgrid(torch.arange(H, dtype=torch.float32), torch.arange(W, dtype=torch.float32), indexing="ij")
+    return torch.stack([x, y, x * 1000 + y, torch.ones_like(x)], -1)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, W, H, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        allt, mine, per_rank = bench.tiles_for_rank(W, H, world, rank)
+        T = bench.TILE
+        ref = _pattern(W, H)
+        packed = torch.zeros((per_rank, T, T, 4))
+        for k, (tx, ty) in enumerate(mine):  # what rt_render_tiles_async writes: 0 outside the image
+            y0, x0 = ty * T, tx * T
+            blk = ref[y0:y0 + T, x0:x0 + T]
+            packed[k, :blk.shape[0], :blk.shape[1]] = blk
+        gathered = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
+        dist.gather(packed, gathered, dst=0)
+        if rank == 0:
+            nx, ny = math.ceil(W / T), math.ceil(H / T)
+            img = bench.assemble_frame(torch.stack(gathered, 0), len(allt), nx, ny)[:H, :W]
+            q.put(bool(torch.equal(img, ref)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H", [(2, 1200, 800), (3, 200, 130), (2, 64, 64)])
+def test_gather_assembles_frame(world, W, H):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_tiles_cover_frame_once(world):
+    W, H = 1200, 800
+    seen = []
+    for r in range(world):
+        allt, mine, per_rank = bench.tiles_for_rank(W, H, world, r)
+        assert len(mine) <= per_rank
+        seen += mine
+    assert sorted(seen) == sorted(allt)
+    assert len(set(seen)) == len(allt) == math.ceil(W / 64) * math.ceil(H / 64)
