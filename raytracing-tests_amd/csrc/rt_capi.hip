@@ -99,7 +99,9 @@ struct rt_dev_scene {
     uint32_t n = 0, n_lights = 0;
     int layout = 0;
     int s_stop = 0;      // IOW-03: samples before the ring schedule's early return (== spp in practice)
-    int blocks_cap = 0;  // persistent grid size: resident blocks the device can hold
+    int blocks_cap = 0;  // persistent grid size: resident blocks the device can hold (max over variants)
+    int cus = 0;
+    int root_link = 0;   // IOW-03 culling BVH: leftData of the root
     DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
     uint32_t ws_units = 0;
@@ -133,7 +135,9 @@ int build_tables(rt_dev_scene *s, int spp) {
 void set_residency(rt_dev_scene *s) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    s->cus = cus;
     s->blocks_cap = cus * rtk::resident_blocks_per_cu(s->kind);
+    if (s->kind == 3) s->blocks_cap = std::max(s->blocks_cap, cus * rtk::resident_blocks_per_cu(4));
 }
 
 int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n, int spp) {
@@ -175,9 +179,14 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
                 boxes[size_t(j) * 6 + 3 + k] = r[k] + e;
             }
         }
-        int depth = 0;
-        std::vector<float> nodes = rtamd::sah_build(boxes.data(), n, &depth);
-        if (depth < rtk::kIowBvhStack && n < 65535) HIP_OK(s->nodes.upload(nodes.data(), nodes.size() * sizeof(float)));
+        int depth = 0, depth4 = 0;
+        const std::vector<float> bin = rtamd::sah_build(boxes.data(), n, &depth);
+        const std::vector<float> wide = rtamd::bvh4_collapse(bin, &depth4);
+        // links travel as int16 on the traversal stack: wide node ids < n, object ids < n
+        if (n < 16384) {
+            HIP_OK(s->nodes.upload(wide.data(), wide.size() * sizeof(float)));
+            s->root_link = 1;
+        }
     }
     set_residency(s);
     return build_tables(s, spp);
@@ -277,7 +286,9 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // launch with nothing parked exits at once.  Parking stops below ~one wave per SIMD, where
     // compaction can no longer shorten the critical path; the last round never parks.
     const int rounds = std::max(0, env_int("RT_ROUNDS", 6));
-    const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", s->blocks_cap * rtk::kBlock / 8)));
+    // grid of this frame's kernel variant
+    const int cap = s->kind == 3 ? s->cus * rtk::resident_blocks_per_cu(rtk::iow_narrow(f) ? 4 : 3) : s->blocks_cap;
+    const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
     if (rounds > 0) {
         int rc = ensure_cont(s);
         if (rc != RT_OK) return rc;
@@ -298,7 +309,7 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             if (r > 0) {
                 ct.in = s->cont[(r - 1) & 1].as<float4>();
                 ct.in_count = cnt + 16 * ((r - 1) & 1);
-                n_units = uint32_t(s->blocks_cap) * rtk::kBlock;
+                n_units = uint32_t(cap) * rtk::kBlock;
             }
             if (r < rounds) {
                 ct.out = s->cont[r & 1].as<float4>();
@@ -309,8 +320,8 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             }
             if (s->kind == 3) {
                 rtk::IowScene sc{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
-                                 s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>()};
-                e = rtk::launch_iow03(f, sc, ch, ct, n_units, s->counter.as<unsigned>(), s->s_stop, s->blocks_cap, st);
+                                 s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link};
+                e = rtk::launch_iow03(f, sc, ch, ct, n_units, s->counter.as<unsigned>(), s->s_stop, cap, st);
             } else {
                 rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
                                  s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>()};

@@ -349,6 +349,71 @@ std::vector<float> sah_build(const float *aabbs, uint32_t n, int *depth) {
     return b.out;
 }
 
+// Collapse the binary tree into 4-wide nodes: a node's children are gathered by repeatedly
+// opening the largest-area internal child until there are four (or only leaves remain).
+std::vector<float> bvh4_collapse(const std::vector<float> &bin, int *depth) {
+    auto is_leaf = [&](int i) { return !(bin[size_t(i) * 8 + 6] > 0.1f); };
+    auto first = [&](int i) { return int(bin[size_t(i) * 8 + 6]); };
+    auto area = [&](int i) {
+        const float *b = &bin[size_t(i) * 8];
+        const float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
+        return dx * dy + dy * dz + dz * dx;
+    };
+    std::vector<std::array<int, 4>> kids;  // binary node ids per wide node (-1 = empty)
+    std::vector<int> lvl;
+    std::vector<float> out;
+    struct Item { int bin, wide, level; };
+    std::vector<Item> work{{0, 0, 1}};
+    kids.push_back({-1, -1, -1, -1});
+    lvl.push_back(1);
+    int maxd = 1;
+    for (size_t w = 0; w < work.size(); w++) {
+        const Item it = work[w];
+        std::vector<int> ch{first(it.bin), first(it.bin) + 1};
+        for (;;) {
+            if (ch.size() >= 4) break;
+            int pick = -1;
+            for (size_t k = 0; k < ch.size(); k++)
+                if (!is_leaf(ch[k]) && (pick < 0 || area(ch[k]) > area(ch[size_t(pick)]))) pick = int(k);
+            if (pick < 0) break;
+            const int b = ch[size_t(pick)];
+            ch.erase(ch.begin() + pick);
+            ch.push_back(first(b));
+            ch.push_back(first(b) + 1);
+        }
+        for (size_t k = 0; k < ch.size(); k++) kids[size_t(it.wide)][k] = ch[k];
+        for (int b : ch)
+            if (!is_leaf(b)) {
+                const int id = int(kids.size());
+                kids.push_back({-1, -1, -1, -1});
+                work.push_back({b, id, it.level + 1});
+                maxd = std::max(maxd, it.level + 1);
+            }
+    }
+    // children that are internal binary nodes map to wide ids in `work` order
+    std::vector<int> wide_of(bin.size() / 8, -1);
+    for (const Item &it : work) wide_of[size_t(it.bin)] = it.wide;
+    out.assign(kids.size() * 32, 0.0f);
+    for (size_t w = 0; w < kids.size(); w++) {
+        float *o = &out[w * 32];
+        for (int k = 0; k < 4; k++) {
+            const int b = kids[w][size_t(k)];
+            if (b < 0) {  // empty slot: a far-away point box, culled by every ray
+                for (int a = 0; a < 6; a++) o[a * 4 + k] = 1e30f;
+                o[24 + k] = 1e9f;
+                continue;
+            }
+            const float *bb = &bin[size_t(b) * 8];
+            o[0 * 4 + k] = bb[0]; o[1 * 4 + k] = bb[1]; o[2 * 4 + k] = bb[2];
+            o[3 * 4 + k] = bb[3]; o[4 * 4 + k] = bb[4]; o[5 * 4 + k] = bb[5];
+            // link: wide node index + 1 (> 0) or -objectID (<= 0)
+            o[24 + k] = is_leaf(b) ? bb[6] : float(wide_of[size_t(b)] + 1);
+        }
+    }
+    if (depth) *depth = maxd;
+    return out;
+}
+
 // ------------------------------------------------------------------------------- camera
 Vec3 front_from_pitch_yaw(float pitch, float yaw, bool normalize) {
     Vec3 f;

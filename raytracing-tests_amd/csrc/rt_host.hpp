@@ -96,10 +96,16 @@ GeometryData04 to_inw04(const rt_geom_desc &d);
 // aabbs: N x (min xyz, max xyz).  Returns (2N-1) x 8 floats in the reference's BFS layout.
 std::vector<float> lbvh_build(const float *aabbs, uint32_t n);
 
-// Binned-SAH BVH over boxes (acceleration structure for IOW-03's closest-hit search; the
+// Full-sweep SAH BVH over boxes (acceleration structure for IOW-03's closest-hit search; the
 // reference has none there).  Same node layout as the LBVH (children contiguous, leftData
 // = first child or -objectID, rightData = parent).  *depth receives the tree depth.
 std::vector<float> sah_build(const float *aabbs, uint32_t n, int *depth);
+
+// 4-wide BVH from a binary one (sah_build / lbvh layout, n >= 2).  Node = 32 floats, SoA over
+// the 4 children: lo_x[4] lo_y[4] lo_z[4] hi_x[4] hi_y[4] hi_z[4] link[4] pad[4]; link > 0 is
+// (wide node index + 1), link <= 0 is -objectID, empty slots hold a far-away box and link 1e9.
+// *depth receives the number of wide levels.
+std::vector<float> bvh4_collapse(const std::vector<float> &bin, int *depth);
 
 // ---- camera (materials.cpp:321-328, base.h:274-281) ------------------------------------
 Vec3 front_from_pitch_yaw(float pitch_deg, float yaw_deg, bool normalize);

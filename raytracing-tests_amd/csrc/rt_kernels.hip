@@ -12,6 +12,8 @@
 //   k_iow03 <- In-One-Weekend/03_Shadows_and_Materials/computeShaderSrc.glsl:196-430
 //   k_inw   <- In-Next-Week/01_BoundingVolumeHierarchy/computeShaderSrc.glsl:230-675 (LIGHTS=false)
 //              In-Next-Week/04_Lights_Camera_And_Action/computeShaderSrc.glsl:243-773 (LIGHTS=true)
+#include <cstdlib>
+
 #include "rt_kernels.hpp"
 #include "rt_math.hpp"
 
@@ -135,16 +137,35 @@ __device__ __forceinline__ bool cull_slab(float4 n0, float4 n1, f3 o, f3 id, flo
     return te <= tx && tx >= -1e-3f && te <= lim;
 }
 
+// Same test for one child of a 4-wide node; returns the entry t, or kMiss when culled.
+constexpr float kMiss = __builtin_huge_valf();
+__device__ __forceinline__ float cull_t(float lx, float ly, float lz, float hx, float hy, float hz, f3 o, f3 id,
+                                        float lim) {
+    const float x0 = (lx - o.x) * id.x, x1 = (hx - o.x) * id.x;
+    const float y0 = (ly - o.y) * id.y, y1 = (hy - o.y) * id.y;
+    const float z0 = (lz - o.z) * id.z, z1 = (hz - o.z) * id.z;
+    const float te = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    const float tx = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    return (te <= tx && tx >= -1e-3f && te <= lim) ? te : kMiss;
+}
+__device__ __forceinline__ void cswap(float &ta, int &ka, float &tb, int &kb) {
+    const bool sw = tb < ta;
+    const float t = sw ? tb : ta;
+    const int k = sw ? kb : ka;
+    tb = sw ? ta : tb; kb = sw ? ka : kb;
+    ta = t; ka = k;
+}
+
 // LaunchRay 03...glsl:196-256.  The reference loops over every object and keeps the first
 // strictly nearer hit, i.e. the minimum t with the lowest index among exact ties.  The BVH
 // walk visits a superset of the objects that can attain that minimum and applies the same
 // (t, index) rule, so it returns the same object and the same t bits.  The closest hit's
 // normal and attributes are evaluated once after the search from the winning object.
+template <int BCAP>
 __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 gd, float max_t, float contrib,
-                                 Ctr &c, unsigned short *bstk) {
+                                 Ctr &c, short *bstk) {
     float min_t = max_t;
     int best = -1;
-    f3 best_to = f3{0, 0, 0}, best_nd = f3{0, 0, 0}, best_td = f3{0, 0, 0};
     c.seg++;
     // Objects whose matrix is glm::mat3(1) transform the direction identically, so M*gd and
     // normalize(M*gd) are evaluated once per ray (same operations, same bits: 1*x folds to x,
@@ -152,19 +173,21 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
     const m3 I = m3{f3{1.0f, 0.0f, 0.0f}, f3{0.0f, 1.0f, 0.0f}, f3{0.0f, 0.0f, 1.0f}};
     const f3 td_id = mul(I, gd);
     const f3 nd_id = normalize(td_id);
+    // local ray of object j (a pure function of j and the ray: recomputed for the winner)
+    auto local = [&](const float *h, const IowObj &ob, f3 &to, f3 &td, f3 &nd) {
+        if (h[19] != 0.0f) { to = mul(I, go - ob.pos); td = td_id; nd = nd_id; }
+        else { to = mul(ob.M, go - ob.pos); td = mul(ob.M, gd); nd = normalize(td); }
+    };
     auto test = [&](int j) {
         c.prims++;
         const float *h = S.hot + (size_t)j * kIowHot;
         const IowObj ob = iow_obj(h);
         f3 to, td, nd;
-        if (h[19] != 0.0f) { to = mul(I, go - ob.pos); td = td_id; nd = nd_id; }
-        else { to = mul(ob.M, go - ob.pos); td = mul(ob.M, gd); nd = normalize(td); }
+        local(h, ob, to, td, nd);
         float t = -1.0f;
         if (ob.type == 2) t = t_ellipsoid(to, nd, ob.is);
         else if (ob.type == 1) t = t_cuboid(to, nd, ob.scale);
-        if (t > 0.0f && (t < min_t || (t == min_t && j < best))) {
-            min_t = t; best = j; best_to = to; best_nd = nd; best_td = td;
-        }
+        if (t > 0.0f && (t < min_t || (t == min_t && j < best))) { min_t = t; best = j; }
     };
     const float dl2 = dot(gd, gd);
     if (!(dl2 > 0.0f)) {
@@ -177,31 +200,41 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
         // leaf parks it and keeps walking inner nodes; primitive tests run when every lane
         // of the wave holds one (or has finished), so they execute with full lanes.
         const f3 id = f3{__builtin_amdgcn_rcpf(gd.x), __builtin_amdgcn_rcpf(gd.y), __builtin_amdgcn_rcpf(gd.z)};
-        int sp = 0, cur = 0, pend = -1;
-        bool walking = true;
+        // 4-wide BVH.  cur = link of the next node to enter: > 0 = wide node cur-1, <= 0 =
+        // leaf of object -cur.  One step loads a 112-B node (7 x float4, SoA over the four
+        // children), tests the four boxes, enters the nearest hit child and pushes the others
+        // farthest-first.
+        int sp = 0, pend = -1, cur = S.root_link;
+        bool walking = true, ovf = false;  // ovf: a child was dropped by a full stack
         for (;;) {
             DBG_TALLY(F_, c, kDbgTrav, walking);
             if (walking) {
-                const float4 n1 = S.nodes[2 * cur + 1];
-                if (n1.z > 0.1f) {
-                    const int L = (int)n1.z;
-                    const float4 a0 = S.nodes[2 * L], a1 = S.nodes[2 * L + 1];
-                    const float4 b0 = S.nodes[2 * L + 2], b1 = S.nodes[2 * L + 3];
-                    c.nodes += 2;
+                if (cur > 0) {
+                    const float4 *nd = S.nodes + 8 * (size_t)(cur - 1);
+                    const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
+                    const float4 lk = nd[6];
+                    c.nodes += 4;
                     const float lim = min_t * 1.0001f + 1e-3f;
-                    float ta, tb;
-                    const bool ha = cull_slab(a0, a1, go, id, lim, ta);
-                    const bool hb = cull_slab(b0, b1, go, id, lim, tb);
-                    if (ha && hb) {
-                        const bool a_first = ta <= tb;
-                        bstk[(sp++) * kBlock] = (unsigned short)(a_first ? L + 1 : L);
-                        cur = a_first ? L : L + 1;
-                    } else if (ha) cur = L;
-                    else if (hb) cur = L + 1;
-                    else if (sp == 0) walking = false;
-                    else cur = bstk[(--sp) * kBlock];
+                    float t0 = cull_t(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, go, id, lim);
+                    float t1 = cull_t(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, go, id, lim);
+                    float t2 = cull_t(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, go, id, lim);
+                    float t3 = cull_t(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, go, id, lim);
+                    int k0 = (int)lk.x, k1 = (int)lk.y, k2 = (int)lk.z, k3 = (int)lk.w;
+                    // sort (t, link) ascending; misses carry t = +inf
+                    cswap(t0, k0, t1, k1); cswap(t2, k2, t3, k3);
+                    cswap(t0, k0, t2, k2); cswap(t1, k1, t3, k3);
+                    cswap(t1, k1, t2, k2);
+                    if (t0 == kMiss) {
+                        if (sp == 0) walking = false;
+                        else cur = bstk[(--sp) * kBlock];
+                    } else {
+                        cur = k0;
+                        if (t3 != kMiss) { if (sp < BCAP) bstk[(sp++) * kBlock] = (short)k3; else ovf = true; }
+                        if (t2 != kMiss) { if (sp < BCAP) bstk[(sp++) * kBlock] = (short)k2; else ovf = true; }
+                        if (t1 != kMiss) { if (sp < BCAP) bstk[(sp++) * kBlock] = (short)k1; else ovf = true; }
+                    }
                 } else if (pend < 0) {
-                    pend = (int)(-n1.z);
+                    pend = -cur;
                     if (sp == 0) walking = false;
                     else cur = bstk[(--sp) * kBlock];
                 }
@@ -212,12 +245,18 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
                 if (__all(!walking)) break;
             }
         }
+        // a dropped subtree may hold the winner: the linear loop covers every object, and the
+        // (t, index) rule makes re-testing the visited ones harmless
+        if (ovf) for (uint32_t j = 0; j < S.n; j++) test((int)j);
     } else {
         for (uint32_t j = 0; j < S.n; j++) test((int)j);  // also the path for zero / NaN directions
     }
     RayRet r;
     if (min_t < max_t) {
-        const IowObj ob = iow_obj(S.hot + (size_t)best * kIowHot);
+        const float *hb = S.hot + (size_t)best * kIowHot;
+        const IowObj ob = iow_obj(hb);
+        f3 best_to, best_td, best_nd;
+        local(hb, ob, best_to, best_td, best_nd);
         const float *cold = S.cold + (size_t)best * kIowCold;
         f3 h = best_to + best_nd * min_t;
         f3 n = ob.type == 2 ? f3{h.x * ob.is.x * ob.scale.x, h.y * ob.is.y * ob.scale.y, h.z * ob.is.z * ob.scale.z}
@@ -269,30 +308,44 @@ __device__ __forceinline__ float schlick(float cosine, float ri) {
 // The entries outlive a sample: the parent-RI lookup (03...glsl:316-319) may read slots above
 // the stack top that an earlier sample of the same pixel wrote, so a pixel's samples stay in
 // order on one lane and the LDS slots persist across them.
-constexpr int kIowStack = 4, kIowSlot = 9;
+// Two layouts: WIDE keeps `bounced` as a ninth float (any u_NumOfBounce); NARROW keeps it as
+// a byte (u_NumOfBounce <= 255), which with a 12-entry BVH stack fits 4 blocks per CU in LDS.
+constexpr int kIowStack = 4;
+template <bool NARROW>
 struct IowStack {
-    float *base;  // LDS, [slot][thread]
+    static constexpr int kSlot = NARROW ? 8 : 9;
+    float *base;          // LDS, [slot][thread]
+    unsigned char *bb;    // NARROW: LDS, [entry][thread]
     int size;
-    __device__ __forceinline__ float &at(int entry, int k) { return base[(entry * kIowSlot + k) * kBlock]; }
+    __device__ __forceinline__ float &at(int entry, int k) { return base[(entry * kSlot + k) * kBlock]; }
+    __device__ __forceinline__ int bounced(int e) {
+        if constexpr (NARROW) return bb[e * kBlock];
+        else return (int)at(e, 8);
+    }
+    __device__ __forceinline__ void set_bounced(int e, int b) {
+        if constexpr (NARROW) bb[e * kBlock] = (unsigned char)b;
+        else at(e, 8) = (float)b;
+    }
     __device__ __forceinline__ void push(f3 o, f3 d, float contrib, float ri, int b, Ctr &c) {
         if (size < kIowStack) {
             at(size, 0) = o.x; at(size, 1) = o.y; at(size, 2) = o.z;
             at(size, 3) = d.x; at(size, 4) = d.y; at(size, 5) = d.z;
-            at(size, 6) = contrib; at(size, 7) = ri; at(size, 8) = (float)b;
+            at(size, 6) = contrib; at(size, 7) = ri; set_bounced(size, b);
             size++;
         } else c.drops++;
     }
 };
 
-// One iteration of LaunchRays' while loop (03...glsl:294-356): pop, cast, shade, push.
-__device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, IowStack &K, int &skip, f3 &sample,
-                                            int sidx, Ctr &c, unsigned short *bstk) {
+template <bool NARROW>
+__device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, IowStack<NARROW> &K, int &skip,
+                                            f3 &sample, int sidx, Ctr &c, short *bstk) {
+    constexpr int BCAP = NARROW ? 12 : kIowBvhStack;
     K.size--;
     const int e = K.size;
     f3 co = mk(K.at(e, 0), K.at(e, 1), K.at(e, 2)), cd = mk(K.at(e, 3), K.at(e, 4), K.at(e, 5));
     float contribution = K.at(e, 6), ri = K.at(e, 7);
-    int bounced = (int)K.at(e, 8);
-    RayRet data = iow_launch_ray(S, F, co, cd, 32000.0f, contribution, c, bstk);
+    int bounced = K.bounced(e);
+    RayRet data = iow_launch_ray<BCAP>(S, F, co, cd, 32000.0f, contribution, c, bstk);
     const bool hit = dot(data.normal, data.normal) > 0.9f;
     sample = sample + (hit ? data.color : background(cd, false)) * contribution;
     if (bounced < F.max_bounces && hit) {
@@ -416,13 +469,17 @@ __device__ __forceinline__ uint32_t park_slot(unsigned *count, bool need) {
 __device__ __forceinline__ float ibits(int v) { return __int_as_float(v); }
 __device__ __forceinline__ float ubits(uint32_t v) { return __uint_as_float(v); }
 
-__global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, Chunk ch, Cont ct, unsigned *counter,
-                                                  int s_stop) {
-    __shared__ float lds[kIowStack * kIowSlot * kBlock];
-    __shared__ unsigned short lds_bvh[kIowBvhStack * kBlock];
-    unsigned short *bstk = lds_bvh + threadIdx.x;
+template <bool NARROW>
+__device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, const Chunk &ch, const Cont &ct,
+                                           unsigned *counter, int s_stop) {
+    using Stack = IowStack<NARROW>;
+    constexpr int kFl = kIowStack * Stack::kSlot;  // stack floats per lane
+    __shared__ float lds[kFl * kBlock];
+    __shared__ unsigned char lds_b[NARROW ? kIowStack * kBlock : 1];
+    __shared__ short lds_bvh[(NARROW ? 12 : kIowBvhStack) * kBlock];
+    short *bstk = lds_bvh + threadIdx.x;
     Ctr c;
-    IowStack K{lds + threadIdx.x, 0};
+    Stack K{lds + threadIdx.x, lds_b + threadIdx.x, 0};
     const uint32_t total = ct.in ? *ct.in_count : units_total(f);
     const bool may_park = ct.out != nullptr && total >= ct.park_min;
     const int W = f.W, H = f.H, spp = f.spp;
@@ -451,7 +508,9 @@ __global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, Chunk ch,
                 fc = f3{a.x, a.y, a.z}; urays = __float_as_uint(a.w);
                 sample = f3{b.x, b.y, b.z};
                 const float *fl = reinterpret_cast<const float *>(p + 3);
-                for (int k = 0; k < kIowStack * kIowSlot; k++) K.base[k * kBlock] = fl[k];
+                for (int k = 0; k < kFl; k++) K.base[k * kBlock] = fl[k];
+                if constexpr (NARROW)
+                    for (int e = 0; e < kIowStack; e++) K.set_bounced(e, __float_as_int(fl[kFl + e]));
                 px = unit_pixel(f, unit);
                 sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
                 sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
@@ -490,7 +549,9 @@ __global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, Chunk ch,
                 p[1] = make_float4(fc.x, fc.y, fc.z, ubits(urays));
                 p[2] = make_float4(sample.x, sample.y, sample.z, 0.0f);
                 float *fl = reinterpret_cast<float *>(p + 3);
-                for (int k = 0; k < kIowStack * kIowSlot; k++) fl[k] = K.base[k * kBlock];
+                for (int k = 0; k < kFl; k++) fl[k] = K.base[k * kBlock];
+                if constexpr (NARROW)
+                    for (int e = 0; e < kIowStack; e++) fl[kFl + e] = ibits(K.bounced(e));
             }
             break;
         }
@@ -500,7 +561,7 @@ __global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, Chunk ch,
             f3 ro, rd;
             iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
             if (f.show_normal) {
-                fc = fc + iow_launch_ray(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
+                fc = fc + iow_launch_ray<NARROW ? 12 : kIowBvhStack>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
                 s++;
                 urays++;
             } else {
@@ -530,6 +591,17 @@ __global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, Chunk ch,
         }
     }
     flush(f, c);
+}
+
+__global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, Chunk ch, Cont ct, unsigned *counter,
+                                                  int s_stop) {
+    iow03_body<false>(f, S, ch, ct, counter, s_stop);
+}
+// u_NumOfBounce <= 255: byte bounce counts + 12-deep BVH stack -> 39 KB LDS per block, and a
+// 128-VGPR budget, so 4 waves per SIMD stay resident
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void k_iow03n(Frame f, IowScene S, Chunk ch, Cont ct, unsigned *counter, int s_stop) {
+    iow03_body<true>(f, S, ch, ct, counter, s_stop);
 }
 
 // ============================================================================ INW
@@ -894,10 +966,16 @@ static dim3 grid_iow01(const Frame &f) {
     return dim3((unsigned)(((f.tw + 15) >> 4) * ((f.th + 15) >> 4)));
 }
 
+bool iow_narrow(const Frame &f) {
+    const char *v = std::getenv("RT_IOW_NARROW");  // A/B switch (measured slower: VGPR spills)
+    return f.max_bounces <= 255 && v && v[0] == '1';
+}
+
 int resident_blocks_per_cu(int kind) {
     int nb = 0;
     hipError_t e;
     if (kind == 3) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03, kBlock, 0);
+    else if (kind == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03n, kBlock, 0);
     else if (kind == 14) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<true>, kBlock, 0);
     else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<false>, kBlock, 0);
     return (e == hipSuccess && nb > 0) ? nb : 2;
@@ -911,7 +989,9 @@ hipError_t launch_iow03(const Frame &f, const IowScene &sc, const Chunk &ch, con
                         unsigned *counter, int s_stop, int blocks_cap, hipStream_t s) {
     hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_iow03, dim3(grid_of(n_units, blocks_cap)), dim3(kBlock), 0, s, f, sc, ch, ct, counter, s_stop);
+    const dim3 g(grid_of(n_units, blocks_cap));
+    if (iow_narrow(f)) hipLaunchKernelGGL(k_iow03n, g, dim3(kBlock), 0, s, f, sc, ch, ct, counter, s_stop);
+    else hipLaunchKernelGGL(k_iow03, g, dim3(kBlock), 0, s, f, sc, ch, ct, counter, s_stop);
     return hipGetLastError();
 }
 hipError_t launch_inw(const Frame &f, const InwScene &sc, const Chunk &ch, const Cont &ct, uint32_t n_units,

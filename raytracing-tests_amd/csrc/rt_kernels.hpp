@@ -32,14 +32,15 @@ constexpr int kIowCold = 8;   // color3 material3 scat2
 constexpr int kInwHot = 28;   // pos3 R9 scale3 delta3 type extra inv_scale3 inv_s2_3 ri_acc pad
 constexpr int kInwCold = 8;   // refr refl srfr srfl color3 ri
 
-constexpr int kIowBvhStack = 32;  // deepest IOW BVH the kernel walks; deeper trees use the linear loop
+constexpr int kIowBvhStack = 32;  // IOW BVH traversal stack entries; a ray that overflows it also runs the linear loop
 struct IowScene {
     const float *hot, *cold;
     uint32_t n;
-    const float4 *nodes;     // conservative BVH over the objects ((2n-1)*2 float4) or null = linear loop
+    const float4 *nodes;     // conservative 4-wide BVH over the objects (8 float4 per node) or null = linear loop
     const float *sunflower;  // spp*2
     const float *fib;        // spp*4 (xyz + pad)
     const int *ring;         // spp*2
+    int root_link;           // link of the BVH root (wide node 0 -> 1)
 };
 struct InwScene {
     const float4 *hot;       // n * 7 float4
@@ -90,7 +91,12 @@ hipError_t launch_inw(const Frame &f, const InwScene &sc, const Chunk &ch, const
                       unsigned *counter, int blocks_cap, hipStream_t s);
 uint32_t units_of(const Frame &f);
 // resident 256-thread blocks per CU for the persistent kernels (occupancy query)
+// resident blocks per CU of the render kernel for `kind` (3 = IOW-03 wide, 4 = IOW-03 narrow,
+// 11/14 = INW layout 1/4)
 int resident_blocks_per_cu(int kind);
+// IOW-03 kernel variant for this frame: narrow (byte bounce counts, 12-deep BVH stack, 4 waves
+// per SIMD with spills) when RT_IOW_NARROW=1 and u_NumOfBounce <= 255; wide otherwise
+bool iow_narrow(const Frame &f);
 // order[i] = unit ids sorted by cost, most expensive first (hipcub radix sort)
 hipError_t sort_units_by_cost(const unsigned *cost, unsigned *keys_tmp, const unsigned *iota, unsigned *order,
                               uint32_t n, void *temp, size_t temp_bytes, hipStream_t s);

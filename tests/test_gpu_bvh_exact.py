@@ -1,7 +1,11 @@
-"""The IOW-03 culling BVH returns exactly the reference's linear-loop closest hit: a full
-frame of the final scene rendered both ways (RT_IOW_LINEAR=1 selects the linear loop) must be
-bit-identical, with identical ray counts.  Runs the two renders in subprocesses because the
-switch is read when the device scene is built."""
+"""Full-frame exactness of the IOW-03 kernel's execution strategies against each other.
+
+- RT_IOW_LINEAR=1: the reference's linear object loop instead of the culling BVH;
+- RT_IOW_NARROW=1: the byte-bounce stack layout (12-deep BVH stack) instead of the 9-float one;
+- RT_ROUNDS=0:     no tail compaction (no parking / resume launches).
+Each must give a bit-identical image of the final scene with identical ray counts.  The
+renders run in subprocesses because the switches are read by the library at scene build /
+launch time."""
 import json
 import os
 import subprocess
@@ -24,24 +28,32 @@ print(json.dumps(st))
 """
 
 
-def _render(tmp_path, linear, w, h, spp):
-    out = str(tmp_path / f"img_{int(linear)}.npy")
+def _render(tmp_path, over, w, h, spp):
+    out = str(tmp_path / f"img_{len(os.listdir(tmp_path))}.npy")
     env = dict(os.environ)
-    env["RT_IOW_LINEAR"] = "1" if linear else "0"
+    for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS"):
+        env.pop(k, None)
+    env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-2000:]
     return np.load(out), json.loads(r.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("w,h,spp", [(600, 400, 2), (1200, 800, 1)])
-def test_bvh_equals_linear_full_frame(tmp_path, gpu, w, h, spp):
-    a, sa = _render(tmp_path, False, w, h, spp)
-    b, sb = _render(tmp_path, True, w, h, spp)
+@pytest.mark.parametrize("over,w,h,spp", [
+    ({"RT_IOW_LINEAR": "1"}, 600, 400, 2),
+    ({"RT_IOW_LINEAR": "1"}, 1200, 800, 1),
+    ({"RT_IOW_NARROW": "1"}, 600, 400, 8),
+    ({"RT_ROUNDS": "0"}, 600, 400, 8),
+    ({"RT_CHUNKS": "lpt"}, 300, 200, 24),
+])
+def test_strategies_bit_identical(tmp_path, gpu, over, w, h, spp):
+    a, sa = _render(tmp_path, {}, w, h, spp)
+    b, sb = _render(tmp_path, over, w, h, spp)
     same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
     bad = np.argwhere(~same.all(axis=2))
     print("mismatching pixels:", len(bad), bad[:10].tolist())
-    print("bvh", sa, "linear", sb)
+    print("default", sa, over, sb)
     assert len(bad) == 0
     for k in ("segments", "stack_drops", "nan_drops"):
         assert sa[k] == sb[k], k
