@@ -127,7 +127,7 @@ def main():
     d_tiles = torch.tensor(mine, dtype=torch.int32, device=dev).reshape(-1, 2).contiguous()
     packed = torch.zeros((per_rank, TILE, TILE, 4), dtype=torch.float32, device=dev)
     counters = torch.zeros(6, dtype=torch.int64, device=dev)
-    dbg = torch.zeros(8, dtype=torch.int64, device=dev)
+    dbg = torch.zeros(16, dtype=torch.int64, device=dev)
     if args.occupancy:
         lib.rt_debug_counters(dbg.data_ptr())
     gathered = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
@@ -235,6 +235,8 @@ def main():
             out["lane_occupancy"] = {name: round(d[2 * i + 1] / max(d[2 * i], 1) / 64, 4)
                                      for i, name in enumerate(("outer", "bvh_walk", "leaf_tests", "segments"))}
             out["wave_iterations"] = {name: d[2 * i] for i, name in enumerate(("outer", "bvh_walk", "leaf_tests", "segments"))}
+            cyc = dict(zip(("camera", "closest_hit", "bvh_walk", "leaf_tests", "segment"), d[8:13]))
+            out["wave_cycles_share"] = {k: round(v / max(1, cyc["camera"] + cyc["segment"]), 4) for k, v in cyc.items()}
         print(json.dumps(out), flush=True)
     lib.rt_dev_scene_free(scene)
     if world > 1:

@@ -139,9 +139,12 @@ int rt_render_image_async(rt_dev_scene *s, const rt_camera *cam, const rt_params
                           float *d_rgba, float *d_depth, uint64_t *d_counters, void *stream);
 
 /* ---- diagnostics ---------------------------------------------------------------------
- * d_buf: device array of 8 uint64 (or NULL to disable).  While set, the kernels add, per
- * wave iteration of each phase (outer work loop, BVH walk, postponed-leaf tests, ray
- * segments), 1 and the number of lanes taking part -- a direct lane-occupancy measure. */
+ * d_buf: device array of 16 uint64 (or NULL to disable).  While set, the IOW-03 kernel adds
+ *   [0..7]  per wave iteration of each phase (outer work loop, BVH walk, postponed-leaf tests,
+ *           ray segments): 1 and the number of lanes taking part (lane occupancy);
+ *   [8..13] wave shader-clock cycles in: the work loop's camera-ray part, closest-hit queries,
+ *           their BVH walk, leaf tests, ray segments, (unused).
+ * Diagnostics cost time; never enable them for a measured run. */
 int rt_debug_counters(uint64_t *d_buf);
 
 #ifdef __cplusplus

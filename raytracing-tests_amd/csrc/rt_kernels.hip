@@ -50,20 +50,36 @@ __device__ __forceinline__ Pix map_pixel(const Frame &f) {
 
 struct Ctr {
     uint32_t seg = 0, nodes = 0, prims = 0, shadow = 0, drops = 0, nans = 0;
-    unsigned long long dbg[kDbgSlots] = {0, 0, 0, 0, 0, 0, 0, 0};  // wave-uniform tallies
+    unsigned long long *wdbg = nullptr;  // diagnostics: this wave's kDbg* row in LDS, or null
 };
-// count one wave-iteration of a phase and how many lanes take part (diagnostic builds only)
+// Diagnostics (rt_debug_counters).  Tallies go to a per-wave LDS row, written by the first
+// active lane, so they cost no registers when off and are exact inside divergent code.
+__device__ __forceinline__ bool first_active_lane() {
+    return (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1;
+}
+// wave cycles of a phase (shader clock)
+#define DBG_T0(f, t) const unsigned long long t = c.wdbg ? (unsigned long long)clock64() : 0ull
+#define DBG_CYC(f, c, slot, t)                                                        \
+    do {                                                                              \
+        if ((c).wdbg) {                                                               \
+            const unsigned long long d_ = (unsigned long long)clock64() - (t);        \
+            if (first_active_lane()) (c).wdbg[slot] += d_;                            \
+        }                                                                             \
+    } while (0)
+// count one wave-iteration of a phase and how many lanes take part
 #define DBG_TALLY(f, c, slot, pred)                                                   \
     do {                                                                              \
-        if ((f).dbg) {                                                                \
+        if ((c).wdbg) {                                                               \
             const unsigned long long m_ = __ballot(pred);                             \
-            (c).dbg[slot] += 1; (c).dbg[(slot) + 1] += (unsigned long long)__popcll(m_); \
+            if (first_active_lane()) {                                                \
+                (c).wdbg[slot] += 1; (c).wdbg[(slot) + 1] += (unsigned long long)__popcll(m_); \
+            }                                                                         \
         }                                                                             \
     } while (0)
 
 __device__ __forceinline__ void flush(const Frame &f, const Ctr &c) {
-    if (f.dbg && (threadIdx.x & 63) == 0)
-        for (int i = 0; i < kDbgSlots; i++) atomicAdd(f.dbg + i, c.dbg[i]);  // wave-uniform values
+    if (c.wdbg && (threadIdx.x & 63) == 0)
+        for (int i = 0; i < kDbgSlots; i++) atomicAdd(f.dbg + i, c.wdbg[i]);
     if (!f.counters) return;
     unsigned long long v[6] = {c.seg, c.nodes, c.prims, c.shadow, c.drops, c.nans};
 #pragma unroll
@@ -164,6 +180,7 @@ __device__ __forceinline__ void cswap(float &ta, int &ka, float &tb, int &kb) {
 template <int BCAP>
 __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 gd, float max_t, float contrib,
                                  Ctr &c, short *bstk) {
+    DBG_T0(F_, t_ray);
     float min_t = max_t;
     int best = -1;
     c.seg++;
@@ -204,6 +221,7 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
         // leaf of object -cur.  One step loads a 112-B node (7 x float4, SoA over the four
         // children), tests the four boxes, enters the nearest hit child and pushes the others
         // farthest-first.
+        DBG_T0(F_, t_trav);
         int sp = 0, pend = -1, cur = S.root_link;
         bool walking = true, ovf = false;  // ovf: a child was dropped by a full stack
         for (;;) {
@@ -241,13 +259,16 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
             }
             if (__all(!walking || pend >= 0)) {
                 DBG_TALLY(F_, c, kDbgLeaf, pend >= 0);
+                DBG_T0(F_, t_leaf);
                 if (pend >= 0) { test(pend); pend = -1; }
+                DBG_CYC(F_, c, kDbgCycLeaf, t_leaf);
                 if (__all(!walking)) break;
             }
         }
         // a dropped subtree may hold the winner: the linear loop covers every object, and the
         // (t, index) rule makes re-testing the visited ones harmless
         if (ovf) for (uint32_t j = 0; j < S.n; j++) test((int)j);
+        DBG_CYC(F_, c, kDbgCycTrav, t_trav);
     } else {
         for (uint32_t j = 0; j < S.n; j++) test((int)j);  // also the path for zero / NaN directions
     }
@@ -265,7 +286,7 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
         r.material = mk(cold[3], cold[4], cold[5]);
         r.scat0 = cold[6]; r.scat1 = cold[7];
         const bool inside = dot(n, best_td) > 0.0f;
-        f3 n_ = inside ? -n : n;
+        f3 n_ = sel(inside, -n, n);
         f3 refl = reflect(best_td, n_);
         if (!inside) {
             f3 nir = normalize(cross(n_, best_td));
@@ -273,7 +294,7 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
             float s = r.scat1;
             float k = 1.0f / __builtin_sqrtf(1.0f + s * s);
             f3 mr = n_ * (s * k) + nn * k;
-            refl = (dot(refl, n_) > dot(mr, n_)) ? refl : mr;
+            refl = sel(dot(refl, n_) > dot(mr, n_), refl, mr);
         }
         m3 inv = inverse(ob.M);
         r.point = go + gd * min_t;
@@ -285,6 +306,7 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
         r.reflected = r.color = r.material = f3{0, 0, 0};
         r.scat0 = r.scat1 = 0.0f;
     }
+    DBG_CYC(F_, c, kDbgCycRay, t_ray);
     return r;
 }
 
@@ -347,7 +369,7 @@ __device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, I
     int bounced = K.bounced(e);
     RayRet data = iow_launch_ray<BCAP>(S, F, co, cd, 32000.0f, contribution, c, bstk);
     const bool hit = dot(data.normal, data.normal) > 0.9f;
-    sample = sample + (hit ? data.color : background(cd, false)) * contribution;
+    sample = sample + sel(hit, data.color, background(cd, false)) * contribution;
     if (bounced < F.max_bounces && hit) {
         bounced++;
         bool spawnRefl = false, spawnRefr = false;
@@ -362,7 +384,7 @@ __device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, I
         }
         float rr = (ri * rcp(target_ri)) * sin_t;
         float refr_c = data.material.x, refl_c = data.material.y;
-        f3 n_ = cos_t > 0.0f ? data.normal : -data.normal;
+        f3 n_ = sel(cos_t > 0.0f, data.normal, -data.normal);
         if (cos_t < 0.0f) {
             refl_dir = fib_dir(S, sidx, data.scat1, data.reflected); spawnRefl = true;
             float inc = refr_c * schlick(-cos_t, ri * rcp(target_ri));
@@ -478,7 +500,12 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
     __shared__ unsigned char lds_b[NARROW ? kIowStack * kBlock : 1];
     __shared__ short lds_bvh[(NARROW ? 12 : kIowBvhStack) * kBlock];
     short *bstk = lds_bvh + threadIdx.x;
+    __shared__ unsigned long long s_dbg[kBlock / 64][kDbgSlots];
     Ctr c;
+    if (f.dbg) {
+        c.wdbg = s_dbg[threadIdx.x >> 6];
+        if ((threadIdx.x & 63) < kDbgSlots) c.wdbg[threadIdx.x & 63] = 0;
+    }
     Stack K{lds + threadIdx.x, lds_b + threadIdx.x, 0};
     const uint32_t total = ct.in ? *ct.in_count : units_total(f);
     const bool may_park = ct.out != nullptr && total >= ct.park_min;
@@ -556,8 +583,8 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
             break;
         }
         DBG_TALLY(f, c, kDbgOuter, busy);
-        if (!busy) continue;
-        if (K.size == 0 && s < s_end) {  // start sample s
+        DBG_T0(f, t_loop);
+        if (busy && K.size == 0 && s < s_end) {  // start sample s
             f3 ro, rd;
             iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
             if (f.show_normal) {
@@ -570,13 +597,16 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
                 skip = 0;
             }
         }
-        DBG_TALLY(f, c, kDbgSeg, K.size > 0);
-        if (K.size > 0) {
+        DBG_TALLY(f, c, kDbgSeg, busy && K.size > 0);
+        DBG_CYC(f, c, kDbgCycCam, t_loop);
+        DBG_T0(f, t_seg);
+        if (busy && K.size > 0) {
             iow_segment(S, f, K, skip, sample, s, c, bstk);
             urays++;
             if (K.size == 0) { fc = fc + sample; s++; }
         }
-        if (K.size == 0 && s >= s_end) {
+        DBG_CYC(f, c, kDbgCycSeg, t_seg);
+        if (busy && K.size == 0 && s >= s_end) {
             if (s_end >= s_stop) {
                 if (ch.final_chunk) write_px(f, px, fc * rcp((float)s_stop), 0.0f);
                 else if (ch.state) {  // early-return pixels: keep the final colour for the last launch

@@ -23,7 +23,10 @@ struct Frame {
 };
 // lane-occupancy counters (per wave-iteration: 1 and popcount of the participating lanes)
 enum { kDbgOuter = 0, kDbgOuterLanes, kDbgTrav, kDbgTravLanes, kDbgLeaf, kDbgLeafLanes, kDbgSeg, kDbgSegLanes,
-       kDbgSlots = 8 };
+       // per-wave shader-clock cycles (IOW-03): camera-ray part of the work loop, closest-hit
+       // queries, their BVH walk (incl. leaf tests), the leaf tests, ray segments (incl. query)
+       kDbgCycCam, kDbgCycRay, kDbgCycTrav, kDbgCycLeaf, kDbgCycSeg, kDbgCycSpare0, kDbgCycSpare1, kDbgCycSpare2,
+       kDbgSlots = 16 };
 
 // IOW-03 device scene: "hot" records walked by the linear loop + "cold" hit attributes.
 constexpr int kIowHot = 20;   // pos3 type M9 scale3 inv_scale3 pad

@@ -17,6 +17,8 @@ __device__ __forceinline__ f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y +
 __device__ __forceinline__ f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 __device__ __forceinline__ f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
 __device__ __forceinline__ f3 operator*(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
+// component-wise select (an aggregate ?: can lower to a private-memory copy)
+__device__ __forceinline__ f3 sel(bool c, f3 a, f3 b) { return f3{c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z}; }
 __device__ __forceinline__ f3 mulv(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
