@@ -86,6 +86,8 @@ rtk::Frame make_frame(const rt_camera *cam, const rt_params *p) {
     }
     f.inv_spp = 1.0f / (float)p->spp;
     f.dbg = g_dbg;
+    const char *lb = std::getenv("RT_LEAF_BATCH");  // tuning switch (65 = only when no lane can advance)
+    f.leaf_batch = (lb && *lb) ? std::max(1, std::atoi(lb)) : 65;
     return f;
 }
 

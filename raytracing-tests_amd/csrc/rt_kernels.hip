@@ -227,6 +227,7 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
         for (;;) {
             DBG_TALLY(F_, c, kDbgTrav, walking);
             if (walking) {
+                bool pop;
                 if (cur > 0) {
                     const float4 *nd = S.nodes + 8 * (size_t)(cur - 1);
                     const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
@@ -242,22 +243,26 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
                     cswap(t0, k0, t1, k1); cswap(t2, k2, t3, k3);
                     cswap(t0, k0, t2, k2); cswap(t1, k1, t3, k3);
                     cswap(t1, k1, t2, k2);
-                    if (t0 == kMiss) {
-                        if (sp == 0) walking = false;
-                        else cur = bstk[(--sp) * kBlock];
-                    } else {
-                        cur = k0;
-                        if (t3 != kMiss) { if (sp < BCAP) bstk[(sp++) * kBlock] = (short)k3; else ovf = true; }
-                        if (t2 != kMiss) { if (sp < BCAP) bstk[(sp++) * kBlock] = (short)k2; else ovf = true; }
-                        if (t1 != kMiss) { if (sp < BCAP) bstk[(sp++) * kBlock] = (short)k1; else ovf = true; }
-                    }
-                } else if (pend < 0) {
-                    pend = -cur;
+                    // branch-free pushes, farthest first: a miss is written above the top and
+                    // overwritten before it could be popped (the array has 3 spare entries)
+                    int p = sp;
+                    bstk[p * kBlock] = (short)k3; p += t3 != kMiss;
+                    bstk[p * kBlock] = (short)k2; p += t2 != kMiss;
+                    bstk[p * kBlock] = (short)k1; p += t1 != kMiss;
+                    if (p > BCAP) { ovf = true; p = BCAP; }
+                    sp = p;
+                    cur = k0;
+                    pop = t0 == kMiss;
+                } else {
+                    pop = pend < 0;  // a leaf waits while the lane still holds one
+                    if (pop) pend = -cur;
+                }
+                if (pop) {
                     if (sp == 0) walking = false;
                     else cur = bstk[(--sp) * kBlock];
                 }
             }
-            if (__all(!walking || pend >= 0)) {
+            if (__all(!walking || pend >= 0) || __popcll(__ballot(pend >= 0)) >= F_.leaf_batch) {
                 DBG_TALLY(F_, c, kDbgLeaf, pend >= 0);
                 DBG_T0(F_, t_leaf);
                 if (pend >= 0) { test(pend); pend = -1; }
@@ -361,7 +366,7 @@ struct IowStack {
 template <bool NARROW>
 __device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, IowStack<NARROW> &K, int &skip,
                                             f3 &sample, int sidx, Ctr &c, short *bstk) {
-    constexpr int BCAP = NARROW ? 12 : kIowBvhStack;
+    constexpr int BCAP = (NARROW ? 12 : kIowBvhStack) - 3;  // logical depth; 3 spare push slots
     K.size--;
     const int e = K.size;
     f3 co = mk(K.at(e, 0), K.at(e, 1), K.at(e, 2)), cd = mk(K.at(e, 3), K.at(e, 4), K.at(e, 5));
@@ -588,7 +593,7 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
             f3 ro, rd;
             iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
             if (f.show_normal) {
-                fc = fc + iow_launch_ray<NARROW ? 12 : kIowBvhStack>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
+                fc = fc + iow_launch_ray<(NARROW ? 12 : kIowBvhStack) - 3>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
                 s++;
                 urays++;
             } else {

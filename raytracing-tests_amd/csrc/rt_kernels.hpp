@@ -20,6 +20,7 @@ struct Frame {
     float aperture, focus, screen_dist, inv_spp;
     float sphere[4];    // IOW-01 only
     unsigned long long *dbg;  // optional lane-occupancy counters (kDbg* slots), null in production
+    int leaf_batch;           // IOW-03 walk: test postponed leaves once this many lanes hold one
 };
 // lane-occupancy counters (per wave-iteration: 1 and popcount of the participating lanes)
 enum { kDbgOuter = 0, kDbgOuterLanes, kDbgTrav, kDbgTravLanes, kDbgLeaf, kDbgLeafLanes, kDbgSeg, kDbgSegLanes,
