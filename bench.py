@@ -128,8 +128,10 @@ def main():
     packed = torch.zeros((per_rank, TILE, TILE, 4), dtype=torch.float32, device=dev)
     counters = torch.zeros(6, dtype=torch.int64, device=dev)
     dbg = torch.zeros(16, dtype=torch.int64, device=dev)
+    px_rays = torch.zeros(per_rank * TILE * TILE, dtype=torch.int32, device=dev)
     if args.occupancy:
         lib.rt_debug_counters(dbg.data_ptr())
+        lib.rt_debug_pixel_rays(px_rays.data_ptr())
     gathered = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
     nx, ny = math.ceil(W / TILE), math.ceil(H / TILE)
     image = torch.empty((ny * TILE, nx * TILE, 4), dtype=torch.float32, device=dev) if rank == 0 else None
@@ -235,6 +237,17 @@ def main():
             out["lane_occupancy"] = {name: round(d[2 * i + 1] / max(d[2 * i], 1) / 64, 4)
                                      for i, name in enumerate(("outer", "bvh_walk", "leaf_tests", "segments"))}
             out["wave_iterations"] = {name: d[2 * i] for i, name in enumerate(("outer", "bvh_walk", "leaf_tests", "segments"))}
+            pr = px_rays[px_rays > 0].double()
+            q = torch.quantile(pr.float().cpu(), torch.tensor([0.5, 0.9, 0.99, 0.999])).tolist()
+            out["pixel_rays"] = {"mean": round(float(pr.mean()), 1), "p50": q[0], "p90": q[1], "p99": q[2],
+                                 "p999": q[3], "max": int(pr.max())}
+            rounds = (C.c_uint32 * 16)()
+            nr = lib.rt_debug_rounds(scene, rounds, 16)
+            out["parked_per_round"] = [int(rounds[i]) for i in range(max(nr, 0))]
+            h = (C.c_uint64 * 66)()
+            if lib.rt_debug_spec_hist(scene, h) == 0 and h[1]:
+                out["sample_rays"] = {"max": h[0], "samples": h[1],
+                                      "log2_hist": {b: [h[2 + b], h[34 + b]] for b in range(32) if h[2 + b]}}
             cyc = dict(zip(("camera", "closest_hit", "bvh_walk", "leaf_tests", "segment"), d[8:13]))
             out["wave_cycles_share"] = {k: round(v / max(1, cyc["camera"] + cyc["segment"]), 4) for k, v in cyc.items()}
         print(json.dumps(out), flush=True)

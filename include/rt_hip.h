@@ -146,6 +146,17 @@ int rt_render_image_async(rt_dev_scene *s, const rt_camera *cam, const rt_params
  *           their BVH walk, leaf tests, ray segments, (unused).
  * Diagnostics cost time; never enable them for a measured run. */
 int rt_debug_counters(uint64_t *d_buf);
+/* d_buf: device array with one uint32 per work unit (or NULL to disable): the IOW-03 kernel
+ * writes the rays each pixel cast when the pixel completes (unit = tile-major pixel index in
+ * tile mode, 8x8-block-major in rect mode). */
+int rt_debug_pixel_rays(uint32_t *d_buf);
+/* Lanes parked by each tail-compaction round of the scene's last render (synchronises the
+ * device).  Returns the number of rounds written to out (<= cap). */
+int rt_debug_rounds(rt_dev_scene *s, uint32_t *out, int cap);
+/* Rays per sample over the scene's last sample-parallel IOW-03 render (synchronises):
+ * out[0] = max, out[1] = samples, out[2+b] = samples with 2^b <= rays < 2^(b+1),
+ * out[34+b] = rays in those samples.  66 entries. */
+int rt_debug_spec_hist(rt_dev_scene *s, uint64_t *out);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,7 @@
 namespace {
 
 unsigned long long *g_dbg = nullptr;  // rt_debug_counters(): lane-occupancy diagnostics
+unsigned *g_px_rays = nullptr;        // rt_debug_pixel_rays(): rays per work unit
 
 #define HIP_OK(expr)                                             \
     do {                                                         \
@@ -86,6 +87,7 @@ rtk::Frame make_frame(const rt_camera *cam, const rt_params *p) {
     }
     f.inv_spp = 1.0f / (float)p->spp;
     f.dbg = g_dbg;
+    f.px_rays = g_px_rays;
     const char *lb = std::getenv("RT_LEAF_BATCH");  // tuning switch (65 = only when no lane can advance)
     f.leaf_batch = (lb && *lb) ? std::max(1, std::atoi(lb)) : 65;
     return f;
@@ -104,6 +106,7 @@ struct rt_dev_scene {
     int blocks_cap = 0;  // persistent grid size: resident blocks the device can hold (max over variants)
     int cus = 0;
     int root_link = 0;   // IOW-03 culling BVH: leftData of the root
+    float ri_prior = 1.0f;  // IOW-03: most common refractive index (sample-parallel guess)
     DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
     uint32_t ws_units = 0;
@@ -111,6 +114,11 @@ struct rt_dev_scene {
     DevBuf ws_state, ws_cost, ws_keys, ws_iota, ws_order, ws_temp;
     // tail-compaction continuation buffers (ping-pong), blocks_cap*kBlock slots each
     DevBuf cont[2], cont_count;
+    // sample-parallel IOW-03 records, sized for spec_cap (pixel units x samples)
+    size_t spec_cap = 0, spec_units = 0;
+    DevBuf sp_col, sp_fin, sp_ctr, sp_assume, sp_list, sp_fb, sp_counts;
+    DevBuf sp_keys, sp_keys2, sp_list2, sp_temp;  // longest-first ordering of the re-execution list
+    size_t sp_temp_bytes = 0;
 };
 
 namespace {
@@ -139,7 +147,8 @@ void set_residency(rt_dev_scene *s) {
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     s->cus = cus;
     s->blocks_cap = cus * rtk::resident_blocks_per_cu(s->kind);
-    if (s->kind == 3) s->blocks_cap = std::max(s->blocks_cap, cus * rtk::resident_blocks_per_cu(4));
+    if (s->kind == 3)  // continuation buffers serve every IOW-03 variant
+        s->blocks_cap = std::max({s->blocks_cap, cus * rtk::resident_blocks_per_cu(4), cus * rtk::resident_blocks_per_cu(5)});
 }
 
 int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n, int spp) {
@@ -160,6 +169,18 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
         h[19] = std::memcmp(r + 3, kI, sizeof(kI)) == 0 ? 1.0f : 0.0f;
     }
     s->kind = 3; s->n = n;
+    {  // most common RefractiveIndex (record float 20, Geometry::FillBuffer materials.h:48-76)
+        std::vector<float> ri(n);
+        for (uint32_t j = 0; j < n; j++) ri[j] = rec[size_t(j) * 24 + 20];
+        std::sort(ri.begin(), ri.end());
+        size_t best = 0;
+        for (size_t i = 0; i < ri.size();) {
+            size_t k = i;
+            while (k < ri.size() && ri[k] == ri[i]) k++;
+            if (k - i > best) { best = k - i; s->ri_prior = ri[i]; }
+            i = k;
+        }
+    }
     HIP_OK(s->hot.upload(hot.data(), hot.size() * sizeof(float)));
     HIP_OK(s->cold.upload(cold.data(), cold.size() * sizeof(float)));
     // Culling BVH over the objects (the reference loops linearly; rtk::iow_launch_ray keeps its
@@ -270,13 +291,46 @@ int ensure_cont(rt_dev_scene *s) {
     if (s->cont_count.p) return RT_OK;
     const size_t slots = size_t(s->blocks_cap) * rtk::kBlock;
     for (auto &b : s->cont) HIP_OK(b.alloc(slots * rtk::kContSlots * sizeof(float4)));
-    HIP_OK(s->cont_count.alloc(128));  // two counts 64 B apart
+    HIP_OK(s->cont_count.alloc(64 * 16));  // one count per round, 64 B apart (rt_debug_rounds)
     return RT_OK;
+}
+
+// Sample-parallel records for P pixel units x S samples; false if they do not fit.
+bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
+    const size_t n = size_t(P) * S;
+    const size_t bytes = n * (4 * sizeof(float4) + 4 * sizeof(uint32_t)) + size_t(P) * (4 + 32);
+    const double max_gb = std::atof(std::getenv("RT_SPEC_MAX_GB") ? std::getenv("RT_SPEC_MAX_GB") : "96");
+    if (double(bytes) > max_gb * 1e9) return false;
+    if (n <= s->spec_cap && P <= s->spec_units) return true;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || bytes > free_b / 2) return false;
+    for (DevBuf *b : {&s->sp_col, &s->sp_fin, &s->sp_ctr, &s->sp_assume, &s->sp_list, &s->sp_fb, &s->sp_counts,
+                      &s->sp_keys, &s->sp_keys2, &s->sp_list2, &s->sp_temp}) {
+        b->~DevBuf();
+        new (b) DevBuf();
+    }
+    if (s->sp_col.alloc(n * sizeof(float4)) != hipSuccess || s->sp_fin.alloc(n * sizeof(float4)) != hipSuccess ||
+        s->sp_ctr.alloc(n * sizeof(uint4)) != hipSuccess || s->sp_assume.alloc(n * sizeof(float4)) != hipSuccess ||
+        s->sp_list.alloc(n * sizeof(uint32_t)) != hipSuccess || s->sp_fb.alloc(size_t(P) * 4) != hipSuccess ||
+        s->sp_counts.alloc(256) != hipSuccess || s->sp_keys.alloc(n * 4) != hipSuccess ||
+        s->sp_keys2.alloc(n * 4) != hipSuccess || s->sp_list2.alloc(n * 4) != hipSuccess ||
+        s->sp_temp.alloc(s->sp_temp_bytes = rtk::sort_pairs_temp_bytes(n, 24)) != hipSuccess) {
+        s->spec_cap = s->spec_units = 0;
+        return false;
+    }
+    s->spec_cap = n;
+    s->spec_units = P;
+    return true;
 }
 
 // Enqueue a whole render (all chunks) on `st`.  The first call for a given frame size
 // allocates the chunk workspace; later calls allocate nothing.
+int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st);
+
 int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
+    if (s->kind == 3 && env_int("RT_IOW_SPEC", 1) != 0 && !rtk::iow_narrow(f) && s->s_stop > 0 &&
+        ensure_spec(s, rtk::units_of(f), uint32_t(s->s_stop)))
+        return launch_scene_spec(s, f, st);
     const std::vector<std::pair<int, int>> plan = chunk_plan(f.spp);
     const uint32_t units = rtk::units_of(f);
     if (plan.size() > 1) {
@@ -287,7 +341,7 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // lanes the previous one parked.  Counts stay on the device (no host round trip): a resume
     // launch with nothing parked exits at once.  Parking stops below ~one wave per SIMD, where
     // compaction can no longer shorten the critical path; the last round never parks.
-    const int rounds = std::max(0, env_int("RT_ROUNDS", 6));
+    const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 6)));  // <= 14: one count slot per round
     // grid of this frame's kernel variant
     const int cap = s->kind == 3 ? s->cus * rtk::resident_blocks_per_cu(rtk::iow_narrow(f) ? 4 : 3) : s->blocks_cap;
     const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
@@ -295,10 +349,10 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         int rc = ensure_cont(s);
         if (rc != RT_OK) return rc;
     }
-    unsigned *cnt = s->cont_count.as<unsigned>();  // [0], [16]: ping-pong counts (separate cache lines)
+    unsigned *cnt = s->cont_count.as<unsigned>();  // cnt[16*r]: lanes parked by round r (separate cache lines)
     hipError_t e = hipSuccess;
     for (size_t k = 0; k < plan.size() && e == hipSuccess; k++) {
-        rtk::Chunk ch;
+        rtk::Chunk ch{};
         ch.s_begin = plan[k].first;
         ch.s_end = plan[k].second;
         ch.final_chunk = k + 1 == plan.size();
@@ -310,12 +364,12 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             uint32_t n_units = units;
             if (r > 0) {
                 ct.in = s->cont[(r - 1) & 1].as<float4>();
-                ct.in_count = cnt + 16 * ((r - 1) & 1);
+                ct.in_count = cnt + 16 * std::min(r - 1, 15);
                 n_units = uint32_t(cap) * rtk::kBlock;
             }
             if (r < rounds) {
                 ct.out = s->cont[r & 1].as<float4>();
-                ct.out_count = cnt + 16 * (r & 1);
+                ct.out_count = cnt + 16 * std::min(r, 15);
                 ct.park_min = park_min;
                 e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), st);
                 if (e != hipSuccess) break;
@@ -335,6 +389,108 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                                         s->ws_iota.as<unsigned>(), s->ws_order.as<unsigned>(), units,
                                         s->ws_temp.p, s->ws_temp_bytes, st);
     }
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
+        return RT_E_HIP;
+    }
+    return RT_OK;
+}
+
+// Sample-parallel IOW-03: speculate every (pixel, sample) at once, then resolve / re-run the
+// samples whose assumed incoming stack state was wrong (RT_SPEC_ITERS passes), and hand any
+// pixel still unresolved to the sequential kernel from its first unresolved sample.  All
+// launches are enqueued on `st`; counts stay on the device.
+int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
+    const uint32_t P = rtk::units_of(f), S = uint32_t(s->s_stop);
+    int rc = ensure_workspace(s, P);
+    if (rc != RT_OK) return rc;
+    const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 6)));
+    const int iters = std::max(0, env_int("RT_SPEC_ITERS", 10));
+    if (rounds > 0 && (rc = ensure_cont(s)) != RT_OK) return rc;
+    unsigned *cnt = s->cont_count.as<unsigned>();
+    unsigned *sc = s->sp_counts.as<unsigned>();  // [0] list count, [16] fallback count
+    rtk::SpecRecs R{s->sp_col.as<float4>(), s->sp_fin.as<float4>(), s->sp_ctr.as<uint4>(), s->sp_assume.as<float4>(),
+                    P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(), sc + 16, s->ws_order.as<uint32_t>()};
+    rtk::IowScene scene{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
+                        s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link};
+    const int cap_s = s->cus * rtk::resident_blocks_per_cu(5);
+    const int cap_q = s->cus * rtk::resident_blocks_per_cu(3);
+    hipError_t e = hipMemsetAsync(R.assume, 0, size_t(P) * sizeof(float4), st);  // sample 0: exact zeros
+    // one compacted pass: the first launch takes `n0` units, resume launches the parked lanes
+    auto pass = [&](auto &&launch, uint32_t n0, int cap) {
+        const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
+        for (int r = 0; r <= rounds && e == hipSuccess; r++) {
+            rtk::Cont ct{};
+            uint32_t n_units = n0;
+            if (r > 0) {
+                ct.in = s->cont[(r - 1) & 1].as<float4>();
+                ct.in_count = cnt + 16 * std::min(r - 1, 15);
+                n_units = uint32_t(cap) * rtk::kBlock;
+            }
+            if (r < rounds) {
+                ct.out = s->cont[r & 1].as<float4>();
+                ct.out_count = cnt + 16 * std::min(r, 15);
+                ct.park_min = park_min;
+                e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), st);
+                if (e != hipSuccess) break;
+            }
+            e = launch(ct, n_units);
+        }
+    };
+    auto spec = [&](int mode) {
+        return [&, mode](const rtk::Cont &ct, uint32_t n) {
+            return rtk::launch_iow03_spec(f, scene, R, mode, ct, n, s->counter.as<unsigned>(), cap_s, st);
+        };
+    };
+    // sample 0 of every pixel (exact), then the other samples heaviest pixel first, assuming
+    // the stack state sample 0 left behind
+    if (e == hipSuccess) pass(spec(rtk::kSpecFirst), P, cap_s);
+    if (S > 1) {
+        // RT_SPEC_PRIOR=1: guess the scene prior for entries sample 0 left unwritten (fewer first-pass
+        // misses, but measured to form long re-execution chains); default: zero, as sample 0 saw them
+        const float prior = env_int("RT_SPEC_PRIOR", 0) ? s->ri_prior : 0.0f;
+        if (e == hipSuccess) e = rtk::launch_iow03_prep(f, R, s->ws_cost.as<unsigned>(), prior, st);
+        if (e == hipSuccess)
+            e = rtk::sort_units_by_cost(s->ws_cost.as<unsigned>(), s->ws_keys.as<unsigned>(), s->ws_iota.as<unsigned>(),
+                                        s->ws_order.as<unsigned>(), P, s->ws_temp.p, s->ws_temp_bytes, st);
+        if (e == hipSuccess) pass(spec(rtk::kSpecRest), P * (S - 1), cap_s);
+    }
+    const bool sort_first = env_int("RT_SPEC_SORT", 1) != 0;
+    for (int it = 0; it < iters && e == hipSuccess; it++) {
+        e = hipMemsetAsync(sc, 0, sizeof(unsigned), st);
+        if (e == hipSuccess) e = rtk::launch_iow03_resolve(f, R, false, nullptr, st);
+        if (it == 0 && sort_first && e == hipSuccess) {
+            // the first re-execution list holds the long samples: run it longest first (LPT),
+            // keyed by each sample's ray count in its speculative run
+            const size_t n = size_t(P) * S;
+            e = rtk::spec_list_keys(R, s->sp_keys.as<unsigned>(), n, st);
+            if (e == hipSuccess)
+                e = rtk::sort_pairs_desc(s->sp_keys.as<unsigned>(), s->sp_keys2.as<unsigned>(), R.list,
+                                         s->sp_list2.as<unsigned>(), n, s->sp_temp.p, s->sp_temp_bytes, 24, st);
+            rtk::SpecRecs R2 = R;
+            R2.list = s->sp_list2.as<uint32_t>();
+            if (e == hipSuccess)
+                pass([&](const rtk::Cont &ct, uint32_t nu) {
+                    return rtk::launch_iow03_spec(f, scene, R2, rtk::kSpecList, ct, nu, s->counter.as<unsigned>(),
+                                                  cap_s, st);
+                }, P * S, cap_s);
+        } else if (e == hipSuccess) pass(spec(rtk::kSpecList), P * S, cap_s);
+    }
+    if (e == hipSuccess) e = hipMemsetAsync(sc + 16, 0, sizeof(unsigned), st);
+    if (e == hipSuccess) e = rtk::launch_iow03_resolve(f, R, true, s->ws_state.as<float4>(), st);
+    // leftovers: the sequential kernel from each pixel's first unresolved sample
+    rtk::Chunk ch{};
+    ch.s_begin = 0;
+    ch.s_end = int(S);
+    ch.final_chunk = 1;
+    ch.state = s->ws_state.as<float4>();
+    ch.order = R.fb_list;
+    ch.order_count = R.fb_count;
+    ch.per_unit_begin = 1;
+    if (e == hipSuccess)
+        pass([&](const rtk::Cont &ct, uint32_t n) {
+            return rtk::launch_iow03(f, scene, ch, ct, n, s->counter.as<unsigned>(), s->s_stop, cap_q, st);
+        }, P, cap_q);
     if (e != hipSuccess) {
         std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
         return RT_E_HIP;
@@ -399,6 +555,34 @@ int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 // Diagnostics (not part of the reference's surface): pass a device buffer of 8 u64 to make
 // the kernels tally lane occupancy per phase; NULL turns it off.
+int rt_debug_pixel_rays(uint32_t *d_buf) {
+    g_px_rays = d_buf;
+    return RT_OK;
+}
+
+int rt_debug_rounds(rt_dev_scene *s, uint32_t *out, int cap) {
+    if (!s || !out || cap <= 0) return RT_E_ARG;
+    if (!s->cont_count.p) return 0;
+    std::vector<unsigned> v(16 * 16);
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(v.data(), s->cont_count.p, v.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+    const int n = std::min(cap, 16);
+    for (int r = 0; r < n; r++) out[r] = v[size_t(16) * r];
+    return n;
+}
+
+int rt_debug_spec_hist(rt_dev_scene *s, uint64_t *out) {
+    if (!s || !out) return RT_E_ARG;
+    std::memset(out, 0, 66 * sizeof(uint64_t));
+    if (!s->spec_cap) return RT_OK;
+    DevBuf d;
+    HIP_OK(d.alloc(66 * sizeof(uint64_t)));
+    HIP_OK(hipMemset(d.p, 0, 66 * sizeof(uint64_t)));
+    HIP_OK(rtk::spec_hist(s->sp_ctr.as<uint4>(), s->spec_cap, d.as<unsigned long long>(), nullptr));
+    HIP_OK(hipMemcpy(out, d.p, 66 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
 int rt_debug_counters(uint64_t *d_buf) {
     g_dbg = reinterpret_cast<unsigned long long *>(d_buf);
     return RT_OK;

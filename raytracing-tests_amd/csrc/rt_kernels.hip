@@ -344,6 +344,9 @@ struct IowStack {
     float *base;          // LDS, [slot][thread]
     unsigned char *bb;    // NARROW: LDS, [entry][thread]
     int size;
+    // sample-parallel mode: entries written by this sample, and entries whose stale RI this
+    // sample read before writing them (its dependence on the previous sample's stack)
+    unsigned wmask = 0, rmask = 0;
     __device__ __forceinline__ float &at(int entry, int k) { return base[(entry * kSlot + k) * kBlock]; }
     __device__ __forceinline__ int bounced(int e) {
         if constexpr (NARROW) return bb[e * kBlock];
@@ -358,6 +361,7 @@ struct IowStack {
             at(size, 0) = o.x; at(size, 1) = o.y; at(size, 2) = o.z;
             at(size, 3) = d.x; at(size, 4) = d.y; at(size, 5) = d.z;
             at(size, 6) = contrib; at(size, 7) = ri; set_bounced(size, b);
+            wmask |= 1u << size;
             size++;
         } else c.drops++;
     }
@@ -386,6 +390,7 @@ __device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, I
             int pi = K.size - 1 - skip;
             float parent = (pi < 0) ? 1.0f : (pi < kIowStack ? K.at(pi, 7) : 0.0f);
             target_ri = cos_t > 0.0f ? parent : data.material.z;
+            if (cos_t > 0.0f && pi >= 0 && pi < kIowStack && !((K.wmask >> pi) & 1u)) K.rmask |= 1u << pi;
         }
         float rr = (ri * rcp(target_ri)) * sin_t;
         float refr_c = data.material.x, refl_c = data.material.y;
@@ -512,7 +517,7 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
         if ((threadIdx.x & 63) < kDbgSlots) c.wdbg[threadIdx.x & 63] = 0;
     }
     Stack K{lds + threadIdx.x, lds_b + threadIdx.x, 0};
-    const uint32_t total = ct.in ? *ct.in_count : units_total(f);
+    const uint32_t total = ct.in ? *ct.in_count : (ch.order_count ? *ch.order_count : units_total(f));
     const bool may_park = ct.out != nullptr && total >= ct.park_min;
     const int W = f.W, H = f.H, spp = f.spp;
     const int s_end = ch.s_end < s_stop ? ch.s_end : s_stop;
@@ -557,7 +562,7 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
                     busy = true;
                     sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
                     sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
-                    s = ch.s_begin;
+                    s = ch.per_unit_begin ? __float_as_int(ch.state[2 * (size_t)unit].w) : ch.s_begin;
                     K.size = 0;
                     urays = 0;
                     if (s == 0) {
@@ -622,6 +627,7 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
                 ch.state[2 * (size_t)unit + 1] = make_float4(K.at(0, 7), K.at(1, 7), K.at(2, 7), K.at(3, 7));
             }
             if (ch.cost) ch.cost[unit] = urays;
+            if (f.px_rays) f.px_rays[unit] = urays;
             busy = false;
         }
     }
@@ -637,6 +643,203 @@ __global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, Chunk ch,
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
 void k_iow03n(Frame f, IowScene S, Chunk ch, Cont ct, unsigned *counter, int s_stop) {
     iow03_body<true>(f, S, ch, ct, counter, s_stop);
+}
+
+// ============================================================================ IOW-03, sample-parallel
+// One unit = one sample of one pixel (u = s*P + pu), so a heavy pixel's samples run on many
+// lanes at once instead of one after another.  Exactness: a sample's result is a function of
+// the pixel, the sample index and the RI left in stack entries 1..3 by the samples before it
+// (entry 0 is always written before any read).  The sample runs with an assumed value for
+// those entries (zeros in the first pass, else what the last resolve computed) and records
+// which entries it read before writing (rmask) and which it wrote (wmask); the resolve replays
+// the pixel in sample order and re-queues exactly the samples whose assumption was wrong.
+template <bool NARROW>
+__device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, const SpecRecs &R, int mode,
+                                            const Cont &ct, unsigned *counter) {
+    using Stack = IowStack<NARROW>;
+    constexpr int kFl = kIowStack * Stack::kSlot;
+    constexpr int BCAP = (NARROW ? 12 : kIowBvhStack) - 3;
+    __shared__ float lds[kFl * kBlock];
+    __shared__ unsigned char lds_b[NARROW ? kIowStack * kBlock : 1];
+    __shared__ short lds_bvh[(NARROW ? 12 : kIowBvhStack) * kBlock];
+    short *bstk = lds_bvh + threadIdx.x;
+    __shared__ unsigned long long s_dbg[kBlock / 64][kDbgSlots];
+    Ctr c;  // per unit here: written to the unit's record, never flushed
+    if (f.dbg) {
+        c.wdbg = s_dbg[threadIdx.x >> 6];
+        if ((threadIdx.x & 63) < kDbgSlots) c.wdbg[threadIdx.x & 63] = 0;
+    }
+    Stack K{lds + threadIdx.x, lds_b + threadIdx.x, 0};
+    const uint32_t total = ct.in ? *ct.in_count
+                         : (mode == kSpecList ? *R.list_count : (mode == kSpecFirst ? R.P : R.P * (R.S - 1)));
+    const bool may_park = ct.out != nullptr && total >= ct.park_min;
+    const int W = f.W, H = f.H, spp = f.spp;
+    int grid = 1;
+    while (grid * grid < spp) grid++;
+    const float aspect = (float)W * rcp((float)H);
+    const float dsx = aspect * rcp((float)(W * grid));
+    const float dsy = 1.0f * rcp((float)(H * grid));
+    bool live = true, busy = false;
+    uint32_t u = 0, urays = 0;
+    int skip = 0;
+    f3 sample = f3{0, 0, 0};
+    for (;;) {
+        const uint32_t q = fetch_unit(counter, live && !busy);
+        if (live && !busy) {
+            if (q >= total) live = false;
+            else if (ct.in) {  // resume a parked lane
+                const float4 *p = ct.in + (size_t)q * kContSlots;
+                const float4 m = p[0], a = p[1], b = p[2];
+                u = __float_as_uint(m.x); skip = __float_as_int(m.y); K.size = __float_as_int(m.z);
+                K.wmask = __float_as_uint(m.w) & 15u; K.rmask = __float_as_uint(m.w) >> 4;
+                sample = f3{a.x, a.y, a.z}; urays = __float_as_uint(a.w);
+                c.seg = __float_as_uint(b.x); c.nodes = __float_as_uint(b.y); c.prims = __float_as_uint(b.z);
+                c.drops = __float_as_uint(b.w) & 0xffffu; c.nans = __float_as_uint(b.w) >> 16;
+                const float *fl = reinterpret_cast<const float *>(p + 3);
+                for (int k = 0; k < kFl; k++) K.base[k * kBlock] = fl[k];
+                if constexpr (NARROW)
+                    for (int e = 0; e < kIowStack; e++) K.set_bounced(e, __float_as_int(fl[kFl + e]));
+                busy = true;
+            } else {
+                // kSpecFirst: sample 0 of every pixel; kSpecRest: samples 1.. pixel-major, pixels
+                // in R.order (heaviest sample 0 first); kSpecList: the re-execution list
+                u = mode == kSpecList ? R.list[q]
+                    : (mode == kSpecFirst ? q : (1u + q % (R.S - 1)) * R.P + R.order[q / (R.S - 1)]);
+                const uint32_t pu = u % R.P;
+                const int s = (int)(u / R.P);
+                const UnitPix px = unit_pixel(f, pu);
+                if (px.in_image) {
+                    busy = true;
+                    c.seg = c.nodes = c.prims = c.drops = c.nans = 0;
+                    urays = 0;
+                    skip = 0;
+                    sample = f3{0, 0, 0};
+                    K.size = 0; K.wmask = 0; K.rmask = 0;
+                    const float4 a = mode == kSpecFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : R.assume[u];
+                    K.at(0, 7) = 0.0f; K.at(1, 7) = a.x; K.at(2, 7) = a.y; K.at(3, 7) = a.z;
+                    const float sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
+                    const float sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
+                    f3 ro, rd;
+                    iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
+                    if (f.show_normal) {  // one ray, no stack: the normal is the sample
+                        sample = iow_launch_ray<BCAP>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
+                        urays = 1;
+                    } else K.push(ro, rd, 1.0f, 1.0f, 0, c);
+                }
+            }
+        }
+        if (__ballot(live) == 0) break;
+        if (may_park && __ballot(!live) != 0 && __popcll(__ballot(busy)) < kParkBelow) {
+            const uint32_t slot = park_slot(ct.out_count, busy);
+            if (busy) {
+                float4 *p = ct.out + (size_t)slot * kContSlots;
+                p[0] = make_float4(ubits(u), ibits(skip), ibits(K.size), ubits(K.wmask | (K.rmask << 4)));
+                p[1] = make_float4(sample.x, sample.y, sample.z, ubits(urays));
+                p[2] = make_float4(ubits(c.seg), ubits(c.nodes), ubits(c.prims), ubits(c.drops | (c.nans << 16)));
+                float *fl = reinterpret_cast<float *>(p + 3);
+                for (int k = 0; k < kFl; k++) fl[k] = K.base[k * kBlock];
+                if constexpr (NARROW)
+                    for (int e = 0; e < kIowStack; e++) fl[kFl + e] = ibits(K.bounced(e));
+            }
+            break;
+        }
+        DBG_TALLY(f, c, kDbgOuter, busy);
+        DBG_TALLY(f, c, kDbgSeg, busy && K.size > 0);
+        DBG_T0(f, t_seg);
+        if (busy && K.size > 0) {
+            iow_segment(S, f, K, skip, sample, (int)(u / R.P), c, bstk);
+            urays++;
+        }
+        DBG_CYC(f, c, kDbgCycSeg, t_seg);
+        if (busy && K.size == 0) {  // sample done: record it
+            R.col[u] = make_float4(sample.x, sample.y, sample.z, ubits(K.rmask | (K.wmask << 4)));
+            R.fin[u] = make_float4(K.at(1, 7), K.at(2, 7), K.at(3, 7), ubits(c.prims));
+            R.ctr[u] = make_uint4(c.seg, c.drops, c.nans, c.nodes);
+            busy = false;
+        }
+    }
+    if (c.wdbg && (threadIdx.x & 63) == 0)
+        for (int i = 0; i < kDbgSlots; i++) atomicAdd(f.dbg + i, c.wdbg[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_iow03s(Frame f, IowScene S, SpecRecs R, int mode, Cont ct,
+                                                   unsigned *counter) {
+    iow03s_body<false>(f, S, R, mode, ct, counter);
+}
+
+// After the sample-0 pass: every later sample of a pixel assumes, for each stack entry 1..3,
+// the RI sample 0 left there, or `prior` where sample 0 never wrote it (a guess, checked by
+// the resolve; `prior` is the scene's most common refractive index, the value such entries
+// almost always hold once any sample has pushed there).  Pixels are keyed by sample 0's ray
+// count so the rest run heaviest first.
+__global__ __launch_bounds__(kBlock) void k_iow03_prep(Frame f, SpecRecs R, unsigned *key, float prior) {
+    const uint32_t pu = blockIdx.x * kBlock + threadIdx.x;
+    if (pu >= R.P) return;  // no cross-lane work in this kernel
+    const UnitPix px = unit_pixel(f, pu);
+    if (!px.in_image) { key[pu] = 0; return; }
+    const uint32_t wm = (__float_as_uint(R.col[pu].w) >> 4) & 15u;
+    const float4 fn = R.fin[pu];
+    const float4 e = make_float4((wm & 2u) ? fn.x : prior, (wm & 4u) ? fn.y : prior, (wm & 8u) ? fn.z : prior, 0.0f);
+    for (uint32_t s = 1; s < R.S; s++) R.assume[(size_t)s * R.P + pu] = e;
+    key[pu] = R.ctr[pu].x;
+}
+
+// Replay of each pixel's samples in order (one lane per pixel unit; records are [s][pu], so
+// consecutive lanes read consecutive records).
+__global__ __launch_bounds__(kBlock) void k_iow03_resolve(Frame f, SpecRecs R, int final_pass, float4 *state) {
+    const uint32_t pu = blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = pu < R.P;
+    const UnitPix px = unit_pixel(f, valid ? pu : 0);
+    bool work = valid && px.in_image;
+    uint32_t E1 = 0, E2 = 0, E3 = 0;  // exact RI bits of entries 1..3 before sample s
+    f3 fc = f3{0, 0, 0};
+    unsigned long long seg = 0, drops = 0, nans = 0, nodes = 0, prims = 0;
+    int first_bad = -1;
+    uint32_t s = 0;
+    for (; work && s < R.S; s++) {
+        const size_t u = (size_t)s * R.P + pu;
+        const float4 cl = R.col[u];
+        const uint32_t fl = __float_as_uint(cl.w), rm = fl & 15u, wm = (fl >> 4) & 15u;
+        const float4 a = R.assume[u];
+        const bool bad = ((rm & 2u) && __float_as_uint(a.x) != E1) || ((rm & 4u) && __float_as_uint(a.y) != E2) ||
+                         ((rm & 8u) && __float_as_uint(a.z) != E3);
+        if (bad) {
+            if (first_bad < 0) first_bad = (int)s;
+            if (final_pass) break;  // the sequential kernel takes over from here
+            R.assume[u] = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
+            R.list[atomicAdd(R.list_count, 1u)] = (uint32_t)u;
+        }
+        if (first_bad < 0) {  // still exact: accumulate in sample order
+            fc = fc + f3{cl.x, cl.y, cl.z};
+            const uint4 ct4 = R.ctr[u];
+            seg += ct4.x; drops += ct4.y; nans += ct4.z; nodes += ct4.w;
+            prims += __float_as_uint(R.fin[u].w);
+        }
+        const float4 fn = R.fin[u];  // the record's own outputs (a guess while it is queued)
+        if (wm & 2u) E1 = __float_as_uint(fn.x);
+        if (wm & 4u) E2 = __float_as_uint(fn.y);
+        if (wm & 8u) E3 = __float_as_uint(fn.z);
+    }
+    if (final_pass && valid && !px.in_image) write_px(f, px, f3{0, 0, 0}, 0.0f);  // tile padding
+    if (final_pass && work) {
+        if (first_bad < 0) {
+            write_px(f, px, fc * rcp((float)R.S), 0.0f);
+            if (f.px_rays) f.px_rays[pu] = (unsigned)seg;
+        } else {  // resume state for the sequential kernel: colour sum, first sample, stack RI
+            state[2 * (size_t)pu] = make_float4(fc.x, fc.y, fc.z, __int_as_float(first_bad));
+            state[2 * (size_t)pu + 1] = make_float4(0.0f, __uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3));
+            R.fb_list[atomicAdd(R.fb_count, 1u)] = pu;
+        }
+    }
+    if (final_pass && f.counters) {
+        const unsigned long long v[5] = {seg, nodes, prims, drops, nans};
+        const int slot[5] = {0, 1, 2, 4, 5};
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const unsigned long long t = wave_sum(v[i]);
+            if ((threadIdx.x & 63) == 0 && t) atomicAdd(f.counters + slot[i], t);
+        }
+    }
 }
 
 // ============================================================================ INW
@@ -1011,6 +1214,7 @@ int resident_blocks_per_cu(int kind) {
     hipError_t e;
     if (kind == 3) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03, kBlock, 0);
     else if (kind == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03n, kBlock, 0);
+    else if (kind == 5) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03s, kBlock, 0);
     else if (kind == 14) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<true>, kBlock, 0);
     else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<false>, kBlock, 0);
     return (e == hipSuccess && nb > 0) ? nb : 2;
@@ -1027,6 +1231,48 @@ hipError_t launch_iow03(const Frame &f, const IowScene &sc, const Chunk &ch, con
     const dim3 g(grid_of(n_units, blocks_cap));
     if (iow_narrow(f)) hipLaunchKernelGGL(k_iow03n, g, dim3(kBlock), 0, s, f, sc, ch, ct, counter, s_stop);
     else hipLaunchKernelGGL(k_iow03, g, dim3(kBlock), 0, s, f, sc, ch, ct, counter, s_stop);
+    return hipGetLastError();
+}
+hipError_t launch_iow03_spec(const Frame &f, const IowScene &sc, const SpecRecs &R, int mode, const Cont &ct,
+                             uint32_t n_units, unsigned *counter, int blocks_cap, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_iow03s, dim3(grid_of(n_units, blocks_cap)), dim3(kBlock), 0, s, f, sc, R, mode, ct, counter);
+    return hipGetLastError();
+}
+// diagnostics: log2 histogram of rays per sample over the last sample-parallel render
+__global__ void k_spec_hist(const uint4 *ctr, size_t n, unsigned long long *out) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const unsigned v = ctr[i].x;
+        if (v == 0) continue;
+        const int b = 31 - __clz(v);
+        atomicAdd(out + 2 + b, 1ull);
+        atomicAdd(out + 34 + b, (unsigned long long)v);
+        atomicMax(out, (unsigned long long)v);
+        atomicAdd(out + 1, 1ull);
+    }
+}
+hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipStream_t s) {
+    hipLaunchKernelGGL(k_spec_hist, dim3(2048), dim3(256), 0, s, ctr, n, d_out);
+    return hipGetLastError();
+}
+__global__ void k_spec_list_keys(SpecRecs R, unsigned *keys, size_t n) {
+    const unsigned cnt = *R.list_count;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        keys[i] = i < cnt ? min(R.ctr[R.list[i]].x, 0xffffffu) : 0u;
+}
+hipError_t spec_list_keys(const SpecRecs &R, unsigned *keys, size_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_spec_list_keys, dim3(4096), dim3(256), 0, s, R, keys, n);
+    return hipGetLastError();
+}
+hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, hipStream_t s) {
+    const unsigned blocks = (R.P + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_iow03_prep, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, key, prior);
+    return hipGetLastError();
+}
+hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pass, float4 *state, hipStream_t s) {
+    const unsigned blocks = (R.P + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_iow03_resolve, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, final_pass ? 1 : 0, state);
     return hipGetLastError();
 }
 hipError_t launch_inw(const Frame &f, const InwScene &sc, const Chunk &ch, const Cont &ct, uint32_t n_units,

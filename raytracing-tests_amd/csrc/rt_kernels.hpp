@@ -21,6 +21,7 @@ struct Frame {
     float sphere[4];    // IOW-01 only
     unsigned long long *dbg;  // optional lane-occupancy counters (kDbg* slots), null in production
     int leaf_batch;           // IOW-03 walk: test postponed leaves once this many lanes hold one
+    unsigned *px_rays;        // optional: rays cast per work unit, written when its pixel completes
 };
 // lane-occupancy counters (per wave-iteration: 1 and popcount of the participating lanes)
 enum { kDbgOuter = 0, kDbgOuterLanes, kDbgTrav, kDbgTravLanes, kDbgLeaf, kDbgLeafLanes, kDbgSeg, kDbgSegLanes,
@@ -67,7 +68,28 @@ struct Chunk {
     float4 *state;           // 2 float4 per unit (may be null for a single-chunk render)
     const unsigned *order;   // unit permutation or null (natural order)
     unsigned *cost;          // rays per unit in this launch, or null
+    const unsigned *order_count;  // device count of `order` entries (null: all units)
+    int per_unit_begin;      // first sample of each unit = bits of state[2*unit].w (else s_begin)
 };
+
+// Sample-parallel IOW-03 (DESIGN.md "Sample-parallel speculation").  A unit is one (pixel,
+// sample) pair, u = s*P + pu.  Each sample runs with an assumed incoming stack state (the RI
+// of entries 1..3 that earlier samples of the pixel left behind) and records what it read and
+// wrote; a resolve pass replays the pixel's samples in order and re-queues every sample whose
+// assumption was wrong.  Records are SoA over u.
+struct SpecRecs {
+    float4 *col;       // rgb of the sample, flags (bits: rmask 0-3, wmask 4-7)
+    float4 *fin;       // RI of entries 1..3 after the sample, prim tests (bits)
+    uint4 *ctr;        // segments, stack drops, NaN directions, node visits
+    float4 *assume;    // assumed RI of entries 1..3 before the sample
+    uint32_t P, S;     // pixel units, samples per pixel (s_stop)
+    uint32_t *list;    // re-execution list (units)
+    unsigned *list_count;
+    uint32_t *fb_list; // pixels left to the sequential kernel after the last resolve
+    unsigned *fb_count;
+    const uint32_t *order;  // pixel units, heaviest sample 0 first (kSpecRest)
+};
+enum { kSpecFirst = 0, kSpecRest = 1, kSpecList = 2 };
 
 // Tail compaction between launches.  Once the work queue is empty, a wave whose busy lanes
 // fall below kParkBelow parks them (state at a ray-segment boundary) in `out`, slot ids from
@@ -95,9 +117,19 @@ hipError_t launch_inw(const Frame &f, const InwScene &sc, const Chunk &ch, const
                       unsigned *counter, int blocks_cap, hipStream_t s);
 uint32_t units_of(const Frame &f);
 // resident 256-thread blocks per CU for the persistent kernels (occupancy query)
+// sample-parallel IOW-03 pass over the units of `mode` (kSpec*)
+hipError_t launch_iow03_spec(const Frame &f, const IowScene &sc, const SpecRecs &R, int mode, const Cont &ct,
+                             uint32_t n_units, unsigned *counter, int blocks_cap, hipStream_t s);
+hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipStream_t s);  // diagnostics
+// after the kSpecFirst pass: assumptions for samples 1.. and the per-pixel ordering keys
+hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, hipStream_t s);
+// replay each pixel's samples: re-queue wrong assumptions; final: write clean pixels, hand
+// the rest (with their resume state in `state`) to the sequential kernel via R.fb_list
+hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pass, float4 *state, hipStream_t s);
+
 // resident blocks per CU of the render kernel for `kind` (3 = IOW-03 wide, 4 = IOW-03 narrow,
 // 11/14 = INW layout 1/4)
-int resident_blocks_per_cu(int kind);
+int resident_blocks_per_cu(int kind);  // 5 = sample-parallel IOW-03
 // IOW-03 kernel variant for this frame: narrow (byte bounce counts, 12-deep BVH stack, 4 waves
 // per SIMD with spills) when RT_IOW_NARROW=1 and u_NumOfBounce <= 255; wide otherwise
 bool iow_narrow(const Frame &f);
@@ -105,5 +137,12 @@ bool iow_narrow(const Frame &f);
 hipError_t sort_units_by_cost(const unsigned *cost, unsigned *keys_tmp, const unsigned *iota, unsigned *order,
                               uint32_t n, void *temp, size_t temp_bytes, hipStream_t s);
 size_t sort_temp_bytes(uint32_t n);
+// descending key/value radix sort over bits [0, end_bit)
+size_t sort_pairs_temp_bytes(size_t n, int end_bit);
+hipError_t sort_pairs_desc(const unsigned *keys_in, unsigned *keys_out, const unsigned *vals_in, unsigned *vals_out,
+                           size_t n, void *temp, size_t temp_bytes, int end_bit, hipStream_t s);
+// keys for ordering the re-execution list longest-first: the ray count of each listed unit's
+// previous execution (0 beyond the list's count)
+hipError_t spec_list_keys(const SpecRecs &R, unsigned *keys, size_t n, hipStream_t s);
 
 }  // namespace rtk

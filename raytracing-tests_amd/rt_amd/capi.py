@@ -93,6 +93,9 @@ SIGNATURES = {
     "rt_pack_inw": (C.c_int, [C.POINTER(RtGeomDesc), C.c_uint32, C.c_int, _FP, _FP, _FP, _U32P]),
     "rt_sample_tables": (C.c_int, [C.c_int, _FP, _FP, _IP]),
     "rt_debug_counters": (C.c_int, [C.c_void_p]),
+    "rt_debug_pixel_rays": (C.c_int, [C.c_void_p]),
+    "rt_debug_rounds": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    "rt_debug_spec_hist": (C.c_int, [C.c_void_p, C.c_void_p]),
 }
 
 _lib = None

@@ -2,7 +2,9 @@
 
 - RT_IOW_LINEAR=1: the reference's linear object loop instead of the culling BVH;
 - RT_IOW_NARROW=1: the byte-bounce stack layout (12-deep BVH stack) instead of the 9-float one;
-- RT_ROUNDS=0:     no tail compaction (no parking / resume launches).
+- RT_ROUNDS=0:     no tail compaction (no parking / resume launches);
+- RT_IOW_SPEC=0:   the sequential per-pixel kernel instead of sample-parallel speculation;
+- RT_SPEC_ITERS=0/1: fewer resolve passes, so more pixels finish on the sequential kernel.
 Each must give a bit-identical image of the final scene with identical ray counts.  The
 renders run in subprocesses because the switches are read by the library at scene build /
 launch time."""
@@ -31,7 +33,7 @@ print(json.dumps(st))
 def _render(tmp_path, over, w, h, spp):
     out = str(tmp_path / f"img_{len(os.listdir(tmp_path))}.npy")
     env = dict(os.environ)
-    for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS"):
+    for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS", "RT_IOW_SPEC", "RT_SPEC_ITERS"):
         env.pop(k, None)
     env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out)
@@ -45,7 +47,10 @@ def _render(tmp_path, over, w, h, spp):
     ({"RT_IOW_LINEAR": "1"}, 1200, 800, 1),
     ({"RT_IOW_NARROW": "1"}, 600, 400, 8),
     ({"RT_ROUNDS": "0"}, 600, 400, 8),
-    ({"RT_CHUNKS": "lpt"}, 300, 200, 24),
+    ({"RT_CHUNKS": "lpt", "RT_IOW_SPEC": "0"}, 300, 200, 24),
+    ({"RT_IOW_SPEC": "0"}, 600, 400, 8),
+    ({"RT_SPEC_ITERS": "0"}, 300, 200, 16),
+    ({"RT_SPEC_ITERS": "1"}, 300, 200, 16),
 ])
 def test_strategies_bit_identical(tmp_path, gpu, over, w, h, spp):
     a, sa = _render(tmp_path, {}, w, h, spp)

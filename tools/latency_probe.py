@@ -1,0 +1,32 @@
+"""Single-pixel latency probe: find the heaviest pixel of a central region, then time it alone
+(sequential kernel vs sample-parallel) to measure per-segment latency of a lone lane."""
+import ctypes as C, os, sys, time, json
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "raytracing-tests_amd")]
+import numpy as np, torch
+import rt_amd as R
+lib = R.load()
+sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0)
+W, H = sc.params.width, sc.params.height
+x0, y0, tw, th = W // 2 - 64, H // 2 - 64, 128, 128
+units = ((tw + 7) // 8) * ((th + 7) // 8) * 64
+pr = torch.zeros(units, dtype=torch.int32, device="cuda")
+lib.rt_debug_pixel_rays(pr.data_ptr())
+p = R.RtParams(); C.memmove(C.addressof(p), C.addressof(sc.params), C.sizeof(p))
+p.tile_x0, p.tile_y0, p.tile_w, p.tile_h = x0, y0, tw, th
+os.environ["RT_IOW_SPEC"] = "0"
+R.render(sc, p)
+lib.rt_debug_pixel_rays(None)
+u = int(torch.argmax(pr).item()); mx = int(pr.max().item())
+b, l = u >> 6, u & 63; nbx = (tw + 7) >> 3
+px, py = x0 + (b % nbx) * 8 + (l & 7), y0 + (b // nbx) * 8 + (l >> 3)
+out = {"pixel": [px, py], "rays": mx}
+for mode in ("0", "1"):
+    os.environ["RT_IOW_SPEC"] = mode
+    q = R.RtParams(); C.memmove(C.addressof(q), C.addressof(sc.params), C.sizeof(q))
+    q.tile_x0, q.tile_y0, q.tile_w, q.tile_h = px, py, 1, 1
+    R.render(sc, q)
+    t0 = time.perf_counter(); _, _, st = R.render(sc, q); dt = time.perf_counter() - t0
+    out["spec" + mode] = {"ms": st["ms"], "wall_ms": dt * 1e3, "segments": st["segments"],
+                          "us_per_segment": st["ms"] * 1e3 / max(1, st["segments"])}
+print(json.dumps(out))
