@@ -127,9 +127,16 @@ hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, f
 // the rest (with their resume state in `state`) to the sequential kernel via R.fb_list
 hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pass, float4 *state, hipStream_t s);
 
+// sample-parallel INW over samples [s0, s0+ns) of every pixel (records indexed (s-s0)*P + pu),
+// then End() over that chunk: carry the sum in `state` or write the pixels
+hipError_t launch_inw_spec(const Frame &f, const InwScene &sc, const SpecRecs &R, int s0, int ns, const Cont &ct,
+                           uint32_t n_units, unsigned *counter, int blocks_cap, hipStream_t s);
+hipError_t launch_inw_fin(const Frame &f, const SpecRecs &R, int s0, int ns, bool final_chunk, float4 *state,
+                          hipStream_t s);
+
 // resident blocks per CU of the render kernel for `kind` (3 = IOW-03 wide, 4 = IOW-03 narrow,
 // 11/14 = INW layout 1/4)
-int resident_blocks_per_cu(int kind);  // 5 = sample-parallel IOW-03
+int resident_blocks_per_cu(int kind);  // 5 = sample-parallel IOW-03, 6/7 = sample-parallel INW 1/4
 // IOW-03 kernel variant for this frame: narrow (byte bounce counts, 12-deep BVH stack, 4 waves
 // per SIMD with spills) when RT_IOW_NARROW=1 and u_NumOfBounce <= 255; wide otherwise
 bool iow_narrow(const Frame &f);

@@ -4,7 +4,8 @@
 - RT_IOW_NARROW=1: the byte-bounce stack layout (12-deep BVH stack) instead of the 9-float one;
 - RT_ROUNDS=0:     no tail compaction (no parking / resume launches);
 - RT_IOW_SPEC=0:   the sequential per-pixel kernel instead of sample-parallel speculation;
-- RT_SPEC_ITERS=0/1: fewer resolve passes, so more pixels finish on the sequential kernel.
+- RT_SPEC_ITERS=0/1: fewer resolve passes, so more pixels finish on the sequential kernel;
+- INW: RT_INW_SPEC=0 (per-pixel sequential samples) and RT_SPEC_MAX_GB tiny (sample chunks).
 Each must give a bit-identical image of the final scene with identical ray counts.  The
 renders run in subprocesses because the switches are read by the library at scene build /
 launch time."""
@@ -23,20 +24,28 @@ SCRIPT = r"""
 import sys, json, numpy as np
 sys.path[:0] = [{root!r}, {root!r} + '/raytracing-tests_amd']
 import rt_amd as R
-sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0, width={w}, height={h}, spp={spp})
-img, _, st = R.render(sc)
+sc = R.make_scene({preset}, {seed}, {n_hint}, width={w}, height={h}, spp={spp})
+img, depth, st = R.render(sc)
+if depth is not None:
+    img = np.concatenate([img, depth[..., None]], axis=2)
 np.save({out!r}, img)
 print(json.dumps(st))
 """
 
 
-def _render(tmp_path, over, w, h, spp):
+IOW = (2, 20250131, 0)     # PRESET_IOW03_FINAL
+INW1 = (4, 1234, 3000)     # PRESET_INW01_RANDOM, 3000 objects
+INW4 = (6, 7, 0)           # PRESET_INW04_CORNELL
+
+
+def _render(tmp_path, over, w, h, spp, scene=IOW):
     out = str(tmp_path / f"img_{len(os.listdir(tmp_path))}.npy")
     env = dict(os.environ)
-    for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS", "RT_IOW_SPEC", "RT_SPEC_ITERS"):
+    for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS", "RT_IOW_SPEC", "RT_SPEC_ITERS",
+              "RT_INW_SPEC", "RT_SPEC_MAX_GB"):
         env.pop(k, None)
     env.update(over)
-    code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out)
+    code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out, preset=scene[0], seed=scene[1], n_hint=scene[2])
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-2000:]
     return np.load(out), json.loads(r.stdout.strip().splitlines()[-1])
@@ -62,3 +71,16 @@ def test_strategies_bit_identical(tmp_path, gpu, over, w, h, spp):
     assert len(bad) == 0
     for k in ("segments", "stack_drops", "nan_drops"):
         assert sa[k] == sb[k], k
+
+
+@pytest.mark.parametrize("over,scene,w,h,spp", [
+    ({"RT_INW_SPEC": "0"}, INW1, 192, 108, 24),
+    ({"RT_SPEC_MAX_GB": "0.005"}, INW1, 192, 108, 24),   # forces several sample chunks
+    ({"RT_INW_SPEC": "0"}, INW4, 128, 128, 16),
+])
+def test_inw_strategies_bit_identical(tmp_path, gpu, over, scene, w, h, spp):
+    a, sa = _render(tmp_path, {}, w, h, spp, scene)
+    b, sb = _render(tmp_path, over, w, h, spp, scene)
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), np.argwhere(~same.all(axis=2))[:10].tolist()
+    assert sa == {**sb, "ms": sa["ms"]}
