@@ -37,8 +37,6 @@ import torch.distributed as dist  # noqa: E402
 import rt_amd as R  # noqa: E402
 
 TILE = 64
-# k_iow03 launches per frame: the pixel launch + RT_ROUNDS resume launches (tail compaction)
-LAUNCHES_PER_FRAME = 1 + max(0, int(os.environ.get("RT_ROUNDS", "6") or 6))
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (= f32 MFMA rate), MI355X_MICROARCH.md
 HBM_PEAK_GBPS = 8000.0     # MI355X HBM3E peak, MI355X_MICROARCH.md
 WORKLOAD = ("In-One-Weekend 03_Adding_Materials final scene (~500 random spheres + ground cuboid), "
@@ -183,19 +181,22 @@ def main():
     st = dict(zip(("segments", "node_visits", "prim_tests", "shadow_queries", "stack_drops", "nan_drops"), c))
     per_step = {k: v / args.steps for k, v in st.items()}
 
+    kname = C.create_string_buffer(64)
+    launches = max(1, lib.rt_debug_launches(scene, kname, 64))  # main-kernel launches per frame
+    kname = kname.value.decode()
     if rank == 0:
         value = st["segments"] / elapsed / 1e6
         flops = algorithmic_flops(per_step)
-        # per launch = per frame / LAUNCHES_PER_FRAME for both the flops and the duration
+        # per launch = per frame / launches for both the flops and the duration
         achieved = flops / (kernel_ms * 1e-3) / 1e12
-        balg = algorithmic_bytes(per_step, W * H / world) / LAUNCHES_PER_FRAME
+        balg = algorithmic_bytes(per_step, W * H / world) / launches
         traffic = None
         prof = os.path.join(ROOT, "profiles", "pmc_iow03.json")
         if os.path.exists(prof):
             try:
                 pm = json.load(open(prof))
                 if pm.get("config") == [W, H, spp]:
-                    if pm.get("launches_per_frame") == LAUNCHES_PER_FRAME:
+                    if pm.get("launches_per_frame") == launches and pm.get("kernel") == kname:
                         traffic = pm.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -220,12 +221,12 @@ def main():
                        "parallelism": f"tiles_rr{world}" + ("+rccl_gather" if world > 1 else "")},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                         "traffic": traffic, "kernel": "k_iow03", "launches_per_frame": LAUNCHES_PER_FRAME,
-                         "avg_launch_ms": round(kernel_ms / LAUNCHES_PER_FRAME, 3),
-                         "flops_per_launch": flops / LAUNCHES_PER_FRAME,
+                         "traffic": traffic, "kernel": kname, "launches_per_frame": launches,
+                         "avg_launch_ms": round(kernel_ms / launches, 3),
+                         "flops_per_launch": flops / launches,
                          "note": "VALU fp32 kernel (no MFMA on this path); peak = FP32 vector peak; "
                                  "traffic = PMC HBM bytes per launch from profiles/pmc_iow03.json"},
-            "hbm": {"achieved_GBps": round(balg / (kernel_ms / LAUNCHES_PER_FRAME * 1e-3) / 1e9, 1),
+            "hbm": {"achieved_GBps": round(balg / (kernel_ms / launches * 1e-3) / 1e9, 1),
                     "peak_GBps": HBM_PEAK_GBPS, "algorithmic_bytes_per_launch": balg},
             "mean_bounces": round(st["segments"] / (W * H * spp * args.steps), 3),
             "rays_per_step": int(per_step["segments"]),

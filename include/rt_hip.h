@@ -157,6 +157,9 @@ int rt_debug_rounds(rt_dev_scene *s, uint32_t *out, int cap);
  * out[0] = max, out[1] = samples, out[2+b] = samples with 2^b <= rays < 2^(b+1),
  * out[34+b] = rays in those samples.  66 entries. */
 int rt_debug_spec_hist(rt_dev_scene *s, uint64_t *out);
+/* Main render kernel of the scene's last render and how many times it was launched (the
+ * bench's per-launch roofline figures divide by this).  Returns the count; writes the name. */
+int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap);
 
 #ifdef __cplusplus
 }

@@ -119,6 +119,9 @@ struct rt_dev_scene {
     DevBuf sp_col, sp_fin, sp_ctr, sp_assume, sp_list, sp_fb, sp_counts;
     DevBuf sp_keys, sp_keys2, sp_list2, sp_temp;  // longest-first ordering of the re-execution list
     size_t sp_temp_bytes = 0;
+    // launches of the render's main kernel in the last render (rt_debug_launches)
+    int last_launches = 0;
+    const char *last_kernel = "";
 };
 
 namespace {
@@ -366,6 +369,8 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     }
     const std::vector<std::pair<int, int>> plan = chunk_plan(f.spp);
     const uint32_t units = rtk::units_of(f);
+    s->last_kernel = s->kind == 3 ? (rtk::iow_narrow(f) ? "k_iow03n" : "k_iow03") : (s->layout == 4 ? "k_inw<true>" : "k_inw<false>");
+    s->last_launches = int(plan.size()) * (1 + std::min(14, std::max(0, env_int("RT_ROUNDS", 6))));
     if (plan.size() > 1) {
         int rc = ensure_workspace(s, units);
         if (rc != RT_OK) return rc;
@@ -477,6 +482,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     };
     // sample 0 of every pixel (exact), then the other samples heaviest pixel first, assuming
     // the stack state sample 0 left behind
+    s->last_kernel = "k_iow03s";
+    s->last_launches = (1 + rounds) * (1 + (S > 1 ? 1 : 0) + iters);
     if (e == hipSuccess) pass(spec(rtk::kSpecFirst), P, cap_s);
     if (S > 1) {
         // RT_SPEC_PRIOR=1: guess the scene prior for entries sample 0 left unwritten (fewer first-pass
@@ -551,6 +558,8 @@ int launch_scene_inw_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st, int ns
     const int cap = s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 7 : 6);
     const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
     hipError_t e = hipSuccess;
+    s->last_kernel = s->layout == 4 ? "k_inw_s<true>" : "k_inw_s<false>";
+    s->last_launches = (1 + rounds) * ((f.spp + ns - 1) / ns);
     for (int s0 = 0; s0 < f.spp && e == hipSuccess; s0 += ns) {
         const int k = std::min(ns, f.spp - s0);
         for (int r = 0; r <= rounds && e == hipSuccess; r++) {
@@ -662,6 +671,15 @@ int rt_debug_spec_hist(rt_dev_scene *s, uint64_t *out) {
     HIP_OK(rtk::spec_hist(s->sp_ctr.as<uint4>(), s->spec_cap, d.as<unsigned long long>(), nullptr));
     HIP_OK(hipMemcpy(out, d.p, 66 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return RT_OK;
+}
+
+int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {
+    if (!s) return RT_E_ARG;
+    if (name_out && name_cap > 0) {
+        std::strncpy(name_out, s->last_kernel, size_t(name_cap) - 1);
+        name_out[name_cap - 1] = 0;
+    }
+    return s->last_launches;
 }
 
 int rt_debug_counters(uint64_t *d_buf) {

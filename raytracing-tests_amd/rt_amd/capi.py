@@ -96,6 +96,7 @@ SIGNATURES = {
     "rt_debug_pixel_rays": (C.c_int, [C.c_void_p]),
     "rt_debug_rounds": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     "rt_debug_spec_hist": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "rt_debug_launches": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
 }
 
 _lib = None

@@ -21,7 +21,8 @@ def collect(d, kernel):
     dispatches = collections.defaultdict(set)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if kernel in r.get("Kernel_Name", ""):
+            name = r.get("Kernel_Name", "")
+            if ("::" + kernel + "(") in name or name.startswith(kernel + "("):
                 agg[r["Counter_Name"]] += float(r["Counter_Value"])
                 dispatches[r["Counter_Name"]].add(r.get("Dispatch_Id", ""))
     return dict(agg), {k: len(v) for k, v in dispatches.items()}
