@@ -35,6 +35,7 @@
 #ifndef RT_HIP_H
 #define RT_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -113,6 +114,16 @@ int rt_render_inw(const float *geom /* N*28, layout 1 (BVH.h:12-19) or 4 (lights
 
 /* LBVH builder: aabbs = N*(min xyz, max xyz) in geometry order -> (2N-1)*8 floats. */
 int rt_lbvh_build(const float *aabbs, uint32_t n, float *nodes_out);
+
+/* The same LBVH built on the GPU, node-for-node identical to rt_lbvh_build:
+ * Morton keys + radix sort, the level merge as a Cartesian tree over the highest differing
+ * bits, bottom-up boxes, breadth-first numbering.  Device pointers; d_ws holds
+ * rt_lbvh_workspace_bytes(n) of scratch; never synchronises.  N <= 2^24 (ids are floats). */
+size_t rt_lbvh_workspace_bytes(uint32_t n);
+int rt_lbvh_build_async(const float *d_aabbs, uint32_t n, float *d_nodes_out, void *d_ws, size_t ws_bytes,
+                        void *stream);
+/* Blocking convenience wrapper (host buffers); *ms (may be NULL) receives the device time. */
+int rt_lbvh_build_gpu(const float *aabbs, uint32_t n, float *nodes_out, int device, double *ms);
 
 /* ---- asynchronous device entry points (bench / multi-GPU path) ---------------------
  * A prepared scene owns its device buffers (scene records, LBVH nodes, sample tables).

@@ -122,6 +122,23 @@ struct rt_dev_scene {
     // launches of the render's main kernel in the last render (rt_debug_launches)
     int last_launches = 0;
     const char *last_kernel = "";
+    // sample-parallel pipelines: one stream per pixel group, each with its own queue counter,
+    // continuation buffers and sort scratch (rt_render_* calls on one scene must not overlap)
+    struct GroupLane {
+        hipStream_t st = nullptr;
+        hipEvent_t done = nullptr;
+        DevBuf counter, cont[2], cont_count, temp;
+        size_t temp_bytes = 0;
+        ~GroupLane() {
+            if (done) (void)hipEventDestroy(done);
+            if (st) (void)hipStreamDestroy(st);
+        }
+    };
+    std::vector<std::unique_ptr<GroupLane>> lanes;
+    hipEvent_t ev_start = nullptr;
+    ~rt_dev_scene() {
+        if (ev_start) (void)hipEventDestroy(ev_start);
+    }
 };
 
 namespace {
@@ -300,6 +317,31 @@ int ensure_cont(rt_dev_scene *s) {
     return RT_OK;
 }
 
+// group lanes of the sample-parallel pipeline; temp_bytes = sort scratch each lane needs
+int ensure_lanes(rt_dev_scene *s, int groups, size_t temp_bytes) {
+    if (!s->ev_start) HIP_OK(hipEventCreateWithFlags(&s->ev_start, hipEventDisableTiming));
+    const size_t slots = size_t(s->blocks_cap) * rtk::kBlock;
+    while (s->lanes.size() < size_t(groups)) {
+        auto L = std::make_unique<rt_dev_scene::GroupLane>();
+        HIP_OK(hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking));
+        HIP_OK(hipEventCreateWithFlags(&L->done, hipEventDisableTiming));
+        HIP_OK(L->counter.alloc(64));
+        for (auto &b : L->cont) HIP_OK(b.alloc(slots * rtk::kContSlots * sizeof(float4)));
+        HIP_OK(L->cont_count.alloc(64 * 16));
+        s->lanes.push_back(std::move(L));
+    }
+    for (int g = 0; g < groups; g++) {
+        auto &L = *s->lanes[size_t(g)];
+        if (L.temp_bytes < temp_bytes) {
+            L.temp.~DevBuf();
+            new (&L.temp) DevBuf();
+            HIP_OK(L.temp.alloc(temp_bytes));
+            L.temp_bytes = temp_bytes;
+        }
+    }
+    return RT_OK;
+}
+
 // Sample-parallel records for P pixel units x S samples; false if they do not fit.
 bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
     const size_t n = size_t(P) * S;
@@ -317,7 +359,7 @@ bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
     if (s->sp_col.alloc(n * sizeof(float4)) != hipSuccess || s->sp_fin.alloc(n * sizeof(float4)) != hipSuccess ||
         s->sp_ctr.alloc(n * sizeof(uint4)) != hipSuccess || s->sp_assume.alloc(n * sizeof(float4)) != hipSuccess ||
         s->sp_list.alloc(n * sizeof(uint32_t)) != hipSuccess || s->sp_fb.alloc(size_t(P) * 4) != hipSuccess ||
-        s->sp_counts.alloc(256) != hipSuccess || s->sp_keys.alloc(n * 4) != hipSuccess ||
+        s->sp_counts.alloc(64 * 64) != hipSuccess || s->sp_keys.alloc(n * 4) != hipSuccess ||
         s->sp_keys2.alloc(n * 4) != hipSuccess || s->sp_list2.alloc(n * 4) != hipSuccess ||
         s->sp_temp.alloc(s->sp_temp_bytes = rtk::sort_pairs_temp_bytes(n, 24)) != hipSuccess) {
         s->spec_cap = s->spec_units = 0;
@@ -444,93 +486,119 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     if (rc != RT_OK) return rc;
     const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 6)));
     const int iters = std::max(0, env_int("RT_SPEC_ITERS", 10));
-    if (rounds > 0 && (rc = ensure_cont(s)) != RT_OK) return rc;
-    unsigned *cnt = s->cont_count.as<unsigned>();
-    unsigned *sc = s->sp_counts.as<unsigned>();  // [0] list count, [16] fallback count
-    rtk::SpecRecs R{s->sp_col.as<float4>(), s->sp_fin.as<float4>(), s->sp_ctr.as<uint4>(), s->sp_assume.as<float4>(),
-                    P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(), sc + 16, s->ws_order.as<uint32_t>()};
+    const int groups = S > 1 ? std::max(1, std::min(32, env_int("RT_SPEC_GROUPS", 1))) : 1;
+    const size_t gmax = size_t(P + groups - 1) / groups + 1;  // pixels in the largest group
+    if ((rc = ensure_cont(s)) != RT_OK) return rc;
+    if ((rc = ensure_lanes(s, groups, rtk::sort_pairs_temp_bytes(gmax * S, 24))) != RT_OK) return rc;
+    unsigned *sc = s->sp_counts.as<unsigned>();  // group g: [32g] list count, [32g+16] fallback count
+    const rtk::SpecRecs R{s->sp_col.as<float4>(), s->sp_fin.as<float4>(), s->sp_ctr.as<uint4>(),
+                          s->sp_assume.as<float4>(), P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(),
+                          sc + 16, s->ws_order.as<uint32_t>(), 0, 0};
     rtk::IowScene scene{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
                         s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link};
     const int cap_s = s->cus * rtk::resident_blocks_per_cu(5);
     const int cap_q = s->cus * rtk::resident_blocks_per_cu(3);
-    hipError_t e = hipMemsetAsync(R.assume, 0, size_t(P) * sizeof(float4), st);  // sample 0: exact zeros
-    // one compacted pass: the first launch takes `n0` units, resume launches the parked lanes
-    auto pass = [&](auto &&launch, uint32_t n0, int cap) {
+    hipError_t e = hipSuccess;
+    // one compacted pass on a stream with its own queue counter and continuation buffers: the
+    // first launch takes `n0` units, resume launches take the parked lanes
+    struct Lane { hipStream_t st; unsigned *counter; const DevBuf *cont; unsigned *cnt; };
+    auto pass = [&](const Lane &q, auto &&launch, uint32_t n0, int cap) {
         const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
         for (int r = 0; r <= rounds && e == hipSuccess; r++) {
             rtk::Cont ct{};
             uint32_t n_units = n0;
             if (r > 0) {
-                ct.in = s->cont[(r - 1) & 1].as<float4>();
-                ct.in_count = cnt + 16 * std::min(r - 1, 15);
+                ct.in = q.cont[(r - 1) & 1].as<float4>();
+                ct.in_count = q.cnt + 16 * std::min(r - 1, 15);
                 n_units = uint32_t(cap) * rtk::kBlock;
             }
             if (r < rounds) {
-                ct.out = s->cont[r & 1].as<float4>();
-                ct.out_count = cnt + 16 * std::min(r, 15);
+                ct.out = q.cont[r & 1].as<float4>();
+                ct.out_count = q.cnt + 16 * std::min(r, 15);
                 ct.park_min = park_min;
-                e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), st);
+                e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), q.st);
                 if (e != hipSuccess) break;
             }
-            e = launch(ct, n_units);
+            e = launch(q, ct, n_units);
         }
     };
-    auto spec = [&](int mode) {
-        return [&, mode](const rtk::Cont &ct, uint32_t n) {
-            return rtk::launch_iow03_spec(f, scene, R, mode, ct, n, s->counter.as<unsigned>(), cap_s, st);
+    auto spec = [&](const rtk::SpecRecs &RR, int mode) {
+        return [&, RR, mode](const Lane &q, const rtk::Cont &ct, uint32_t n) {
+            return rtk::launch_iow03_spec(f, scene, RR, mode, ct, n, q.counter, cap_s, q.st);
         };
     };
-    // sample 0 of every pixel (exact), then the other samples heaviest pixel first, assuming
-    // the stack state sample 0 left behind
     s->last_kernel = "k_iow03s";
-    s->last_launches = (1 + rounds) * (1 + (S > 1 ? 1 : 0) + iters);
-    if (e == hipSuccess) pass(spec(rtk::kSpecFirst), P, cap_s);
+    s->last_launches = (1 + rounds) * (1 + groups * ((S > 1 ? 1 : 0) + iters));
+    // (1) on the caller's stream: sample 0 of every pixel (exact), the guesses for the other
+    // samples, and the pixel order (heaviest sample 0 first)
+    const Lane L0{st, s->counter.as<unsigned>(), s->cont, s->cont_count.as<unsigned>()};
+    e = hipMemsetAsync(R.assume, 0, size_t(P) * sizeof(float4), st);
+    if (e == hipSuccess) pass(L0, spec(R, rtk::kSpecFirst), P, cap_s);
     if (S > 1) {
-        // RT_SPEC_PRIOR=1: guess the scene prior for entries sample 0 left unwritten (fewer first-pass
-        // misses, but measured to form long re-execution chains); default: zero, as sample 0 saw them
-        const float prior = env_int("RT_SPEC_PRIOR", 0) ? s->ri_prior : 0.0f;
-        if (e == hipSuccess) e = rtk::launch_iow03_prep(f, R, s->ws_cost.as<unsigned>(), prior, st);
+        // Entries sample 0 left unwritten: guess 0 (as sample 0 saw them) for samples below
+        // RT_SPEC_PRIOR_FROM, the scene's most common RI from there on (guessing it for early
+        // samples formed long re-run chains, so by default it is never used)
+        const uint32_t prior_from = uint32_t(std::max(1, env_int("RT_SPEC_PRIOR_FROM", 1 << 30)));
+        if (e == hipSuccess)
+            e = rtk::launch_iow03_prep(f, R, s->ws_cost.as<unsigned>(), s->ri_prior, prior_from, st);
         if (e == hipSuccess)
             e = rtk::sort_units_by_cost(s->ws_cost.as<unsigned>(), s->ws_keys.as<unsigned>(), s->ws_iota.as<unsigned>(),
                                         s->ws_order.as<unsigned>(), P, s->ws_temp.p, s->ws_temp_bytes, st);
-        if (e == hipSuccess) pass(spec(rtk::kSpecRest), P * (S - 1), cap_s);
     }
+    if (e == hipSuccess) e = hipEventRecord(s->ev_start, st);
+    // (2) one independent pipeline per pixel group, each on its own stream, so one group's long
+    // samples overlap the other groups' work: speculative pass over samples 1.., resolve and
+    // re-run passes (the first list longest first), final resolve, sequential leftovers
     const bool sort_first = env_int("RT_SPEC_SORT", 1) != 0;
-    for (int it = 0; it < iters && e == hipSuccess; it++) {
-        e = hipMemsetAsync(sc, 0, sizeof(unsigned), st);
-        if (e == hipSuccess) e = rtk::launch_iow03_resolve(f, R, false, nullptr, st);
-        if (it == 0 && sort_first && e == hipSuccess) {
-            // the first re-execution list holds the long samples: run it longest first (LPT),
-            // keyed by each sample's ray count in its speculative run
-            const size_t n = size_t(P) * S;
-            e = rtk::spec_list_keys(R, s->sp_keys.as<unsigned>(), n, st);
-            if (e == hipSuccess)
-                e = rtk::sort_pairs_desc(s->sp_keys.as<unsigned>(), s->sp_keys2.as<unsigned>(), R.list,
-                                         s->sp_list2.as<unsigned>(), n, s->sp_temp.p, s->sp_temp_bytes, 24, st);
-            rtk::SpecRecs R2 = R;
-            R2.list = s->sp_list2.as<uint32_t>();
-            if (e == hipSuccess)
-                pass([&](const rtk::Cont &ct, uint32_t nu) {
-                    return rtk::launch_iow03_spec(f, scene, R2, rtk::kSpecList, ct, nu, s->counter.as<unsigned>(),
-                                                  cap_s, st);
-                }, P * S, cap_s);
-        } else if (e == hipSuccess) pass(spec(rtk::kSpecList), P * S, cap_s);
+    for (int g = 0; g < groups && e == hipSuccess; g++) {
+        auto &GL = *s->lanes[size_t(g)];
+        const Lane L{GL.st, GL.counter.as<unsigned>(), GL.cont, GL.cont_count.as<unsigned>()};
+        rtk::SpecRecs RG = R;
+        const uint32_t base = uint32_t(uint64_t(P) * g / groups);
+        const uint32_t cnt_g = uint32_t(uint64_t(P) * (g + 1) / groups) - base;
+        if (S > 1) { RG.order_base = base; RG.order_n = cnt_g; }
+        RG.list = R.list + size_t(base) * S;
+        RG.list_count = sc + 32 * g;
+        RG.fb_list = R.fb_list + base;
+        RG.fb_count = sc + 32 * g + 16;
+        const size_t nmax = size_t(cnt_g) * S;  // list bound for this group
+        e = hipStreamWaitEvent(L.st, s->ev_start, 0);
+        if (S > 1 && e == hipSuccess) pass(L, spec(RG, rtk::kSpecRest), cnt_g * (S - 1), cap_s);
+        for (int it = 0; it < iters && e == hipSuccess; it++) {
+            e = hipMemsetAsync(RG.list_count, 0, sizeof(unsigned), L.st);
+            if (e == hipSuccess) e = rtk::launch_iow03_resolve(f, RG, false, nullptr, L.st);
+            if (it == 0 && sort_first && e == hipSuccess) {
+                // the first re-execution list holds the long samples: run it longest first (LPT),
+                // keyed by each sample's ray count in its speculative run
+                unsigned *k1 = s->sp_keys.as<unsigned>() + size_t(base) * S;
+                unsigned *k2 = s->sp_keys2.as<unsigned>() + size_t(base) * S;
+                uint32_t *l2 = s->sp_list2.as<uint32_t>() + size_t(base) * S;
+                e = rtk::spec_list_keys(RG, k1, nmax, L.st);
+                if (e == hipSuccess)
+                    e = rtk::sort_pairs_desc(k1, k2, RG.list, l2, nmax, GL.temp.p, GL.temp_bytes, 24, L.st);
+                rtk::SpecRecs R2 = RG;
+                R2.list = l2;
+                if (e == hipSuccess) pass(L, spec(R2, rtk::kSpecList), uint32_t(nmax), cap_s);
+            } else if (e == hipSuccess) pass(L, spec(RG, rtk::kSpecList), uint32_t(nmax), cap_s);
+        }
+        if (e == hipSuccess) e = hipMemsetAsync(RG.fb_count, 0, sizeof(unsigned), L.st);
+        if (e == hipSuccess) e = rtk::launch_iow03_resolve(f, RG, true, s->ws_state.as<float4>(), L.st);
+        // leftovers: the sequential kernel from each pixel's first unresolved sample
+        rtk::Chunk ch{};
+        ch.s_begin = 0;
+        ch.s_end = int(S);
+        ch.final_chunk = 1;
+        ch.state = s->ws_state.as<float4>();
+        ch.order = RG.fb_list;
+        ch.order_count = RG.fb_count;
+        ch.per_unit_begin = 1;
+        if (e == hipSuccess)
+            pass(L, [&, ch](const Lane &q, const rtk::Cont &ct, uint32_t n) {
+                return rtk::launch_iow03(f, scene, ch, ct, n, q.counter, s->s_stop, cap_q, q.st);
+            }, cnt_g, cap_q);
+        if (e == hipSuccess) e = hipEventRecord(GL.done, L.st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, GL.done, 0);  // join
     }
-    if (e == hipSuccess) e = hipMemsetAsync(sc + 16, 0, sizeof(unsigned), st);
-    if (e == hipSuccess) e = rtk::launch_iow03_resolve(f, R, true, s->ws_state.as<float4>(), st);
-    // leftovers: the sequential kernel from each pixel's first unresolved sample
-    rtk::Chunk ch{};
-    ch.s_begin = 0;
-    ch.s_end = int(S);
-    ch.final_chunk = 1;
-    ch.state = s->ws_state.as<float4>();
-    ch.order = R.fb_list;
-    ch.order_count = R.fb_count;
-    ch.per_unit_begin = 1;
-    if (e == hipSuccess)
-        pass([&](const rtk::Cont &ct, uint32_t n) {
-            return rtk::launch_iow03(f, scene, ch, ct, n, s->counter.as<unsigned>(), s->s_stop, cap_q, st);
-        }, P, cap_q);
     if (e != hipSuccess) {
         std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
         return RT_E_HIP;
@@ -769,6 +837,47 @@ int rt_lbvh_build(const float *aabbs, uint32_t n, float *nodes_out) {
     return RT_OK;
 }
 
+size_t rt_lbvh_workspace_bytes(uint32_t n) { return rtk::lbvh_workspace_bytes(n); }
+
+int rt_lbvh_build_async(const float *d_aabbs, uint32_t n, float *d_nodes_out, void *d_ws, size_t ws_bytes,
+                        void *stream) {
+    if (!d_aabbs || !d_nodes_out || n == 0 || (n > 1 && (!d_ws || ws_bytes < rtk::lbvh_workspace_bytes(n))))
+        return RT_E_ARG;
+    if (n > (1u << 24)) return RT_E_UNSUPPORTED;  // node / object ids are stored as floats (exact to 2^24)
+    const hipError_t e = rtk::lbvh_build_device(d_aabbs, n, d_nodes_out, d_ws, ws_bytes, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "[rt_hip] lbvh build failed: %s\n", hipGetErrorString(e));
+        return RT_E_HIP;
+    }
+    return RT_OK;
+}
+
+int rt_lbvh_build_gpu(const float *aabbs, uint32_t n, float *nodes_out, int device, double *ms) {
+    if (!aabbs || !nodes_out || n == 0) return RT_E_ARG;
+    int rc = check_device(device);
+    if (rc != RT_OK) return rc;
+    const size_t total = 2 * size_t(n) - 1;
+    DevBuf d_in, d_out, d_ws;
+    HIP_OK(d_in.upload(aabbs, size_t(n) * 6 * sizeof(float)));
+    HIP_OK(d_out.alloc(total * 8 * sizeof(float)));
+    HIP_OK(d_ws.alloc(rtk::lbvh_workspace_bytes(n)));
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventRecord(e0, nullptr));
+    rc = rt_lbvh_build_async(d_in.as<float>(), n, d_out.as<float>(), d_ws.p, d_ws.bytes, nullptr);
+    HIP_OK(hipEventRecord(e1, nullptr));
+    HIP_OK(hipEventSynchronize(e1));
+    float t = 0.0f;
+    (void)hipEventElapsedTime(&t, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (ms) *ms = t;
+    if (rc != RT_OK) return rc;
+    HIP_OK(hipMemcpy(nodes_out, d_out.p, total * 8 * sizeof(float), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
 rt_dev_scene *rt_dev_scene_iow03(const float *types, const float *records, uint32_t n, int spp, int device) {
     if (!types || !records || spp < 1) return nullptr;
     if (check_device(device) != RT_OK) return nullptr;
@@ -792,7 +901,11 @@ rt_dev_scene *rt_dev_scene_inw(const float *geom, uint32_t n, int layout, const 
     return s;
 }
 
-void rt_dev_scene_free(rt_dev_scene *s) { delete s; }
+void rt_dev_scene_free(rt_dev_scene *s) {
+    if (!s) return;
+    (void)hipDeviceSynchronize();  // the scene's internal stream may still run its last frame
+    delete s;
+}
 
 int rt_render_tiles_async(rt_dev_scene *s, const rt_camera *cam, const rt_params *p, const int *d_tiles,
                           int n_tiles, int tile_size, float *d_out_packed, float *d_out_depth_packed,

@@ -671,7 +671,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     }
     Stack K{lds + threadIdx.x, lds_b + threadIdx.x, 0};
     const uint32_t total = ct.in ? *ct.in_count
-                         : (mode == kSpecList ? *R.list_count : (mode == kSpecFirst ? R.P : R.P * (R.S - 1)));
+                         : (mode == kSpecList ? *R.list_count : (mode == kSpecFirst ? R.P : R.order_n * (R.S - 1)));
     const bool may_park = ct.out != nullptr && total >= ct.park_min;
     const int W = f.W, H = f.H, spp = f.spp;
     int grid = 1;
@@ -704,7 +704,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 // kSpecFirst: sample 0 of every pixel; kSpecRest: samples 1.. pixel-major, pixels
                 // in R.order (heaviest sample 0 first); kSpecList: the re-execution list
                 u = mode == kSpecList ? R.list[q]
-                    : (mode == kSpecFirst ? q : (1u + q % (R.S - 1)) * R.P + R.order[q / (R.S - 1)]);
+                    : (mode == kSpecFirst ? q : (1u + q % (R.S - 1)) * R.P + R.order[R.order_base + q / (R.S - 1)]);
                 const uint32_t pu = u % R.P;
                 const int s = (int)(u / R.P);
                 const UnitPix px = unit_pixel(f, pu);
@@ -772,23 +772,26 @@ __global__ __launch_bounds__(kBlock) void k_iow03s(Frame f, IowScene S, SpecRecs
 // the resolve; `prior` is the scene's most common refractive index, the value such entries
 // almost always hold once any sample has pushed there).  Pixels are keyed by sample 0's ray
 // count so the rest run heaviest first.
-__global__ __launch_bounds__(kBlock) void k_iow03_prep(Frame f, SpecRecs R, unsigned *key, float prior) {
+__global__ __launch_bounds__(kBlock) void k_iow03_prep(Frame f, SpecRecs R, unsigned *key, float prior,
+                                                       uint32_t prior_from) {
     const uint32_t pu = blockIdx.x * kBlock + threadIdx.x;
     if (pu >= R.P) return;  // no cross-lane work in this kernel
     const UnitPix px = unit_pixel(f, pu);
     if (!px.in_image) { key[pu] = 0; return; }
     const uint32_t wm = (__float_as_uint(R.col[pu].w) >> 4) & 15u;
     const float4 fn = R.fin[pu];
-    const float4 e = make_float4((wm & 2u) ? fn.x : prior, (wm & 4u) ? fn.y : prior, (wm & 8u) ? fn.z : prior, 0.0f);
-    for (uint32_t s = 1; s < R.S; s++) R.assume[(size_t)s * R.P + pu] = e;
+    const float4 e0 = make_float4((wm & 2u) ? fn.x : 0.0f, (wm & 4u) ? fn.y : 0.0f, (wm & 8u) ? fn.z : 0.0f, 0.0f);
+    const float4 e1 = make_float4((wm & 2u) ? fn.x : prior, (wm & 4u) ? fn.y : prior, (wm & 8u) ? fn.z : prior, 0.0f);
+    for (uint32_t s = 1; s < R.S; s++) R.assume[(size_t)s * R.P + pu] = s >= prior_from ? e1 : e0;
     key[pu] = R.ctr[pu].x;
 }
 
 // Replay of each pixel's samples in order (one lane per pixel unit; records are [s][pu], so
 // consecutive lanes read consecutive records).
 __global__ __launch_bounds__(kBlock) void k_iow03_resolve(Frame f, SpecRecs R, int final_pass, float4 *state) {
-    const uint32_t pu = blockIdx.x * kBlock + threadIdx.x;
-    const bool valid = pu < R.P;
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;  // pixel i of the group (or of all units)
+    const bool valid = R.order_n ? i < R.order_n : i < R.P;
+    const uint32_t pu = valid ? (R.order_n ? R.order[R.order_base + i] : i) : 0;
     const UnitPix px = unit_pixel(f, valid ? pu : 0);
     bool work = valid && px.in_image;
     uint32_t E1 = 0, E2 = 0, E3 = 0;  // exact RI bits of entries 1..3 before sample s
@@ -1375,13 +1378,14 @@ hipError_t spec_list_keys(const SpecRecs &R, unsigned *keys, size_t n, hipStream
     hipLaunchKernelGGL(k_spec_list_keys, dim3(4096), dim3(256), 0, s, R, keys, n);
     return hipGetLastError();
 }
-hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, hipStream_t s) {
+hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,
+                             hipStream_t s) {
     const unsigned blocks = (R.P + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_iow03_prep, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, key, prior);
+    hipLaunchKernelGGL(k_iow03_prep, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, key, prior, prior_from);
     return hipGetLastError();
 }
 hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pass, float4 *state, hipStream_t s) {
-    const unsigned blocks = (R.P + kBlock - 1) / kBlock;
+    const unsigned blocks = ((R.order_n ? R.order_n : R.P) + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_iow03_resolve, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, final_pass ? 1 : 0, state);
     return hipGetLastError();
 }

@@ -88,6 +88,7 @@ struct SpecRecs {
     uint32_t *fb_list; // pixels left to the sequential kernel after the last resolve
     unsigned *fb_count;
     const uint32_t *order;  // pixel units, heaviest sample 0 first (kSpecRest)
+    uint32_t order_base, order_n;  // this group's slice of `order` (order_n == 0: all P units)
 };
 enum { kSpecFirst = 0, kSpecRest = 1, kSpecList = 2 };
 
@@ -120,9 +121,13 @@ uint32_t units_of(const Frame &f);
 // sample-parallel IOW-03 pass over the units of `mode` (kSpec*)
 hipError_t launch_iow03_spec(const Frame &f, const IowScene &sc, const SpecRecs &R, int mode, const Cont &ct,
                              uint32_t n_units, unsigned *counter, int blocks_cap, hipStream_t s);
+// LBVH build on the device (rt_lbvh.hip); ws = lbvh_workspace_bytes(n) of scratch
+size_t lbvh_workspace_bytes(uint32_t n);
+hipError_t lbvh_build_device(const float *aabb, uint32_t n, float *out, void *ws, size_t ws_bytes, hipStream_t s);
 hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipStream_t s);  // diagnostics
 // after the kSpecFirst pass: assumptions for samples 1.. and the per-pixel ordering keys
-hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, hipStream_t s);
+hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,
+                             hipStream_t s);
 // replay each pixel's samples: re-queue wrong assumptions; final: write clean pixels, hand
 // the rest (with their resume state in `state`) to the sequential kernel via R.fb_list
 hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pass, float4 *state, hipStream_t s);

@@ -79,6 +79,9 @@ SIGNATURES = {
     "rt_render_inw": (C.c_int, [_FP, C.c_uint32, C.c_int, _FP, _FP, C.c_uint32, C.POINTER(RtCamera),
                                 C.POINTER(RtParams), _FP, _FP, C.POINTER(RtStats)]),
     "rt_lbvh_build": (C.c_int, [_FP, C.c_uint32, _FP]),
+    "rt_lbvh_workspace_bytes": (C.c_size_t, [C.c_uint32]),
+    "rt_lbvh_build_async": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "rt_lbvh_build_gpu": (C.c_int, [_FP, C.c_uint32, _FP, C.c_int, C.POINTER(C.c_double)]),
     "rt_dev_scene_iow03": (C.c_void_p, [_FP, _FP, C.c_uint32, C.c_int, C.c_int]),
     "rt_dev_scene_inw": (C.c_void_p, [_FP, C.c_uint32, C.c_int, _FP, _FP, C.c_uint32, C.c_int, C.c_int]),
     "rt_dev_scene_free": (None, [C.c_void_p]),
@@ -213,6 +216,16 @@ def make_scene(preset: int, seed: int = 0, n_hint: int = 0, **param_overrides) -
     for k, v in pack(arr, n, stage).items():
         setattr(sc, k, v)
     return sc
+
+
+def lbvh_build_gpu(aabbs, device: int = -1):
+    """GPU LBVH (rt_lbvh_build_gpu): same (2N-1) x 8 node buffer as lbvh_build; returns (nodes, ms)."""
+    aabbs = np.ascontiguousarray(aabbs, np.float32)
+    n = aabbs.shape[0]
+    nodes = np.zeros((2 * n - 1, 8), np.float32)
+    ms = C.c_double(0.0)
+    check(load().rt_lbvh_build_gpu(fptr(aabbs), n, fptr(nodes), device, C.byref(ms)), "rt_lbvh_build_gpu")
+    return nodes, ms.value
 
 
 def lbvh_build(aabbs: np.ndarray) -> np.ndarray:
