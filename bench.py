@@ -95,6 +95,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16, help="host cores for the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--occupancy", action="store_true", help="report per-phase lane occupancy (diagnostic)")
+    ap.add_argument("--save-image", default="", help="rank 0 saves the assembled frame (.npy) for checking")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,10 +103,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # RT_BENCH_BACKEND=gloo: multi-rank rehearsal on a box with fewer GPUs than ranks (ranks
+    # share devices, collectives go through host memory); the measured path is nccl (RCCL)
+    backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    host_coll = world > 1 and backend != "nccl"
 
     lib = R.load()
     over = {}
@@ -147,15 +157,24 @@ def main():
                 raise RuntimeError(f"rt_render_tiles_async -> {rc}")
         if i is not None:
             ev[i][1].record(stream)
-        if world > 1:  # the one exchange step: RCCL gather of the packed tiles to rank 0
+        if world > 1 and not host_coll:  # the one exchange step: RCCL gather of the packed tiles to rank 0
             dist.gather(packed, gathered, dst=0)
+        elif world > 1:
+            hg = [torch.empty_like(packed, device="cpu") for _ in range(world)] if rank == 0 else None
+            dist.gather(packed.cpu(), hg, dst=0)
+            if rank == 0:
+                for g_, h_ in zip(gathered, hg):
+                    g_.copy_(h_)
         if rank == 0:  # assemble the frame: tile t of rank r is allt[r + world*t]
             src = torch.stack(gathered, 0) if world > 1 else packed.unsqueeze(0)
             image.copy_(assemble_frame(src, len(allt), nx, ny))
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            if host_coll:
+                dist.barrier()
+            else:
+                dist.barrier(device_ids=[local])
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -174,6 +193,8 @@ def main():
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     ctr = counters.clone()
     if world > 1:
+        if host_coll:
+            t, ctr = t.cpu(), ctr.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(ctr, op=dist.ReduceOp.SUM)
     elapsed, kernel_ms = float(t[0]), float(t[1])
@@ -252,6 +273,8 @@ def main():
             cyc = dict(zip(("camera", "closest_hit", "bvh_walk", "leaf_tests", "segment"), d[8:13]))
             out["wave_cycles_share"] = {k: round(v / max(1, cyc["camera"] + cyc["segment"]), 4) for k, v in cyc.items()}
         print(json.dumps(out), flush=True)
+        if args.save_image:
+            np.save(args.save_image, image[:H, :W].cpu().numpy())
     lib.rt_dev_scene_free(scene)
     if world > 1:
         dist.destroy_process_group()
