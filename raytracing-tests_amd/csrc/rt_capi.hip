@@ -118,6 +118,7 @@ struct rt_dev_scene {
     size_t spec_cap = 0, spec_units = 0;
     DevBuf sp_col, sp_fin, sp_ctr, sp_assume, sp_list, sp_fb, sp_counts;
     DevBuf sp_keys, sp_keys2, sp_list2, sp_temp;  // longest-first ordering of the re-execution list
+    DevBuf sp_pstate;  // asynchronous windows: per-pixel frontier state
     size_t sp_temp_bytes = 0;
     // launches of the render's main kernel in the last render (rt_debug_launches)
     int last_launches = 0;
@@ -136,6 +137,7 @@ struct rt_dev_scene {
     };
     std::vector<std::unique_ptr<GroupLane>> lanes;
     hipEvent_t ev_start = nullptr;
+    unsigned epoch = 0;  // frame tag of the asynchronous-window records
     ~rt_dev_scene() {
         if (ev_start) (void)hipEventDestroy(ev_start);
     }
@@ -352,7 +354,7 @@ bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || bytes > free_b / 2) return false;
     for (DevBuf *b : {&s->sp_col, &s->sp_fin, &s->sp_ctr, &s->sp_assume, &s->sp_list, &s->sp_fb, &s->sp_counts,
-                      &s->sp_keys, &s->sp_keys2, &s->sp_list2, &s->sp_temp}) {
+                      &s->sp_keys, &s->sp_keys2, &s->sp_list2, &s->sp_temp, &s->sp_pstate}) {
         b->~DevBuf();
         new (b) DevBuf();
     }
@@ -361,6 +363,7 @@ bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
         s->sp_list.alloc(n * sizeof(uint32_t)) != hipSuccess || s->sp_fb.alloc(size_t(P) * 4) != hipSuccess ||
         s->sp_counts.alloc(64 * 64) != hipSuccess || s->sp_keys.alloc(n * 4) != hipSuccess ||
         s->sp_keys2.alloc(n * 4) != hipSuccess || s->sp_list2.alloc(n * 4) != hipSuccess ||
+        s->sp_pstate.alloc(size_t(P) * 3 * sizeof(uint4)) != hipSuccess ||
         s->sp_temp.alloc(s->sp_temp_bytes = rtk::sort_pairs_temp_bytes(n, 24)) != hipSuccess) {
         s->spec_cap = s->spec_units = 0;
         return false;
@@ -493,7 +496,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     unsigned *sc = s->sp_counts.as<unsigned>();  // group g: [32g] list count, [32g+16] fallback count
     const rtk::SpecRecs R{s->sp_col.as<float4>(), s->sp_fin.as<float4>(), s->sp_ctr.as<uint4>(),
                           s->sp_assume.as<float4>(), P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(),
-                          sc + 16, s->ws_order.as<uint32_t>(), 0, 0};
+                          sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>()};
     rtk::IowScene scene{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
                         s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link};
     const int cap_s = s->cus * rtk::resident_blocks_per_cu(5);
@@ -534,6 +537,23 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const Lane L0{st, s->counter.as<unsigned>(), s->cont, s->cont_count.as<unsigned>()};
     e = hipMemsetAsync(R.assume, 0, size_t(P) * sizeof(float4), st);
     if (e == hipSuccess) pass(L0, spec(R, rtk::kSpecFirst), P, cap_s);
+    if (S > 1 && env_int("RT_IOW_ASYNC", 0) != 0) {
+        // (2') asynchronous windows: the rest of the frame in one persistent launch
+        if (e == hipSuccess) e = rtk::launch_iow03_keys0(f, R, s->ws_cost.as<unsigned>(), st);
+        if (e == hipSuccess)
+            e = rtk::sort_units_by_cost(s->ws_cost.as<unsigned>(), s->ws_keys.as<unsigned>(), s->ws_iota.as<unsigned>(),
+                                        s->ws_order.as<unsigned>(), P, s->ws_temp.p, s->ws_temp_bytes, st);
+        s->last_kernel = "k_iow03a";
+        s->last_launches = 1;
+        if (e == hipSuccess)
+            e = rtk::launch_iow03_async(f, scene, R, s->counter.as<unsigned>(), ++s->epoch,
+                                        s->cus * rtk::resident_blocks_per_cu(8), st);
+        if (e != hipSuccess) {
+            std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
+            return RT_E_HIP;
+        }
+        return RT_OK;
+    }
     if (S > 1) {
         // Entries sample 0 left unwritten: guess 0 (as sample 0 saw them) for samples below
         // RT_SPEC_PRIOR_FROM, the scene's most common RI from there on (guessing it for early

@@ -694,7 +694,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 K.wmask = __float_as_uint(m.w) & 15u; K.rmask = __float_as_uint(m.w) >> 4;
                 sample = f3{a.x, a.y, a.z}; urays = __float_as_uint(a.w);
                 c.seg = __float_as_uint(b.x); c.nodes = __float_as_uint(b.y); c.prims = __float_as_uint(b.z);
-                c.drops = __float_as_uint(b.w) & 0xffffu; c.nans = __float_as_uint(b.w) >> 16;
+                c.drops = __float_as_uint(b.w); c.nans = __float_as_uint(p[12].x);
                 const float *fl = reinterpret_cast<const float *>(p + 3);
                 for (int k = 0; k < kFl; k++) K.base[k * kBlock] = fl[k];
                 if constexpr (NARROW)
@@ -735,7 +735,8 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 float4 *p = ct.out + (size_t)slot * kContSlots;
                 p[0] = make_float4(ubits(u), ibits(skip), ibits(K.size), ubits(K.wmask | (K.rmask << 4)));
                 p[1] = make_float4(sample.x, sample.y, sample.z, ubits(urays));
-                p[2] = make_float4(ubits(c.seg), ubits(c.nodes), ubits(c.prims), ubits(c.drops | (c.nans << 16)));
+                p[2] = make_float4(ubits(c.seg), ubits(c.nodes), ubits(c.prims), ubits(c.drops));
+                p[12] = make_float4(ubits(c.nans), 0.0f, 0.0f, 0.0f);
                 float *fl = reinterpret_cast<float *>(p + 3);
                 for (int k = 0; k < kFl; k++) fl[k] = K.base[k * kBlock];
                 if constexpr (NARROW)
@@ -1192,6 +1193,229 @@ __global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S, Chunk ch, C
     flush(f, c);
 }
 
+// ============================================================================ IOW-03, asynchronous windows
+// The sample-parallel scheme without global passes.  A wave takes pixels from the global queue
+// and issues all their samples to its own lanes, so every record of a pixel is written and read
+// by one wave (workgroup-scope visibility, no cross-CU hand-off).  Per pixel the wave keeps, in
+// global memory, a frontier: samples below it are validated and the exact stack state E before
+// it is known.  When a sample finishes, the frontier of its pixel advances over finished samples
+// in sample order; a misprediction is re-run at once, by the lane that found it, with E, which
+// is exact there, so re-runs never chain.  A sample issued when the frontier already stands at
+// it also uses E.  A pixel whose samples are all issued no longer holds a slot, so the wave keeps
+// issuing new pixels while long samples finish; nothing waits for a global pass.
+constexpr int kIss = 2;   // pixels a wave is issuing samples from
+constexpr int kBvA = 28;  // BVH stack entries
+struct IssueSlot {
+    int pu;             // pixel unit, -1 = empty
+    int next;           // next sample to issue
+    unsigned G[3];      // guess for samples issued ahead of the frontier (state after sample 0)
+};
+// per-pixel frontier state in global memory (SpecRecs.pstate, 3 x uint4 per pixel unit):
+//   [0] fr, E0, E1, E2   [1] fc.xyz (bits), seg   [2] drops, nans, nodes, prims
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__global__ __launch_bounds__(kBlock) void k_iow03a(Frame f, IowScene S, SpecRecs R, unsigned *counter, unsigned epoch) {
+    constexpr int kFl = kIowStack * 9;
+    constexpr int BCAP = kBvA - 3;
+    __shared__ float lds[kFl * kBlock];
+    __shared__ short lds_bvh[kBvA * kBlock];
+    __shared__ unsigned long long s_dbg[kBlock / 64][kDbgSlots];
+    __shared__ IssueSlot s_iss[kBlock / 64][kIss];
+    short *bstk = lds_bvh + threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63);
+    IssueSlot *iss = s_iss[threadIdx.x >> 6];
+    Ctr c;  // counters of the lane's current unit
+    if (f.dbg) {
+        c.wdbg = s_dbg[threadIdx.x >> 6];
+        if (lane < kDbgSlots) c.wdbg[lane] = 0;
+    }
+    IowStack<false> K{lds + threadIdx.x, nullptr, 0};
+    if (lane < kIss) iss[lane].pu = -1;
+    wave_sync_lds();
+    const uint32_t P = R.P, SS = R.S;
+    const int W = f.W, H = f.H;
+    int grid = 1;
+    while (grid * grid < f.spp) grid++;
+    const float aspect = (float)W * rcp((float)H);
+    const float dsx = aspect * rcp((float)(W * grid));
+    const float dsy = 1.0f * rcp((float)(H * grid));
+    const unsigned done_tag = (1u << 8) | ((epoch & 0xffffu) << 16);
+    bool busy = false, exhausted = false;
+    uint32_t u = 0, pu = 0;
+    int s = 0, skip = 0;
+    f3 sample = f3{0, 0, 0};
+    unsigned long long acc[5] = {0, 0, 0, 0, 0};  // seg, nodes, prims, drops, nans of finished pixels
+    // start sample s of pixel pu on this lane with assumed stack RI a1..a3
+    auto start = [&](uint32_t p_, int s_, unsigned a1, unsigned a2, unsigned a3) {
+        pu = p_; s = s_;
+        u = (uint32_t)s * P + pu;
+        R.assume[u] = make_float4(__uint_as_float(a1), __uint_as_float(a2), __uint_as_float(a3), 0.0f);
+        busy = true;
+        c.seg = c.nodes = c.prims = c.drops = c.nans = 0;
+        skip = 0;
+        sample = f3{0, 0, 0};
+        K.size = 0; K.wmask = 0; K.rmask = 0;
+        K.at(0, 7) = 0.0f; K.at(1, 7) = __uint_as_float(a1); K.at(2, 7) = __uint_as_float(a2); K.at(3, 7) = __uint_as_float(a3);
+        const UnitPix px = unit_pixel(f, pu);
+        const float sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
+        const float sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
+        f3 ro, rd;
+        iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
+        if (f.show_normal) sample = iow_launch_ray<BCAP>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
+        else K.push(ro, rd, 1.0f, 1.0f, 0, c);
+    };
+    for (;;) {
+        // (1) refill empty issue slots from the global pixel queue (heaviest sample 0 first)
+        const bool empty = lane < kIss && iss[lane].pu < 0;
+        const unsigned long long em = __ballot(empty);
+        if (!exhausted && em) {
+            const int leader = __ffsll((long long)em) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(counter, (unsigned)__popcll(em));
+            base = __shfl(base, leader, 64);
+            const uint32_t q = base + (uint32_t)__popcll(em & ((1ull << lane) - 1ull));
+            if (empty && q < P) {
+                const uint32_t p_ = R.order[q];
+                const UnitPix px = unit_pixel(f, p_);
+                if (!px.in_image) write_px(f, px, f3{0, 0, 0}, 0.0f);  // tile padding: done
+                else {  // sample 0 ran exactly in the first pass: frontier at 1
+                    const float4 c0 = R.col[p_], f0 = R.fin[p_];
+                    const uint4 k0 = R.ctr[p_];
+                    const unsigned wm = (__float_as_uint(c0.w) >> 4) & 15u;
+                    const unsigned e0 = (wm & 2u) ? __float_as_uint(f0.x) : 0u;
+                    const unsigned e1 = (wm & 4u) ? __float_as_uint(f0.y) : 0u;
+                    const unsigned e2 = (wm & 8u) ? __float_as_uint(f0.z) : 0u;
+                    uint4 *ps = R.pstate + 3 * (size_t)p_;
+                    ps[0] = make_uint4(1u, e0, e1, e2);
+                    ps[1] = make_uint4(__float_as_uint(c0.x), __float_as_uint(c0.y), __float_as_uint(c0.z), k0.x);
+                    ps[2] = make_uint4(k0.y, k0.z, k0.w, __float_as_uint(f0.w));
+                    if (SS <= 1) {  // nothing left to issue
+                        write_px(f, px, f3{c0.x, c0.y, c0.z} * rcp((float)SS), 0.0f);
+                        acc[0] += k0.x; acc[1] += k0.w; acc[2] += __float_as_uint(f0.w); acc[3] += k0.y; acc[4] += k0.z;
+                        if (f.px_rays) f.px_rays[p_] = k0.x;
+                    } else {
+                        iss[lane].G[0] = e0; iss[lane].G[1] = e1; iss[lane].G[2] = e2;
+                        iss[lane].next = 1;
+                        iss[lane].pu = (int)p_;
+                    }
+                }
+            }
+            if (__ballot(empty && q >= P) != 0) exhausted = true;
+        }
+        __threadfence_block();  // pixel states before any lane reads them
+        wave_sync_lds();
+        // (2) idle lanes take the next samples of the issue slots, in slot order
+        const unsigned long long idle = __ballot(!busy);
+        if (idle) {
+            const int me = (int)__popcll(idle & ((1ull << lane) - 1ull));
+            const int n_idle = (int)__popcll(idle);
+            int before = 0;
+            for (int k = 0; k < kIss && before < n_idle; k++) {
+                const int pk = iss[k].pu;
+                if (pk < 0) continue;
+                const int nx = iss[k].next;
+                const int take = min((int)SS - nx, n_idle - before);
+                if (!busy && me >= before && me < before + take) {
+                    const int s_ = nx + (me - before);
+                    const uint4 st0 = R.pstate[3 * (size_t)pk];  // frontier and exact state
+                    const bool exact = (int)st0.x == s_;
+                    start((uint32_t)pk, s_, exact ? st0.y : iss[k].G[0], exact ? st0.z : iss[k].G[1],
+                          exact ? st0.w : iss[k].G[2]);
+                }
+                if (lane == k) {  // one writer per slot
+                    iss[k].next = nx + take;
+                    if (nx + take >= (int)SS) iss[k].pu = -1;  // all issued: the pixel leaves the window
+                }
+                before += take;
+            }
+        }
+        wave_sync_lds();
+        // (3) one ray segment per busy lane
+        DBG_TALLY(f, c, kDbgOuter, busy);
+        DBG_TALLY(f, c, kDbgSeg, busy && K.size > 0);
+        DBG_T0(f, t_seg);
+        if (busy && K.size > 0) iow_segment(S, f, K, skip, sample, s, c, bstk);
+        DBG_CYC(f, c, kDbgCycSeg, t_seg);
+        // (4) finished samples write their record
+        const bool fin = busy && K.size == 0;
+        if (fin) {
+            R.col[u] = make_float4(sample.x, sample.y, sample.z, __uint_as_float(K.rmask | (K.wmask << 4) | done_tag));
+            R.fin[u] = make_float4(K.at(1, 7), K.at(2, 7), K.at(3, 7), __uint_as_float(c.prims));
+            R.ctr[u] = make_uint4(c.seg, c.drops, c.nans, c.nodes);
+            busy = false;
+        }
+        __threadfence_block();  // the records before the frontier reads them
+        // (5) advance the frontier of every pixel that just had a sample finish, one lane per pixel
+        unsigned long long fm = __ballot(fin);
+        while (fm) {
+            const int ld = __ffsll((long long)fm) - 1;
+            const uint32_t pid = __shfl(pu, ld, 64);
+            fm &= ~__ballot(fin && pu == pid);
+            if (lane == ld) {
+                uint4 *ps = R.pstate + 3 * (size_t)pid;
+                uint4 st0 = ps[0], st1 = ps[1], st2 = ps[2];
+                int fr = (int)st0.x;
+                f3 fc = f3{__uint_as_float(st1.x), __uint_as_float(st1.y), __uint_as_float(st1.z)};
+                bool bad = false;
+                while (fr < (int)SS) {
+                    const size_t uu = (size_t)fr * P + pid;
+                    const float4 cl = R.col[uu];
+                    const unsigned fl = __float_as_uint(cl.w);
+                    if ((fl & 0xffff0100u) != done_tag) break;  // not finished in this frame yet
+                    const float4 a = R.assume[uu];
+                    const unsigned rm = fl & 15u, wm = (fl >> 4) & 15u;
+                    if (((rm & 2u) && __float_as_uint(a.x) != st0.y) || ((rm & 4u) && __float_as_uint(a.y) != st0.z) ||
+                        ((rm & 8u) && __float_as_uint(a.z) != st0.w)) { bad = true; break; }
+                    fc = fc + f3{cl.x, cl.y, cl.z};
+                    const float4 fn = R.fin[uu];
+                    const uint4 k4 = R.ctr[uu];
+                    st1.w += k4.x; st2.x += k4.y; st2.y += k4.z; st2.z += k4.w; st2.w += __float_as_uint(fn.w);
+                    if (wm & 2u) st0.y = __float_as_uint(fn.x);
+                    if (wm & 4u) st0.z = __float_as_uint(fn.y);
+                    if (wm & 8u) st0.w = __float_as_uint(fn.z);
+                    fr++;
+                }
+                st0.x = (unsigned)fr;
+                st1.x = __float_as_uint(fc.x); st1.y = __float_as_uint(fc.y); st1.z = __float_as_uint(fc.z);
+                ps[0] = st0; ps[1] = st1; ps[2] = st2;
+                if (bad) {
+                    // mark the record unfinished (its re-run rewrites it) and re-run it here with E
+                    R.col[(size_t)fr * P + pid].w = 0.0f;
+                    start(pid, fr, st0.y, st0.z, st0.w);
+                } else if (fr >= (int)SS) {  // pixel complete
+                    write_px(f, unit_pixel(f, pid), fc * rcp((float)SS), 0.0f);
+                    acc[0] += st1.w; acc[1] += st2.z; acc[2] += st2.w; acc[3] += st2.x; acc[4] += st2.y;
+                    if (f.px_rays) f.px_rays[pid] = st1.w;
+                }
+            }
+        }
+        __threadfence_block();
+        wave_sync_lds();
+        if (exhausted && __ballot(busy) == 0 && __ballot(lane < kIss && iss[lane].pu >= 0) == 0) break;
+    }
+    if (c.wdbg && lane == 0)
+        for (int i = 0; i < kDbgSlots; i++) atomicAdd(f.dbg + i, c.wdbg[i]);
+    if (f.counters) {
+        const int slot_of[5] = {0, 1, 2, 4, 5};
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const unsigned long long t = wave_sum(acc[i]);
+            if (lane == 0 && t) atomicAdd(f.counters + slot_of[i], t);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_iow03_keys0(Frame f, SpecRecs R, unsigned *key) {
+    const uint32_t pu = blockIdx.x * kBlock + threadIdx.x;
+    if (pu >= R.P) return;  // no cross-lane work
+    key[pu] = unit_pixel(f, pu).in_image ? R.ctr[pu].x : 0u;
+}
+
 // ---------------------------------------------------------------- INW, sample-parallel
 // One unit = one sample of one pixel (u = (s - s0)*P + pu within a chunk of samples [s0, s0+ns)).
 // INW samples are independent invocations (01_BVH...glsl:601-675), so no speculation is needed:
@@ -1326,6 +1550,7 @@ int resident_blocks_per_cu(int kind) {
     if (kind == 3) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03, kBlock, 0);
     else if (kind == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03n, kBlock, 0);
     else if (kind == 5) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03s, kBlock, 0);
+    else if (kind == 8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03a, kBlock, 0);
     else if (kind == 6) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_s<false>, kBlock, 0);
     else if (kind == 7) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_s<true>, kBlock, 0);
     else if (kind == 14) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<true>, kBlock, 0);
@@ -1376,6 +1601,18 @@ __global__ void k_spec_list_keys(SpecRecs R, unsigned *keys, size_t n) {
 }
 hipError_t spec_list_keys(const SpecRecs &R, unsigned *keys, size_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_spec_list_keys, dim3(4096), dim3(256), 0, s, R, keys, n);
+    return hipGetLastError();
+}
+hipError_t launch_iow03_async(const Frame &f, const IowScene &sc, const SpecRecs &R, unsigned *counter,
+                              unsigned epoch, int blocks, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_iow03a, dim3(blocks > 0 ? blocks : 1), dim3(kBlock), 0, s, f, sc, R, counter, epoch);
+    return hipGetLastError();
+}
+hipError_t launch_iow03_keys0(const Frame &f, const SpecRecs &R, unsigned *key, hipStream_t s) {
+    const unsigned blocks = (R.P + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_iow03_keys0, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, key);
     return hipGetLastError();
 }
 hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,

@@ -89,6 +89,7 @@ struct SpecRecs {
     unsigned *fb_count;
     const uint32_t *order;  // pixel units, heaviest sample 0 first (kSpecRest)
     uint32_t order_base, order_n;  // this group's slice of `order` (order_n == 0: all P units)
+    uint4 *pstate;     // asynchronous windows: per pixel unit 3 x uint4 of frontier state
 };
 enum { kSpecFirst = 0, kSpecRest = 1, kSpecList = 2 };
 
@@ -125,6 +126,12 @@ hipError_t launch_iow03_spec(const Frame &f, const IowScene &sc, const SpecRecs 
 size_t lbvh_workspace_bytes(uint32_t n);
 hipError_t lbvh_build_device(const float *aabb, uint32_t n, float *out, void *ws, size_t ws_bytes, hipStream_t s);
 hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipStream_t s);  // diagnostics
+// asynchronous-window IOW-03 over samples 1.. (after the kSpecFirst pass and the pixel order):
+// every pixel's samples, validation and re-runs inside one persistent launch; writes the pixels
+hipError_t launch_iow03_async(const Frame &f, const IowScene &sc, const SpecRecs &R, unsigned *counter,
+                              unsigned epoch, int blocks, hipStream_t s);
+// sort keys = sample 0's ray count per pixel unit (0 for tile padding)
+hipError_t launch_iow03_keys0(const Frame &f, const SpecRecs &R, unsigned *key, hipStream_t s);
 // after the kSpecFirst pass: assumptions for samples 1.. and the per-pixel ordering keys
 hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,
                              hipStream_t s);
@@ -141,7 +148,8 @@ hipError_t launch_inw_fin(const Frame &f, const SpecRecs &R, int s0, int ns, boo
 
 // resident blocks per CU of the render kernel for `kind` (3 = IOW-03 wide, 4 = IOW-03 narrow,
 // 11/14 = INW layout 1/4)
-int resident_blocks_per_cu(int kind);  // 5 = sample-parallel IOW-03, 6/7 = sample-parallel INW 1/4
+int resident_blocks_per_cu(int kind);  // 5 = sample-parallel IOW-03, 6/7 = sample-parallel INW 1/4,
+                                       // 8 = asynchronous-window IOW-03
 // IOW-03 kernel variant for this frame: narrow (byte bounce counts, 12-deep BVH stack, 4 waves
 // per SIMD with spills) when RT_IOW_NARROW=1 and u_NumOfBounce <= 255; wide otherwise
 bool iow_narrow(const Frame &f);

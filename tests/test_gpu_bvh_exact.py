@@ -4,8 +4,9 @@
 - RT_IOW_NARROW=1: the byte-bounce stack layout (12-deep BVH stack) instead of the 9-float one;
 - RT_ROUNDS=0:     no tail compaction (no parking / resume launches);
 - RT_IOW_SPEC=0:   the sequential per-pixel kernel instead of sample-parallel speculation;
-- RT_SPEC_ITERS=0/1: fewer resolve passes, so more pixels finish on the sequential kernel;
-- RT_SPEC_GROUPS=1/7: other pixel-group splits of the two-stream pipeline;
+- RT_SPEC_ITERS=0/1: fewer resolve passes, more pixels finished by the sequential kernel;
+- RT_SPEC_GROUPS=2/7: pixel groups on separate streams;
+- RT_IOW_ASYNC=1: asynchronous windows (per-wave frontiers) instead of global resolve passes;
 - INW: RT_INW_SPEC=0 (per-pixel sequential samples) and RT_SPEC_MAX_GB tiny (sample chunks).
 Each must give a bit-identical image of the final scene with identical ray counts.  The
 renders run in subprocesses because the switches are read by the library at scene build /
@@ -43,7 +44,7 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     out = str(tmp_path / f"img_{len(os.listdir(tmp_path))}.npy")
     env = dict(os.environ)
     for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS", "RT_IOW_SPEC", "RT_SPEC_ITERS",
-              "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_SPEC_GROUPS"):
+              "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_SPEC_GROUPS", "RT_IOW_ASYNC"):
         env.pop(k, None)
     env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out, preset=scene[0], seed=scene[1], n_hint=scene[2])
@@ -61,7 +62,8 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     ({"RT_IOW_SPEC": "0"}, 600, 400, 8),
     ({"RT_SPEC_ITERS": "0"}, 300, 200, 16),
     ({"RT_SPEC_ITERS": "1"}, 300, 200, 16),
-    ({"RT_SPEC_GROUPS": "1"}, 600, 400, 8),
+    ({"RT_IOW_ASYNC": "1"}, 600, 400, 8),
+    ({"RT_SPEC_GROUPS": "2"}, 300, 200, 12),
     ({"RT_SPEC_GROUPS": "7", "RT_SPEC_ITERS": "2"}, 300, 200, 16),
 ])
 def test_strategies_bit_identical(tmp_path, gpu, over, w, h, spp):
