@@ -496,7 +496,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     unsigned *sc = s->sp_counts.as<unsigned>();  // group g: [32g] list count, [32g+16] fallback count
     const rtk::SpecRecs R{s->sp_col.as<float4>(), s->sp_fin.as<float4>(), s->sp_ctr.as<uint4>(),
                           s->sp_assume.as<float4>(), P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(),
-                          sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>()};
+                          sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), ++s->epoch};
     rtk::IowScene scene{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
                         s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link};
     const int cap_s = s->cus * rtk::resident_blocks_per_cu(5);
@@ -505,7 +505,9 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // one compacted pass on a stream with its own queue counter and continuation buffers: the
     // first launch takes `n0` units, resume launches take the parked lanes
     struct Lane { hipStream_t st; unsigned *counter; const DevBuf *cont; unsigned *cnt; };
-    auto pass = [&](const Lane &q, auto &&launch, uint32_t n0, int cap) {
+    // fix = true: before each resume launch, make the parked samples exact where possible
+    const bool fix_on = env_int("RT_SPEC_FIX", 0) != 0;  // measured neutral: off by default
+    auto pass = [&](const Lane &q, auto &&launch, uint32_t n0, int cap, bool fix = false) {
         const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
         for (int r = 0; r <= rounds && e == hipSuccess; r++) {
             rtk::Cont ct{};
@@ -514,6 +516,11 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                 ct.in = q.cont[(r - 1) & 1].as<float4>();
                 ct.in_count = q.cnt + 16 * std::min(r - 1, 15);
                 n_units = uint32_t(cap) * rtk::kBlock;
+                if (fix && fix_on) {
+                    e = rtk::launch_iow03_fix(f, R, q.cont[(r - 1) & 1].as<float4>(), ct.in_count,
+                                              cap * rtk::kBlock, q.st);
+                    if (e != hipSuccess) break;
+                }
             }
             if (r < rounds) {
                 ct.out = q.cont[r & 1].as<float4>();
@@ -546,7 +553,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         s->last_kernel = "k_iow03a";
         s->last_launches = 1;
         if (e == hipSuccess)
-            e = rtk::launch_iow03_async(f, scene, R, s->counter.as<unsigned>(), ++s->epoch,
+            e = rtk::launch_iow03_async(f, scene, R, s->counter.as<unsigned>(), R.epoch,
                                         s->cus * rtk::resident_blocks_per_cu(8), st);
         if (e != hipSuccess) {
             std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
@@ -583,7 +590,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         RG.fb_count = sc + 32 * g + 16;
         const size_t nmax = size_t(cnt_g) * S;  // list bound for this group
         e = hipStreamWaitEvent(L.st, s->ev_start, 0);
-        if (S > 1 && e == hipSuccess) pass(L, spec(RG, rtk::kSpecRest), cnt_g * (S - 1), cap_s);
+        if (S > 1 && e == hipSuccess) pass(L, spec(RG, rtk::kSpecRest), cnt_g * (S - 1), cap_s, true);
         for (int it = 0; it < iters && e == hipSuccess; it++) {
             e = hipMemsetAsync(RG.list_count, 0, sizeof(unsigned), L.st);
             if (e == hipSuccess) e = rtk::launch_iow03_resolve(f, RG, false, nullptr, L.st);
@@ -598,8 +605,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                     e = rtk::sort_pairs_desc(k1, k2, RG.list, l2, nmax, GL.temp.p, GL.temp_bytes, 24, L.st);
                 rtk::SpecRecs R2 = RG;
                 R2.list = l2;
-                if (e == hipSuccess) pass(L, spec(R2, rtk::kSpecList), uint32_t(nmax), cap_s);
-            } else if (e == hipSuccess) pass(L, spec(RG, rtk::kSpecList), uint32_t(nmax), cap_s);
+                if (e == hipSuccess) pass(L, spec(R2, rtk::kSpecList), uint32_t(nmax), cap_s, true);
+            } else if (e == hipSuccess) pass(L, spec(RG, rtk::kSpecList), uint32_t(nmax), cap_s, true);
         }
         if (e == hipSuccess) e = hipMemsetAsync(RG.fb_count, 0, sizeof(unsigned), L.st);
         if (e == hipSuccess) e = rtk::launch_iow03_resolve(f, RG, true, s->ws_state.as<float4>(), L.st);

@@ -683,11 +683,37 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     uint32_t u = 0, urays = 0;
     int skip = 0;
     f3 sample = f3{0, 0, 0};
+    const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
+    // start unit u (sample s of pixel pu) with assumed stack RI a.xyz in entries 1..3
+    auto begin = [&](uint32_t u_, float4 a) {
+        u = u_;
+        const uint32_t pu = u % R.P;
+        const int s = (int)(u / R.P);
+        const UnitPix px = unit_pixel(f, pu);
+        busy = true;
+        c.seg = c.nodes = c.prims = c.drops = c.nans = 0;
+        urays = 0;
+        skip = 0;
+        sample = f3{0, 0, 0};
+        K.size = 0; K.wmask = 0; K.rmask = 0;
+        K.at(0, 7) = 0.0f; K.at(1, 7) = a.x; K.at(2, 7) = a.y; K.at(3, 7) = a.z;
+        const float sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
+        const float sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
+        f3 ro, rd;
+        iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
+        if (f.show_normal) {  // one ray, no stack: the normal is the sample
+            sample = iow_launch_ray<BCAP>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
+            urays = 1;
+        } else K.push(ro, rd, 1.0f, 1.0f, 0, c);
+    };
     for (;;) {
         const uint32_t q = fetch_unit(counter, live && !busy);
         if (live && !busy) {
             if (q >= total) live = false;
-            else if (ct.in) {  // resume a parked lane
+            else if (ct.in && ct.in[(size_t)q * kContSlots + 12].y != 0.0f) {  // doomed while parked: restart exact
+                u = __float_as_uint(ct.in[(size_t)q * kContSlots].x);
+                begin(u, R.assume[u]);
+            } else if (ct.in) {  // resume a parked lane
                 const float4 *p = ct.in + (size_t)q * kContSlots;
                 const float4 m = p[0], a = p[1], b = p[2];
                 u = __float_as_uint(m.x); skip = __float_as_int(m.y); K.size = __float_as_int(m.z);
@@ -705,27 +731,8 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 // in R.order (heaviest sample 0 first); kSpecList: the re-execution list
                 u = mode == kSpecList ? R.list[q]
                     : (mode == kSpecFirst ? q : (1u + q % (R.S - 1)) * R.P + R.order[R.order_base + q / (R.S - 1)]);
-                const uint32_t pu = u % R.P;
-                const int s = (int)(u / R.P);
-                const UnitPix px = unit_pixel(f, pu);
-                if (px.in_image) {
-                    busy = true;
-                    c.seg = c.nodes = c.prims = c.drops = c.nans = 0;
-                    urays = 0;
-                    skip = 0;
-                    sample = f3{0, 0, 0};
-                    K.size = 0; K.wmask = 0; K.rmask = 0;
-                    const float4 a = mode == kSpecFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : R.assume[u];
-                    K.at(0, 7) = 0.0f; K.at(1, 7) = a.x; K.at(2, 7) = a.y; K.at(3, 7) = a.z;
-                    const float sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
-                    const float sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
-                    f3 ro, rd;
-                    iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
-                    if (f.show_normal) {  // one ray, no stack: the normal is the sample
-                        sample = iow_launch_ray<BCAP>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
-                        urays = 1;
-                    } else K.push(ro, rd, 1.0f, 1.0f, 0, c);
-                }
+                if (unit_pixel(f, u % R.P).in_image)
+                    begin(u, mode == kSpecFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : R.assume[u]);
             }
         }
         if (__ballot(live) == 0) break;
@@ -736,7 +743,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 p[0] = make_float4(ubits(u), ibits(skip), ibits(K.size), ubits(K.wmask | (K.rmask << 4)));
                 p[1] = make_float4(sample.x, sample.y, sample.z, ubits(urays));
                 p[2] = make_float4(ubits(c.seg), ubits(c.nodes), ubits(c.prims), ubits(c.drops));
-                p[12] = make_float4(ubits(c.nans), 0.0f, 0.0f, 0.0f);
+                p[12] = make_float4(ubits(c.nans), 0.0f, 0.0f, 0.0f);  // .y: restart flag (k_iow03_fix)
                 float *fl = reinterpret_cast<float *>(p + 3);
                 for (int k = 0; k < kFl; k++) fl[k] = K.base[k * kBlock];
                 if constexpr (NARROW)
@@ -753,7 +760,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         }
         DBG_CYC(f, c, kDbgCycSeg, t_seg);
         if (busy && K.size == 0) {  // sample done: record it
-            R.col[u] = make_float4(sample.x, sample.y, sample.z, ubits(K.rmask | (K.wmask << 4)));
+            R.col[u] = make_float4(sample.x, sample.y, sample.z, ubits(K.rmask | (K.wmask << 4) | done_tag));
             R.fin[u] = make_float4(K.at(1, 7), K.at(2, 7), K.at(3, 7), ubits(c.prims));
             R.ctr[u] = make_uint4(c.seg, c.drops, c.nans, c.nodes);
             busy = false;
@@ -761,6 +768,56 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     }
     if (c.wdbg && (threadIdx.x & 63) == 0)
         for (int i = 0; i < kDbgSlots; i++) atomicAdd(f.dbg + i, c.wdbg[i]);
+}
+
+// Between launches of a sample-parallel pass (a kernel boundary, so every record written so far
+// is visible): for each parked sample whose pixel's earlier samples are all finished and valid,
+// the exact incoming stack state E is known.  Entries the sample neither read nor wrote are set
+// to E (exact: it would have started with them); if an entry it already read differs from E,
+// it is doomed and restarts with E on resume.  Either way its assumption becomes exact, so long
+// samples stop waiting for a later resolve pass to be found wrong.
+__global__ __launch_bounds__(kBlock) void k_iow03_fix(Frame f, SpecRecs R, float4 *cont, const unsigned *count) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= *count) return;  // no cross-lane work in this kernel
+    float4 *p = cont + (size_t)i * kContSlots;
+    const uint32_t u = __float_as_uint(p[0].x);
+    if (p[12].y != 0.0f) return;
+    const uint32_t pu = u % R.P, s = u / R.P;
+    const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
+    unsigned E1 = 0, E2 = 0, E3 = 0;
+    for (uint32_t t = 0; t < s; t++) {
+        const size_t uu = (size_t)t * R.P + pu;
+        const unsigned fl = __float_as_uint(R.col[uu].w);
+        if ((fl & 0xffff0100u) != done_tag) return;  // an earlier sample is still running
+        const float4 a = R.assume[uu];
+        const unsigned rm = fl & 15u, wm = (fl >> 4) & 15u;
+        if (((rm & 2u) && __float_as_uint(a.x) != E1) || ((rm & 4u) && __float_as_uint(a.y) != E2) ||
+            ((rm & 8u) && __float_as_uint(a.z) != E3))
+            return;  // an earlier sample is itself wrong: E is not known yet
+        const float4 fn = R.fin[uu];
+        if (wm & 2u) E1 = __float_as_uint(fn.x);
+        if (wm & 4u) E2 = __float_as_uint(fn.y);
+        if (wm & 8u) E3 = __float_as_uint(fn.z);
+    }
+    const unsigned masks = __float_as_uint(p[0].w), wm = masks & 15u, rm = masks >> 4;
+    float4 a = R.assume[u];
+    const unsigned E[3] = {E1, E2, E3};
+    float *av = &a.x;
+    bool doomed = false;
+    for (int k = 1; k <= 3; k++)
+        if (((rm >> k) & 1u) && __float_as_uint(av[k - 1]) != E[k - 1]) doomed = true;
+    if (doomed) {
+        R.assume[u] = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
+        p[12].y = 1.0f;
+        return;
+    }
+    float *fl = reinterpret_cast<float *>(p + 3);  // parked stack, [entry*9 + field], RI = field 7
+    for (int k = 1; k <= 3; k++)
+        if (!((wm >> k) & 1u) && !((rm >> k) & 1u)) {
+            fl[k * 9 + 7] = __uint_as_float(E[k - 1]);
+            av[k - 1] = __uint_as_float(E[k - 1]);
+        }
+    R.assume[u] = a;
 }
 
 __global__ __launch_bounds__(kBlock) void k_iow03s(Frame f, IowScene S, SpecRecs R, int mode, Cont ct,
@@ -1608,6 +1665,12 @@ hipError_t launch_iow03_async(const Frame &f, const IowScene &sc, const SpecRecs
     hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_iow03a, dim3(blocks > 0 ? blocks : 1), dim3(kBlock), 0, s, f, sc, R, counter, epoch);
+    return hipGetLastError();
+}
+hipError_t launch_iow03_fix(const Frame &f, const SpecRecs &R, float4 *cont, const unsigned *count, int max_lanes,
+                            hipStream_t s) {
+    const unsigned blocks = (unsigned)((max_lanes + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_iow03_fix, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, cont, count);
     return hipGetLastError();
 }
 hipError_t launch_iow03_keys0(const Frame &f, const SpecRecs &R, unsigned *key, hipStream_t s) {

@@ -90,6 +90,7 @@ struct SpecRecs {
     const uint32_t *order;  // pixel units, heaviest sample 0 first (kSpecRest)
     uint32_t order_base, order_n;  // this group's slice of `order` (order_n == 0: all P units)
     uint4 *pstate;     // asynchronous windows: per pixel unit 3 x uint4 of frontier state
+    uint32_t epoch;    // frame tag: finished records carry it in their flags
 };
 enum { kSpecFirst = 0, kSpecRest = 1, kSpecList = 2 };
 
@@ -130,6 +131,10 @@ hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipS
 // every pixel's samples, validation and re-runs inside one persistent launch; writes the pixels
 hipError_t launch_iow03_async(const Frame &f, const IowScene &sc, const SpecRecs &R, unsigned *counter,
                               unsigned epoch, int blocks, hipStream_t s);
+// between launches of a pass: make parked samples exact where their pixel's earlier samples are
+// all finished and validated (patch unread stack entries, or restart a doomed sample)
+hipError_t launch_iow03_fix(const Frame &f, const SpecRecs &R, float4 *cont, const unsigned *count, int max_lanes,
+                            hipStream_t s);
 // sort keys = sample 0's ray count per pixel unit (0 for tile padding)
 hipError_t launch_iow03_keys0(const Frame &f, const SpecRecs &R, unsigned *key, hipStream_t s);
 // after the kSpecFirst pass: assumptions for samples 1.. and the per-pixel ordering keys

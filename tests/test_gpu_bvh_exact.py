@@ -7,6 +7,7 @@
 - RT_SPEC_ITERS=0/1: fewer resolve passes, more pixels finished by the sequential kernel;
 - RT_SPEC_GROUPS=2/7: pixel groups on separate streams;
 - RT_IOW_ASYNC=1: asynchronous windows (per-wave frontiers) instead of global resolve passes;
+- RT_SPEC_FIX=1: mid-pass correction of parked samples (patch / restart with the exact state);
 - INW: RT_INW_SPEC=0 (per-pixel sequential samples) and RT_SPEC_MAX_GB tiny (sample chunks).
 Each must give a bit-identical image of the final scene with identical ray counts.  The
 renders run in subprocesses because the switches are read by the library at scene build /
@@ -44,7 +45,7 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     out = str(tmp_path / f"img_{len(os.listdir(tmp_path))}.npy")
     env = dict(os.environ)
     for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS", "RT_IOW_SPEC", "RT_SPEC_ITERS",
-              "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_SPEC_GROUPS", "RT_IOW_ASYNC"):
+              "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_SPEC_GROUPS", "RT_IOW_ASYNC", "RT_SPEC_FIX"):
         env.pop(k, None)
     env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out, preset=scene[0], seed=scene[1], n_hint=scene[2])
@@ -63,6 +64,7 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     ({"RT_SPEC_ITERS": "0"}, 300, 200, 16),
     ({"RT_SPEC_ITERS": "1"}, 300, 200, 16),
     ({"RT_IOW_ASYNC": "1"}, 600, 400, 8),
+    ({"RT_SPEC_FIX": "1"}, 600, 400, 12),
     ({"RT_SPEC_GROUPS": "2"}, 300, 200, 12),
     ({"RT_SPEC_GROUPS": "7", "RT_SPEC_ITERS": "2"}, 300, 200, 16),
 ])
