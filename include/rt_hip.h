@@ -49,7 +49,7 @@ extern "C" {
 #define RT_E_ARG        -1   /* bad argument (null pointer, non-positive size, bad layout) */
 #define RT_E_HIP        -2   /* a HIP runtime call failed */
 #define RT_E_NODEVICE   -3   /* no usable gfx950 device */
-#define RT_E_UNSUPPORTED -4  /* a feature the path does not implement (e.g. TextureIndex > 0) */
+#define RT_E_UNSUPPORTED -4  /* a feature the call cannot serve (e.g. TextureIndex > 0 with no texture bound) */
 
 /* Camera uniforms.
  *   IOW-01: u_CameraPosn, u_CameraDirn, u_FocusDist            (01_Adding_Sphere/computeShaderSrc.glsl:5-7)
@@ -112,6 +112,55 @@ int rt_render_inw(const float *geom /* N*28, layout 1 (BVH.h:12-19) or 4 (lights
                   const rt_camera *cam, const rt_params *p,
                   float *rgba /* W*H*4 */, float *depth /* W*H, may be NULL */, rt_stats *st);
 
+/* ---- textures --------------------------------------------------------
+ * INW-04 material textures, u_MaterialTextures[u_NumOfTexture2D]
+ * (04_Lights_Camera_And_Action/computeShaderSrc.glsl:10, bound from slot 2 by
+ * GeometryData_04::BindExtraData, lights.cpp:18-22).  texels: row 0 first (the GL upload
+ * order; stbi flips on load, utility.cpp:217), channels 3 (GL_RGB8) or 4 (GL_RGBA8),
+ * tightly packed.  An object with TextureIndex k in 1..n_tex multiplies its colour by the
+ * nearest texel (GL_NEAREST, GL_REPEAT: a compute shader samples level 0 with the
+ * magnification filter, utility.cpp:182-193) of its cube-projected object-space hit point
+ * (04...glsl:416-464); TextureIndex > n_tex leaves the colour as is. */
+typedef struct rt_texture {
+    const uint8_t *texels;
+    int width, height, channels;
+} rt_texture;
+
+int rt_render_inw_tex(const float *geom, uint32_t n, int layout, const float *nodes, const float *lights,
+                      uint32_t n_lights, const rt_texture *tex, int n_tex, const rt_camera *cam,
+                      const rt_params *p, float *rgba, float *depth, rt_stats *st);
+
+/* Noise textures <- Helper::Noise::MakeTexture<glm::vec3>  Utilities/utility.h:69-192
+ * (Snoise2 / Fbm2 / Turbulance, Utilities/utility.cpp:609-769; the stage UI calls it with
+ * 600 x 100, gradient {0, 1}, lights.cpp:206).  rgb_out: width*height*3 bytes (GL_RGB8 texels,
+ * row 0 first).  gradient: n_grad rgb triples (a list shorter than 2 gets black in front,
+ * then white at the end, as MakeTexture does).  width must be one the reference's four
+ * column batches tile exactly (600 is; others index out of bounds there): RT_E_ARG
+ * otherwise, and for a constant noise field (the reference divides by zero). */
+#define RT_NOISE_SIMPLEX    0
+#define RT_NOISE_FBM        1
+#define RT_NOISE_TURBULENCE 2
+int rt_noise_texture(int width, int height, int type, const float *gradient, int n_grad, float freq, float lac,
+                     float gain, int octaves, uint8_t *rgb_out, int device, double *ms);
+size_t rt_noise_workspace_bytes(int width, int height);
+/* Device pointers, never synchronises.  A constant noise field writes zeros and sets the
+ * third uint32 of d_ws to 1. */
+int rt_noise_texture_async(int width, int height, int type, const float *gradient, int n_grad, float freq,
+                           float lac, float gain, int octaves, uint8_t *d_rgb_out, void *d_ws, size_t ws_bytes,
+                           void *stream);
+
+/* Re-projection <- TEXTURE_2D::LoadFromDiskToGPU(location, loadAs, mapTo)
+ * Utilities/utility.cpp:266-463 (MercatorToCubic / CubicToMercator); load_as == map_to copies.
+ * Where the reference is undefined: the output starts zeroed, the later loop position wins a
+ * texel two positions store to, a load past the last texel reads the last texel. */
+#define RT_MAP_MERCATOR 0
+#define RT_MAP_CUBIC    1
+int rt_texture_remap(const uint8_t *in, int width, int height, int channels, int load_as, int map_to,
+                     uint8_t *out, int device, double *ms);
+size_t rt_remap_workspace_bytes(int width, int height);
+int rt_texture_remap_async(const uint8_t *d_in, int width, int height, int channels, int load_as, int map_to,
+                           uint8_t *d_out, void *d_ws, size_t ws_bytes, void *stream);
+
 /* LBVH builder: aabbs = N*(min xyz, max xyz) in geometry order -> (2N-1)*8 floats. */
 int rt_lbvh_build(const float *aabbs, uint32_t n, float *nodes_out);
 
@@ -135,6 +184,10 @@ rt_dev_scene *rt_dev_scene_iow03(const float *types, const float *records, uint3
                                  int spp, int device);
 rt_dev_scene *rt_dev_scene_inw(const float *geom, uint32_t n, int layout, const float *nodes,
                                const float *lights, uint32_t n_lights, int spp, int device);
+/* The same with material textures bound (see rt_texture); copied to the device. */
+rt_dev_scene *rt_dev_scene_inw_tex(const float *geom, uint32_t n, int layout, const float *nodes,
+                                   const float *lights, uint32_t n_lights, const rt_texture *tex, int n_tex,
+                                   int spp, int device);
 void rt_dev_scene_free(rt_dev_scene *s);
 
 /* Render one tile list.  tiles: device int array of n_tiles (tx, ty) pairs of tile_size^2
@@ -148,6 +201,27 @@ int rt_render_tiles_async(rt_dev_scene *s, const rt_camera *cam, const rt_params
 /* Render the rectangle in p->tile_* into a full W*H image resident on the device. */
 int rt_render_image_async(rt_dev_scene *s, const rt_camera *cam, const rt_params *p,
                           float *d_rgba, float *d_depth, uint64_t *d_counters, void *stream);
+
+/* ---- progressive display -------------------------------------------------
+ * Tile order <- Adding_Materials::OnUpdate  In-One-Weekend/03_Shadows_and_Materials/materials.cpp:84-152:
+ * the drawable tiles of the centre-out square spiral over tile_w x tile_h tiles, each as
+ * (tx, ty, dispatch_w, dispatch_h); the last tile index of an axis is dispatched W % tile wide
+ * (materials.cpp:142-143; 0 when the tile divides W, as in the reference).  Writes up to cap
+ * quadruples to out (may be NULL) and returns the number of tiles. */
+int rt_tile_spiral(int width, int height, int tile_w, int tile_h, int *out, int cap);
+/* One progressive update (OnUpdate with m_NumberOfTilesAtATime = count): renders tiles
+ * [first, first + count) of that order into the full W*H device image (p->tile_* ignored).
+ * Returns the next cursor (== rt_tile_spiral's count when the frame is complete) or an
+ * error. */
+int rt_render_spiral_async(rt_dev_scene *s, const rt_camera *cam, const rt_params *p, int tile_w, int tile_h,
+                           int first, int count, float *d_rgba, float *d_depth, uint64_t *d_counters,
+                           void *stream);
+/* Display pass <- the fullscreen-quad blit into the RGBA8 framebuffer
+ * (In-Next-Week/01_BoundingVolumeHierarchy/BVH.cpp:6-43; materials.cpp:154-161): the colour
+ * image, or with use_depth the depth image as (d, d, d, 1), converted as GL stores unorm8
+ * (clamp to [0,1], round to nearest, NaN -> 0).  d_out: W*H*4 bytes. */
+int rt_display_rgba8_async(const float *d_rgba, const float *d_depth, int width, int height, int use_depth,
+                           uint8_t *d_out, void *stream);
 
 /* ---- diagnostics ---------------------------------------------------------------------
  * d_buf: device array of 16 uint64 (or NULL to disable).  While set, the IOW-03 kernel adds

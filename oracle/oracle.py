@@ -25,8 +25,17 @@ def load():
         lib.orc_num_threads.restype = C.c_int
         lib.orc_set_threads.argtypes = [C.c_int]
         for fn in ("orc_render_iow01", "orc_render_iow03", "orc_render_inw", "orc_lbvh_build",
-                   "orc_pack_iow03", "orc_pack_inw", "orc_sample_tables"):
+                   "orc_pack_iow03", "orc_pack_inw", "orc_sample_tables", "orc_render_inw_tex",
+                   "orc_noise_texture", "orc_texture_remap"):
             getattr(lib, fn).restype = C.c_int
+        lib.orc_noise_texture.argtypes = [C.c_int, C.c_int, C.c_int, _FP, C.c_int, C.c_float, C.c_float,
+                                          C.c_float, C.c_int, C.c_void_p]
+        lib.orc_texture_remap.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        for fn in ("orc_dm_atan2", "orc_dm_acos"):
+            getattr(lib, fn).restype = C.c_double
+        lib.orc_dm_atan2.argtypes = [C.c_double, C.c_double]
+        lib.orc_dm_acos.argtypes = [C.c_double]
+        lib.orc_dm_sincos.argtypes = [C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         _lib = lib
     return _lib
 
@@ -79,12 +88,44 @@ def render(scene, params=None):
     else:
         depth = np.zeros((p.height, p.width), np.float32)
         lights = scene.lights if scene.lights is not None and len(scene.lights) else None
-        rc = lib.orc_render_inw(_f(scene.geom), C.c_uint32(scene.n), C.c_int(scene.layout), _f(scene.nodes),
-                                _f(lights), C.c_uint32(scene.n_lights), C.byref(scene.camera), C.byref(p),
-                                _f(rgba), _f(depth), C.byref(st))
+        tex = getattr(scene, "textures", None) or []
+        keep = [np.ascontiguousarray(t, np.uint8) for t in tex]
+        arr = (_OrcTexture * max(1, len(keep)))()
+        for i, t in enumerate(keep):
+            arr[i] = _OrcTexture(t.ctypes.data, t.shape[1], t.shape[0], t.shape[2])
+        rc = lib.orc_render_inw_tex(_f(scene.geom), C.c_uint32(scene.n), C.c_int(scene.layout), _f(scene.nodes),
+                                    _f(lights), C.c_uint32(scene.n_lights), arr, C.c_uint32(len(keep)),
+                                    C.byref(scene.camera), C.byref(p), _f(rgba), _f(depth), C.byref(st))
     if rc:
         raise RuntimeError(f"oracle render -> {rc}")
     return rgba, depth, _sd(st)
+
+
+class _OrcTexture(C.Structure):
+    _fields_ = [("texels", C.c_void_p), ("width", C.c_int), ("height", C.c_int), ("channels", C.c_int)]
+
+
+def noise_texture(width=600, height=100, kind=0, gradient=((0, 0, 0), (1, 1, 1)), freq=0.01, lac=2.0, gain=0.5,
+                  octaves=5):
+    """CPU restatement of Helper::Noise::MakeTexture<glm::vec3> (utility.h:69-192)."""
+    g = np.ascontiguousarray(np.asarray(gradient, np.float32).reshape(-1, 3))
+    out = np.zeros((height, width, 3), np.uint8)
+    rc = load().orc_noise_texture(width, height, kind, _f(g) if len(g) else None, len(g), freq, lac, gain, octaves,
+                                  out.ctypes.data)
+    if rc:
+        raise RuntimeError(f"orc_noise_texture -> {rc}")
+    return out
+
+
+def texture_remap(img, load_as, map_to):
+    """CPU restatement of LoadFromDiskToGPU's re-projection (utility.cpp:266-463)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros_like(img)
+    rc = load().orc_texture_remap(img.ctypes.data, img.shape[1], img.shape[0], img.shape[2], load_as, map_to,
+                                  out.ctypes.data)
+    if rc:
+        raise RuntimeError(f"orc_texture_remap -> {rc}")
+    return out
 
 
 def lbvh_build(aabbs):

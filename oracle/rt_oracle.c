@@ -469,6 +469,8 @@ typedef struct {
     int layout, spp, max_bounces;
     const float *sf;
     v3 camdir;
+    const orc_texture *tex; /* u_MaterialTextures[u_NumOfTexture2D] (04.glsl:10) */
+    uint32_t n_tex;
 } inw_scene;
 
 typedef struct { v3 pos, scale, delta; m3 R; int type; float extra; } xform_t;
@@ -614,6 +616,54 @@ static int is_lit_geom(const inw_scene *S, uint32_t in) { /* 04.glsl:468-474 */
     return r;
 }
 
+/* texture(u_MaterialTextures[k], st) of a compute shader: no derivatives, so lambda = 0 and
+ * the magnification filter applies -- GL_NEAREST (utility.cpp:182 Upload(..., GL_LINEAR,
+ * GL_NEAREST)) -- with GL_REPEAT wrapping (utility.cpp:191-192): texel (floor(s*w) mod w,
+ * floor(t*h) mod h) of an RGB8 / RGBA8 image, each channel c/255 (unorm8 -> float).
+ * The texel address is computed in binary32 (the driver's fixed-point addressing is not
+ * observable here: parity unpinned). */
+static int tex_wrap(float u, int size) {
+    float f = floorf(u);
+    if (!(f == f) || f > 2147483520.0f || f < -2147483520.0f) return 0; /* NaN / inf -> texel 0 */
+    long long i = (long long)f % size;
+    return (int)(i < 0 ? i + size : i);
+}
+static v3 tex_fetch(const orc_texture *t, float s, float tt) {
+    const int i = tex_wrap(s * (float)t->width, t->width), j = tex_wrap(tt * (float)t->height, t->height);
+    const uint8_t *px = t->texels + ((size_t)j * t->width + i) * (size_t)t->channels;
+    return V3((float)px[0] / 255.0f, (float)px[1] / 255.0f, (float)px[2] / 255.0f);
+}
+
+/* FillHitMaterialData 04.glsl:416-464, the TextureIndex > 0 branch: cube-projection UV of the
+ * object-space hit position, colour *= texel */
+static v3 tex_color(const orc_texture *t, v3 lp) {
+    lp = normalize(lp);
+    float mx = lp.x;
+    uint32_t face = mx > 0 ? 1u : 3u;
+    v3 fd = mul(V3(1, 0, 0), mx > 0 ? 1.0f : -1.0f);
+    for (int i = 1; i < 3; i++) {
+        const float li = v3get(lp, i);
+        if (fabsf(mx) < fabsf(li)) {
+            mx = li;
+            face = mx > 0 ? (i == 1 ? 0u : 2u) : (i == 1 ? 5u : 4u);
+            fd = mul(V3((float)(i == 0), (float)(i == 1), (float)(i == 2)), mx > 0 ? 1.0f : -1.0f);
+        }
+    }
+    lp = mul(lp, rcp(dot(lp, fd)));
+    lp = mul(lp, 0.5f);
+    lp = add(lp, V3(0.5f, 0.5f, 0.5f));
+    float u = 0, v = 0;
+    switch (face) {
+        case 0: u = lp.x; v = 1.0f - lp.z; break;
+        case 1: u = 1.0f - lp.y; v = 1.0f - lp.z; break;
+        case 2: u = lp.x; v = lp.y; break;
+        case 3: u = lp.z; v = lp.y; break;
+        case 4: u = 1.0f - lp.y; v = 1.0f - lp.x; break;
+        default: u = lp.z; v = 1.0f - lp.x; break;
+    }
+    return tex_fetch(t, (float)face * 0.16666f + u * 0.16666f, v);
+}
+
 /* deviateWithLinmit90deg BVH.glsl:28-46 (power == 1) */
 static v3 deviate(const inw_scene *S, v3 dir, float tan_theta, int s) {
     float ap = (2.0f * tan_theta) * 0.5f;
@@ -681,6 +731,11 @@ static void inw_sample(const inw_scene *S, int px, int py, int W, int H, float s
             } else {   /* FillHitMaterialData 04.glsl:403-415 (TextureIndex == 0 path) */
                 m_ri = extra; m_refr = f[20]; m_refl = f[21]; m_srfr = f[22]; m_srfl = f[23];
                 m_color = V3(f[24], f[25], f[26]);
+                const uint32_t ti = f2u(f[27] + 0.1f);
+                if (ti > 0 && ti <= S->n_tex) { /* :416; local posn :569 (Position without motion) */
+                    const xform_t x = fetch_xform(S, (int)fg);
+                    m_color = mulv(m_color, tex_color(S->tex + (ti - 1), m3tmul(x.R, sub(hitpoint, x.pos))));
+                }
             }
             surr = surrounding_ri(S, &K, add(hitpoint, mul(normal, 0.001f)), ratio, c);
         } else {
@@ -755,13 +810,23 @@ static void inw_sample(const inw_scene *S, int px, int py, int W, int H, float s
 int orc_render_inw(const float *geom, uint32_t n, int layout, const float *nodes,
                    const float *lights, uint32_t n_lights, const orc_camera *cam,
                    const orc_params *p, float *rgba, float *depth, orc_stats *st) {
+    return orc_render_inw_tex(geom, n, layout, nodes, lights, n_lights, NULL, 0, cam, p, rgba, depth, st);
+}
+
+int orc_render_inw_tex(const float *geom, uint32_t n, int layout, const float *nodes,
+                       const float *lights, uint32_t n_lights, const orc_texture *tex, uint32_t n_tex,
+                       const orc_camera *cam, const orc_params *p, float *rgba, float *depth, orc_stats *st) {
     if (!geom || !nodes || !cam || !p || !rgba || n == 0 || p->width <= 0 || p->height <= 0 || p->spp < 1)
         return -1;
     if (layout != 1 && layout != 4) return -1;
     if (n_lights > 0 && !lights) return -1;
-    if (layout == 4)
+    if (n_tex > 0 && !tex) return -1;
+    for (uint32_t k = 0; k < n_tex; k++)
+        if (!tex[k].texels || tex[k].width <= 0 || tex[k].height <= 0 || (tex[k].channels != 3 && tex[k].channels != 4))
+            return -1;
+    if (layout == 4 && n_tex == 0)
         for (uint32_t g = 0; g < n; g++)
-            if ((uint32_t)(geom[(size_t)g * 28 + 27] + 0.1f) > 0) return -4; /* texture path: not in scope */
+            if (f2u(geom[(size_t)g * 28 + 27] + 0.1f) > 0) return -4; /* textured objects need textures */
     double t0 = now_ms();
     const int W = p->width, H = p->height, spp = p->spp;
     int x0 = p->tile_x0, y0 = p->tile_y0, tw = p->tile_w, th = p->tile_h;
@@ -772,6 +837,8 @@ int orc_render_inw(const float *geom, uint32_t n, int layout, const float *nodes
     S.geom = geom; S.nodes = nodes; S.lights = lights; S.n = n; S.n_lights = layout == 4 ? n_lights : 0;
     S.layout = layout; S.spp = spp; S.max_bounces = p->max_bounces; S.sf = sf;
     S.camdir = V3(cam->dir[0], cam->dir[1], cam->dir[2]);
+    S.tex = layout == 4 ? tex : NULL;
+    S.n_tex = layout == 4 ? n_tex : 0;
     const float sd = 1.0f / (2.0f * (float)tan((double)(cam->fov_y_rad * 0.5f)));
     const v3 P = V3(cam->pos[0], cam->pos[1], cam->pos[2]);
     ctr total = {0, 0, 0, 0, 0, 0};

@@ -58,6 +58,18 @@ int orc_render_inw(const float *geom, uint32_t n, int layout, const float *nodes
                    const float *lights, uint32_t n_lights, const orc_camera *cam,
                    const orc_params *p, float *rgba, float *depth, orc_stats *st);
 
+/* INW-04 material textures: texels row 0 first (GL upload order), channels 3 (RGB8) or 4 (RGBA8) */
+typedef struct { const uint8_t *texels; int width, height, channels; } orc_texture;
+int orc_render_inw_tex(const float *geom, uint32_t n, int layout, const float *nodes,
+                       const float *lights, uint32_t n_lights, const orc_texture *tex, uint32_t n_tex,
+                       const orc_camera *cam, const orc_params *p, float *rgba, float *depth, orc_stats *st);
+/* Helper::Noise::MakeTexture<glm::vec3> (utility.h:69-192): RGB8 texels, width*height*3 */
+int orc_noise_texture(int width, int height, int type, const float *gradient, int n_grad, float freq,
+                      float lac, float gain, int octaves, uint8_t *rgb_out);
+/* TEXTURE_2D::LoadFromDiskToGPU's re-projection (utility.cpp:266-463): load_as / map_to 0 =
+ * MERCATOR, 1 = CUBIC */
+int orc_texture_remap(const uint8_t *in, int width, int height, int channels, int load_as, int map_to,
+                      uint8_t *out);
 int orc_lbvh_build(const float *aabbs, uint32_t n, float *nodes_out);
 int orc_pack_iow03(const orc_geom_desc *g, uint32_t n, float *types, float *records);
 int orc_pack_inw(const orc_geom_desc *g, uint32_t n, int layout, float *geom, float *aabbs,

@@ -108,6 +108,8 @@ struct rt_dev_scene {
     int root_link = 0;   // IOW-03 culling BVH: leftData of the root
     float ri_prior = 1.0f;  // IOW-03: most common refractive index (sample-parallel guess)
     DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
+    DevBuf tex, tex_info;  // INW-04 material textures (float4 texels, (first, w, h, 0) per texture)
+    uint32_t n_tex = 0;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
     uint32_t ws_units = 0;
     size_t ws_temp_bytes = 0;
@@ -239,8 +241,11 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
     return build_tables(s, spp);
 }
 
+int upload_textures(rt_dev_scene *s, const rt_texture *tex, int n_tex);
+
 int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const float *nodes,
-             const float *lights, uint32_t n_lights, int spp) {
+             const float *lights, uint32_t n_lights, const rt_texture *tex, int n_tex, int spp) {
+    if (int rc = upload_textures(s, layout == 4 ? tex : nullptr, layout == 4 ? n_tex : 0); rc != RT_OK) return rc;
     std::vector<float> hot(size_t(n) * rtk::kInwHot, 0.0f), cold(size_t(n) * rtk::kInwCold, 0.0f);
     for (uint32_t j = 0; j < n; j++) {
         const float *f = geom + size_t(j) * 28;
@@ -257,7 +262,12 @@ int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const f
             c[4] = f[25]; c[5] = f[26]; c[6] = f[27]; c[7] = f[20];
         } else {            // lights.h:6-21
             c[0] = f[20]; c[1] = f[21]; c[2] = f[22]; c[3] = f[23];
-            c[4] = f[24]; c[5] = f[25]; c[6] = f[26]; c[7] = f[19];
+            c[4] = f[24]; c[5] = f[25]; c[6] = f[26];
+            // TextureIndex = uint(texel 6.w + 0.1) (04...glsl:414), as uint bits; the RI (f[19])
+            // reaches the kernel as IntersectRay's extra data instead
+            const float ti = f[27] + 0.1f;
+            const uint32_t tu = ti <= 0.0f ? 0u : (ti >= 4294967040.0f ? 0xffffffffu : uint32_t(ti));
+            std::memcpy(&c[7], &tu, 4);
         }
     }
     s->kind = layout == 4 ? 14 : 11;
@@ -463,7 +473,8 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                 e = rtk::launch_iow03(f, sc, ch, ct, n_units, s->counter.as<unsigned>(), s->s_stop, cap, st);
             } else {
                 rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
-                                 s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>()};
+                                 s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>(),
+                                 s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
                 e = rtk::launch_inw(f, sc, ch, ct, n_units, s->counter.as<unsigned>(), s->blocks_cap, st);
             }
         }
@@ -488,7 +499,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     int rc = ensure_workspace(s, P);
     if (rc != RT_OK) return rc;
     const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 6)));
-    const int iters = std::max(0, env_int("RT_SPEC_ITERS", 10));
+    const int iters = std::max(0, env_int("RT_SPEC_ITERS", 1));
     const int groups = S > 1 ? std::max(1, std::min(32, env_int("RT_SPEC_GROUPS", 1))) : 1;
     const size_t gmax = size_t(P + groups - 1) / groups + 1;  // pixels in the largest group
     if ((rc = ensure_cont(s)) != RT_OK) return rc;
@@ -563,9 +574,10 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     }
     if (S > 1) {
         // Entries sample 0 left unwritten: guess 0 (as sample 0 saw them) for samples below
-        // RT_SPEC_PRIOR_FROM, the scene's most common RI from there on (guessing it for early
-        // samples formed long re-run chains, so by default it is never used)
-        const uint32_t prior_from = uint32_t(std::max(1, env_int("RT_SPEC_PRIOR_FROM", 1 << 30)));
+        // RT_SPEC_PRIOR_FROM (2), the scene's most common RI from there on.  The prior misses
+        // far less often (the re-run pass re-traces ~1.5% of the rays instead of ~20%); the
+        // dependent chains it forms are cheap for the validating sequential pass.
+        const uint32_t prior_from = uint32_t(std::max(1, env_int("RT_SPEC_PRIOR_FROM", 2)));
         if (e == hipSuccess)
             e = rtk::launch_iow03_prep(f, R, s->ws_cost.as<unsigned>(), s->ri_prior, prior_from, st);
         if (e == hipSuccess)
@@ -619,6 +631,10 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         ch.order = RG.fb_list;
         ch.order_count = RG.fb_count;
         ch.per_unit_begin = 1;
+        if (env_int("RT_SPEC_VALIDATE", 1) != 0) {  // reuse the records that are still exact
+            ch.rec_col = R.col; ch.rec_fin = R.fin; ch.rec_assume = R.assume; ch.rec_ctr = R.ctr;
+            ch.rec_P = P;
+        }
         if (e == hipSuccess)
             pass(L, [&, ch](const Lane &q, const rtk::Cont &ct, uint32_t n) {
                 return rtk::launch_iow03(f, scene, ch, ct, n, q.counter, s->s_stop, cap_q, q.st);
@@ -649,7 +665,8 @@ int launch_scene_inw_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st, int ns
     R.P = P;
     R.S = uint32_t(f.spp);
     rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
-                     s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>()};
+                     s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>(),
+                     s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
     const int cap = s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 7 : 6);
     const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
     hipError_t e = hipSuccess;
@@ -728,8 +745,78 @@ int render_blocking(rt_dev_scene *s, const rt_camera *cam, const rt_params *p, f
 bool inw_textured(const float *geom, uint32_t n, int layout) {
     if (layout != 4) return false;
     for (uint32_t g = 0; g < n; g++)
-        if (uint32_t(geom[size_t(g) * 28 + 27] + 0.1f) > 0) return true;
+        if (geom[size_t(g) * 28 + 27] + 0.1f >= 1.0f) return true;
     return false;
+}
+
+bool textures_ok(const rt_texture *tex, int n_tex) {
+    if (n_tex < 0 || (n_tex > 0 && !tex)) return false;
+    for (int k = 0; k < n_tex; k++)
+        if (!tex[k].texels || tex[k].width <= 0 || tex[k].height <= 0 || (tex[k].channels != 3 && tex[k].channels != 4) ||
+            size_t(tex[k].width) * size_t(tex[k].height) > (size_t(1) << 31))
+            return false;
+    return true;
+}
+
+// u_MaterialTextures[0..n_tex) (04...glsl:10; bound by GeometryData_04::BindExtraData,
+// lights.cpp:22): unorm8 texels -> float (c / 255, the GL conversion) once, on the host
+int upload_textures(rt_dev_scene *s, const rt_texture *tex, int n_tex) {
+    s->n_tex = 0;
+    if (n_tex == 0) {
+        HIP_OK(s->tex.alloc(16));
+        HIP_OK(s->tex_info.alloc(16));
+        return RT_OK;
+    }
+    size_t total = 0;
+    std::vector<int> info(size_t(n_tex) * 4, 0);
+    for (int k = 0; k < n_tex; k++) {
+        info[4 * k] = int(total);
+        info[4 * k + 1] = tex[k].width;
+        info[4 * k + 2] = tex[k].height;
+        total += size_t(tex[k].width) * size_t(tex[k].height);
+    }
+    if (total > (size_t(1) << 31)) return RT_E_ARG;
+    std::vector<float> texels(total * 4, 0.0f);
+    for (int k = 0; k < n_tex; k++) {
+        const size_t m = size_t(tex[k].width) * size_t(tex[k].height);
+        const int ch = tex[k].channels;
+        float *o = texels.data() + size_t(info[4 * k]) * 4;
+        for (size_t i = 0; i < m; i++) {
+            for (int c = 0; c < 3; c++) o[4 * i + c] = float(tex[k].texels[i * ch + c]) / 255.0f;
+            o[4 * i + 3] = ch == 4 ? float(tex[k].texels[i * ch + 3]) / 255.0f : 1.0f;
+        }
+    }
+    HIP_OK(s->tex.upload(texels.data(), texels.size() * sizeof(float)));
+    HIP_OK(s->tex_info.upload(info.data(), info.size() * sizeof(int)));
+    s->n_tex = uint32_t(n_tex);
+    return RT_OK;
+}
+
+bool noise_args_ok(int width, int height, int type, const float *gradient, int n_grad, int octaves) {
+    return width > 0 && height > 0 && size_t(width) * size_t(height) < (size_t(1) << 31) && type >= 0 && type <= 2 &&
+           octaves >= 0 && n_grad >= 0 && n_grad <= 64 && (n_grad == 0 || gradient) &&
+           rtk::noise_batches_exact(uint32_t(width));
+}
+bool remap_args_ok(int width, int height, int channels, int load_as, int map_to) {
+    return width > 0 && height > 0 && size_t(width) * size_t(height) < (size_t(1) << 31) &&
+           (channels == 3 || channels == 4) && load_as >= 0 && load_as <= 1 && map_to >= 0 && map_to <= 1 &&
+           (load_as == map_to || rtk::noise_batches_exact(uint32_t(width)));
+}
+// device time of the work enqueued by `fn` on the null stream
+template <class F> int timed(F &&fn, double *ms) {
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventRecord(e0, nullptr));
+    const int rc = fn();
+    HIP_OK(hipEventRecord(e1, nullptr));
+    HIP_OK(hipEventSynchronize(e1));
+    float t = 0.0f;
+    (void)hipEventElapsedTime(&t, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (ms) *ms = t;
+    return rc;
 }
 
 }  // namespace
@@ -840,15 +927,22 @@ int rt_render_iow03(const float *types, const float *records, uint32_t n, const 
 int rt_render_inw(const float *geom, uint32_t n, int layout, const float *nodes, const float *lights,
                   uint32_t n_lights, const rt_camera *cam, const rt_params *p, float *rgba, float *depth,
                   rt_stats *st) {
+    return rt_render_inw_tex(geom, n, layout, nodes, lights, n_lights, nullptr, 0, cam, p, rgba, depth, st);
+}
+
+int rt_render_inw_tex(const float *geom, uint32_t n, int layout, const float *nodes, const float *lights,
+                      uint32_t n_lights, const rt_texture *tex, int n_tex, const rt_camera *cam, const rt_params *p,
+                      float *rgba, float *depth, rt_stats *st) {
     if (!geom || !nodes || n == 0 || !cam || !params_ok(p) || !rgba) return RT_E_ARG;
     if (layout != 1 && layout != 4) return RT_E_ARG;
     if (layout == 4 && n_lights > 0 && !lights) return RT_E_ARG;
-    if (inw_textured(geom, n, layout)) return RT_E_UNSUPPORTED;
+    if (!textures_ok(tex, n_tex)) return RT_E_ARG;
+    if (n_tex == 0 && inw_textured(geom, n, layout)) return RT_E_UNSUPPORTED;  // no texture bound
     int rc = check_device(p->device);
     if (rc != RT_OK) return rc;
     std::unique_ptr<rt_dev_scene> s(new (std::nothrow) rt_dev_scene());
     if (!s) return RT_E_ARG;
-    rc = make_inw(s.get(), geom, n, layout, nodes, lights, n_lights, p->spp);
+    rc = make_inw(s.get(), geom, n, layout, nodes, lights, n_lights, tex, n_tex, p->spp);
     if (rc != RT_OK) return rc;
     return render_blocking(s.get(), cam, p, rgba, depth, st);
 }
@@ -905,6 +999,132 @@ int rt_lbvh_build_gpu(const float *aabbs, uint32_t n, float *nodes_out, int devi
     return RT_OK;
 }
 
+size_t rt_noise_workspace_bytes(int width, int height) {
+    return width > 0 && height > 0 ? rtk::noise_workspace_bytes(width, height) : 0;
+}
+
+
+int rt_noise_texture_async(int width, int height, int type, const float *gradient, int n_grad, float freq,
+                           float lac, float gain, int octaves, uint8_t *d_rgb_out, void *d_ws, size_t ws_bytes,
+                           void *stream) {
+    if (!noise_args_ok(width, height, type, gradient, n_grad, octaves) || !d_rgb_out || !d_ws ||
+        ws_bytes < rtk::noise_workspace_bytes(width, height))
+        return RT_E_ARG;
+    const hipError_t e = rtk::noise_texture(width, height, type, gradient, n_grad, freq, lac, gain, octaves, d_rgb_out,
+                                            d_ws, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "[rt_hip] noise texture failed: %s\n", hipGetErrorString(e));
+        return RT_E_HIP;
+    }
+    return RT_OK;
+}
+
+int rt_noise_texture(int width, int height, int type, const float *gradient, int n_grad, float freq, float lac,
+                     float gain, int octaves, uint8_t *rgb_out, int device, double *ms) {
+    if (!noise_args_ok(width, height, type, gradient, n_grad, octaves) || !rgb_out) return RT_E_ARG;
+    int rc = check_device(device);
+    if (rc != RT_OK) return rc;
+    const size_t bytes = size_t(width) * size_t(height) * 3;
+    DevBuf d_out, d_ws;
+    HIP_OK(d_out.alloc(bytes));
+    HIP_OK(d_ws.alloc(rtk::noise_workspace_bytes(width, height)));
+    rc = timed([&] {
+        return rt_noise_texture_async(width, height, type, gradient, n_grad, freq, lac, gain, octaves,
+                                      d_out.as<uint8_t>(), d_ws.p, d_ws.bytes, nullptr);
+    }, ms);
+    if (rc != RT_OK) return rc;
+    uint32_t status = 0;
+    HIP_OK(hipMemcpy(&status, d_ws.as<uint32_t>() + 2, sizeof(status), hipMemcpyDeviceToHost));
+    if (status) return RT_E_ARG;  // degenerate value range (the reference divides by zero)
+    HIP_OK(hipMemcpy(rgb_out, d_out.p, bytes, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+size_t rt_remap_workspace_bytes(int width, int height) {
+    return width > 0 && height > 0 ? rtk::remap_workspace_bytes(width, height) : 0;
+}
+
+int rt_texture_remap_async(const uint8_t *d_in, int width, int height, int channels, int load_as, int map_to,
+                           uint8_t *d_out, void *d_ws, size_t ws_bytes, void *stream) {
+    if (!remap_args_ok(width, height, channels, load_as, map_to) || !d_in || !d_out) return RT_E_ARG;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (load_as == map_to) {
+        e = hipMemcpyAsync(d_out, d_in, size_t(width) * height * channels, hipMemcpyDeviceToDevice, st);
+    } else {
+        if (!d_ws || ws_bytes < rtk::remap_workspace_bytes(width, height)) return RT_E_ARG;
+        e = rtk::texture_remap(d_in, width, height, channels, load_as, d_out, d_ws, st);
+    }
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "[rt_hip] texture remap failed: %s\n", hipGetErrorString(e));
+        return RT_E_HIP;
+    }
+    return RT_OK;
+}
+
+int rt_texture_remap(const uint8_t *in, int width, int height, int channels, int load_as, int map_to, uint8_t *out,
+                     int device, double *ms) {
+    if (!remap_args_ok(width, height, channels, load_as, map_to) || !in || !out) return RT_E_ARG;
+    int rc = check_device(device);
+    if (rc != RT_OK) return rc;
+    const size_t bytes = size_t(width) * size_t(height) * channels;
+    DevBuf d_in, d_out, d_ws;
+    HIP_OK(d_in.upload(in, bytes));
+    HIP_OK(d_out.alloc(bytes));
+    HIP_OK(d_ws.alloc(rtk::remap_workspace_bytes(width, height)));
+    rc = timed([&] {
+        return rt_texture_remap_async(d_in.as<uint8_t>(), width, height, channels, load_as, map_to,
+                                      d_out.as<uint8_t>(), d_ws.p, d_ws.bytes, nullptr);
+    }, ms);
+    if (rc != RT_OK) return rc;
+    HIP_OK(hipMemcpy(out, d_out.p, bytes, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_tile_spiral(int width, int height, int tile_w, int tile_h, int *out, int cap) {
+    if (width <= 0 || height <= 0 || tile_w <= 0 || tile_h <= 0 || cap < 0 || (cap > 0 && !out)) return RT_E_ARG;
+    if (width / tile_w > 32766 || height / tile_h > 32766) return RT_E_ARG;  // int16 tile indices
+    const std::vector<rtamd::SpiralTile> t = rtamd::tile_spiral(width, height, tile_w, tile_h);
+    for (size_t i = 0; i < t.size() && int(i) < cap; i++) {
+        out[4 * i] = t[i].tx; out[4 * i + 1] = t[i].ty; out[4 * i + 2] = t[i].w; out[4 * i + 3] = t[i].h;
+    }
+    return int(t.size());
+}
+
+int rt_render_spiral_async(rt_dev_scene *s, const rt_camera *cam, const rt_params *p, int tile_w, int tile_h,
+                           int first, int count, float *d_rgba, float *d_depth, uint64_t *d_counters,
+                           void *stream) {
+    if (!s || !cam || !params_ok(p) || !d_rgba || tile_w <= 0 || tile_h <= 0 || first < 0 || count < 0)
+        return RT_E_ARG;
+    if (p->width / tile_w > 32766 || p->height / tile_h > 32766) return RT_E_ARG;
+    const std::vector<rtamd::SpiralTile> t = rtamd::tile_spiral(p->width, p->height, tile_w, tile_h);
+    int i = std::min(first, int(t.size()));
+    const int end = int(std::min<size_t>(t.size(), size_t(i) + size_t(count)));
+    for (; i < end; i++) {
+        if (t[size_t(i)].w <= 0 || t[size_t(i)].h <= 0) continue;  // a zero-size dispatch draws nothing
+        rt_params q = *p;
+        q.tile_x0 = t[size_t(i)].tx * tile_w;
+        q.tile_y0 = t[size_t(i)].ty * tile_h;
+        q.tile_w = t[size_t(i)].w;
+        q.tile_h = t[size_t(i)].h;
+        const int rc = rt_render_image_async(s, cam, &q, d_rgba, d_depth, d_counters, stream);
+        if (rc != RT_OK) return rc;
+    }
+    return end;
+}
+
+int rt_display_rgba8_async(const float *d_rgba, const float *d_depth, int width, int height, int use_depth,
+                           uint8_t *d_out, void *stream) {
+    if (width <= 0 || height <= 0 || !d_out || (use_depth ? !d_depth : !d_rgba)) return RT_E_ARG;
+    const hipError_t e = rtk::display_rgba8(d_rgba, d_depth, uint32_t(size_t(width) * size_t(height)), use_depth,
+                                            d_out, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "[rt_hip] display pass failed: %s\n", hipGetErrorString(e));
+        return RT_E_HIP;
+    }
+    return RT_OK;
+}
+
 rt_dev_scene *rt_dev_scene_iow03(const float *types, const float *records, uint32_t n, int spp, int device) {
     if (!types || !records || spp < 1) return nullptr;
     if (check_device(device) != RT_OK) return nullptr;
@@ -917,14 +1137,21 @@ rt_dev_scene *rt_dev_scene_iow03(const float *types, const float *records, uint3
 
 rt_dev_scene *rt_dev_scene_inw(const float *geom, uint32_t n, int layout, const float *nodes, const float *lights,
                                uint32_t n_lights, int spp, int device) {
+    return rt_dev_scene_inw_tex(geom, n, layout, nodes, lights, n_lights, nullptr, 0, spp, device);
+}
+
+rt_dev_scene *rt_dev_scene_inw_tex(const float *geom, uint32_t n, int layout, const float *nodes,
+                                   const float *lights, uint32_t n_lights, const rt_texture *tex, int n_tex,
+                                   int spp, int device) {
     if (!geom || !nodes || n == 0 || spp < 1 || (layout != 1 && layout != 4)) return nullptr;
     if (layout == 4 && n_lights > 0 && !lights) return nullptr;
-    if (inw_textured(geom, n, layout)) return nullptr;
+    if (!textures_ok(tex, n_tex)) return nullptr;
+    if (n_tex == 0 && inw_textured(geom, n, layout)) return nullptr;
     if (check_device(device) != RT_OK) return nullptr;
     rt_dev_scene *s = new (std::nothrow) rt_dev_scene();
     if (!s) return nullptr;
     (void)hipGetDevice(&s->device);
-    if (make_inw(s, geom, n, layout, nodes, lights, n_lights, spp) != RT_OK) { delete s; return nullptr; }
+    if (make_inw(s, geom, n, layout, nodes, lights, n_lights, tex, n_tex, spp) != RT_OK) { delete s; return nullptr; }
     return s;
 }
 

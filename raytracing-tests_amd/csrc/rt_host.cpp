@@ -669,4 +669,30 @@ int scene_preset(int preset, uint32_t seed, int n_hint, std::vector<rt_geom_desc
     }
 }
 
+// materials.cpp:84-152.  The state has the reference's widths (materials.h:110-116: int16
+// indices and ring corners, uint16 maxima, int8 steps); every OnUpdate draws
+// m_NumberOfTilesAtATime drawable tiles, skipping undrawable spiral positions (the goto), so
+// the sequence of drawable tiles is the whole schedule.  The last index of an axis is the
+// partial tile, dispatched W % tile wide (0 when the tile divides W; kept).
+std::vector<SpiralTile> tile_spiral(int W, int H, int tw, int th) {
+    std::vector<SpiralTile> out;
+    const uint16_t mx0 = uint16_t(W / tw), mx1 = uint16_t(H / th);
+    int16_t i0 = int16_t((mx0 - 0.1f) / 2), i1 = int16_t((mx1 - 0.1f) / 2);
+    int16_t r00[2] = {i0, i1}, r01[2] = {i0, int16_t(i1 + 1)};
+    int16_t r10[2] = {int16_t(i0 + 1), int16_t(i1 - 1)}, r11[2] = {int16_t(i0 + 1), int16_t(i1 + 1)};
+    int8_t st[2] = {0, 0};
+    const int lim = (mx0 > mx1 ? mx0 : mx1) + 1;
+    while ((i0 < i1 ? i0 : i1) < lim) {
+        if (i1 == r00[1] && i0 == r00[0]) { r00[0]--; r00[1]--; st[0] = 0; st[1] = 1; }
+        if (i1 == r01[1] && i0 == r01[0]) { r01[0]--; r01[1]++; st[0] = 1; st[1] = 0; }
+        if (i1 == r11[1] && i0 == r11[0]) { r11[0]++; r11[1]++; st[0] = 0; st[1] = -1; }
+        if (i1 == r10[1] && i0 == r10[0]) { r10[0]++; r10[1]--; st[0] = -1; st[1] = 0; }
+        if (i1 > -1 && i1 < mx1 + 1 && i0 > -1 && i0 < mx0 + 1)
+            out.push_back({i0, i1, i0 >= mx0 ? W % tw : tw, i1 >= mx1 ? H % th : th});
+        i0 = int16_t(i0 + st[0]);
+        i1 = int16_t(i1 + st[1]);
+    }
+    return out;
+}
+
 }  // namespace rtamd

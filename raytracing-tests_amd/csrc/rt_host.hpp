@@ -113,6 +113,11 @@ Vec3 front_from_pitch_yaw(float pitch_deg, float yaw_deg, bool normalize);
 // ---- sample tables ----------------------------------------------------------------------
 void sample_tables(int spp, float *sunflower, float *fib, int *ring);
 
+// Progressive tile order of Adding_Materials::OnUpdate (materials.cpp:84-152): the drawable
+// tiles of the centre-out square spiral, each (tx, ty, dispatch_w, dispatch_h)
+struct SpiralTile { int tx, ty, w, h; };
+std::vector<SpiralTile> tile_spiral(int W, int H, int tw, int th);
+
 // ---- presets ----------------------------------------------------------------------------
 int scene_preset(int preset, uint32_t seed, int n_hint, std::vector<rt_geom_desc> &out,
                  rt_cam_desc &cam, rt_params &params);

@@ -594,6 +594,29 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
         }
         DBG_TALLY(f, c, kDbgOuter, busy);
         DBG_T0(f, t_loop);
+        if (ch.rec_col) {
+            // take every following sample whose speculative record assumed the exact stack
+            // state (the RI of the entries it read before writing them) from its record
+            while (busy && K.size == 0 && s < s_end) {
+                const size_t u = (size_t)s * ch.rec_P + unit;
+                const float4 cl = ch.rec_col[u], a = ch.rec_assume[u];
+                const uint32_t fl = __float_as_uint(cl.w), rm = fl & 15u, wm = (fl >> 4) & 15u;
+                if (((rm & 2u) && __float_as_uint(a.x) != __float_as_uint(K.at(1, 7))) ||
+                    ((rm & 4u) && __float_as_uint(a.y) != __float_as_uint(K.at(2, 7))) ||
+                    ((rm & 8u) && __float_as_uint(a.z) != __float_as_uint(K.at(3, 7))))
+                    break;
+                const float4 fn = ch.rec_fin[u];
+                const uint4 ct4 = ch.rec_ctr[u];
+                fc = fc + f3{cl.x, cl.y, cl.z};
+                if (wm & 2u) K.at(1, 7) = fn.x;
+                if (wm & 4u) K.at(2, 7) = fn.y;
+                if (wm & 8u) K.at(3, 7) = fn.z;
+                c.seg += ct4.x; c.drops += ct4.y; c.nans += ct4.z; c.nodes += ct4.w;
+                c.prims += __float_as_uint(fn.w);
+                urays += ct4.x;
+                s++;
+            }
+        }
         if (busy && K.size == 0 && s < s_end) {  // start sample s
             f3 ro, rd;
             iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
@@ -1077,6 +1100,50 @@ __device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame 
     K.push_ray(tip - la, la, 1.0f, 0.0f, c);
 }
 
+// texture(u_MaterialTextures[k], st) in a compute shader: lambda = 0, so the magnification
+// filter GL_NEAREST applies (utility.cpp:182), with GL_REPEAT (utility.cpp:191-192)
+__device__ __forceinline__ int tex_wrap(float u, int size) {
+    const float f = __builtin_floorf(u);
+    if (!(f == f) || f > 2147483520.0f || f < -2147483520.0f) return 0;  // NaN / inf: texel 0
+    const int i = (int)f % size;
+    return i < 0 ? i + size : i;
+}
+// FillHitMaterialData 04...glsl:416-464 (TextureIndex > 0): cube projection of the
+// object-space hit position onto a 6-face strip, nearest texel
+__device__ f3 inw_tex_color(const InwScene &S, uint32_t k, f3 lp) {
+    lp = normalize(lp);
+    float mx = lp.x;
+    uint32_t face = mx > 0 ? 1u : 3u;
+    f3 fd = f3{1, 0, 0} * (mx > 0 ? 1.0f : -1.0f);
+    if (__builtin_fabsf(mx) < __builtin_fabsf(lp.y)) {
+        mx = lp.y;
+        face = mx > 0 ? 0u : 5u;
+        fd = f3{0, 1, 0} * (mx > 0 ? 1.0f : -1.0f);
+    }
+    if (__builtin_fabsf(mx) < __builtin_fabsf(lp.z)) {
+        mx = lp.z;
+        face = mx > 0 ? 2u : 4u;
+        fd = f3{0, 0, 1} * (mx > 0 ? 1.0f : -1.0f);
+    }
+    lp = lp * rcp(dot(lp, fd));
+    lp = lp * 0.5f;
+    lp = lp + f3{0.5f, 0.5f, 0.5f};
+    float u, v;
+    switch (face) {
+        case 0: u = lp.x; v = 1.0f - lp.z; break;
+        case 1: u = 1.0f - lp.y; v = 1.0f - lp.z; break;
+        case 2: u = lp.x; v = lp.y; break;
+        case 3: u = lp.z; v = lp.y; break;
+        case 4: u = 1.0f - lp.y; v = 1.0f - lp.x; break;
+        default: u = lp.z; v = 1.0f - lp.x; break;
+    }
+    const int4 ti = S.tex_info[k];
+    const int i = tex_wrap(((float)face * 0.16666f + u * 0.16666f) * (float)ti.y, ti.y);
+    const int j = tex_wrap(v * (float)ti.z, ti.z);
+    const float4 c = S.tex[(size_t)ti.x + (size_t)j * (size_t)ti.y + (size_t)i];
+    return f3{c.x, c.y, c.z};
+}
+
 // One iteration of out_Pixel's ray loop (01_BVH...glsl:414-597 / 04...glsl:510-713):
 // pop a ray, closest hit, surrounding RI, shadow rays, push reflect/refract, accumulate.
 template <bool LIGHTS>
@@ -1101,8 +1168,16 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         }
         const float4 m0 = S.cold[2 * (int)fg], m1 = S.cold[2 * (int)fg + 1];
         const float m_refr = m0.x, m_refl = m0.y, m_srfr = m0.z, m_srfl = m0.w;
-        const f3 m_color = mk(m1.x, m1.y, m1.z);
+        f3 m_color = mk(m1.x, m1.y, m1.z);
         const float m_ri = LIGHTS ? extra : m1.w;
+        if (LIGHTS && S.n_tex) {  // layout 4 keeps the TextureIndex (uint bits) in m1.w
+            const uint32_t ti = __float_as_uint(m1.w);
+            if (ti - 1u < S.n_tex) {  // 04...glsl:416; local position :569 (no motion offset)
+                const float4 h0 = S.hot[7 * (int)fg], h1 = S.hot[7 * (int)fg + 1], h2 = S.hot[7 * (int)fg + 2];
+                const m3 R{mk(h0.w, h1.x, h1.y), mk(h1.z, h1.w, h2.x), mk(h2.y, h2.z, h2.w)};
+                m_color = mulv(m_color, inw_tex_color(S, ti - 1u, tmul(R, hitpoint - mk(h0.x, h0.y, h0.z))));
+            }
+        }
         const float surr = inw_surrounding_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
         if (LIGHTS) {  // 04...glsl:604-665
             uint32_t is_lit = S.n_lights > 0 ? 0u : (uint32_t)is_lit_geom(S, f2u(fg + 0.1f));

@@ -55,6 +55,11 @@ struct InwScene {
     uint32_t n, n_lights;
     int layout;
     const float *sunflower;  // spp*2
+    // u_MaterialTextures (04...glsl:10): texels as float4 (unorm8 / 255, converted on the
+    // host), tex_info[k] = (first texel, width, height, 0); n_tex = 0: none bound
+    const float4 *tex;
+    const int4 *tex_info;
+    uint32_t n_tex;
 };
 
 // One launch of a chunked render: samples [s_begin, s_end) of every pixel unit.  A pixel's
@@ -70,6 +75,11 @@ struct Chunk {
     unsigned *cost;          // rays per unit in this launch, or null
     const unsigned *order_count;  // device count of `order` entries (null: all units)
     int per_unit_begin;      // first sample of each unit = bits of state[2*unit].w (else s_begin)
+    // sample-parallel records (SpecRecs, below) to validate before running a sample, or null:
+    // a sample whose record assumed the exact incoming stack state is taken from the record
+    const float4 *rec_col, *rec_fin, *rec_assume;
+    const uint4 *rec_ctr;
+    uint32_t rec_P;
 };
 
 // Sample-parallel IOW-03 (DESIGN.md "Sample-parallel speculation").  A unit is one (pixel,
@@ -126,6 +136,19 @@ hipError_t launch_iow03_spec(const Frame &f, const IowScene &sc, const SpecRecs 
 // LBVH build on the device (rt_lbvh.hip); ws = lbvh_workspace_bytes(n) of scratch
 size_t lbvh_workspace_bytes(uint32_t n);
 hipError_t lbvh_build_device(const float *aabb, uint32_t n, float *out, void *ws, size_t ws_bytes, hipStream_t s);
+// Texture producers (rt_texture.hip): noise textures (MakeTexture, utility.h:69-192) and the
+// Mercator <-> cubic re-projection (utility.cpp:266-463).  noise_batches_exact(W): the
+// reference's 4 column batches tile [0, W) (other widths index out of bounds there).
+bool noise_batches_exact(uint32_t W);
+size_t noise_workspace_bytes(int W, int H);
+hipError_t noise_texture(int W, int H, int type, const float *grad, int n_grad, float freq, float lac, float gain,
+                         int octaves, uint8_t *d_rgb, void *d_ws, hipStream_t s);
+// Display pass (rt_display.hip): RGBA32F colour or R32F depth -> RGBA8 framebuffer texels
+hipError_t display_rgba8(const float *rgba, const float *depth, uint32_t n, int use_depth, uint8_t *out,
+                         hipStream_t s);
+size_t remap_workspace_bytes(int W, int H);
+hipError_t texture_remap(const uint8_t *d_in, int W, int H, int C, int load_as, uint8_t *d_out, void *d_ws,
+                         hipStream_t s);
 hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipStream_t s);  // diagnostics
 // asynchronous-window IOW-03 over samples 1.. (after the kSpecFirst pass and the pixel order):
 // every pixel's samples, validation and re-runs inside one persistent launch; writes the pixels

@@ -64,6 +64,10 @@ class RtCamDesc(C.Structure):
                 ("fov_y_deg", C.c_float), ("aperture", C.c_float), ("focus_dist", C.c_float)]
 
 
+class RtTexture(C.Structure):
+    _fields_ = [("texels", C.c_void_p), ("width", C.c_int), ("height", C.c_int), ("channels", C.c_int)]
+
+
 _FP = C.POINTER(C.c_float)
 _IP = C.POINTER(C.c_int)
 _U32P = C.POINTER(C.c_uint32)
@@ -78,12 +82,26 @@ SIGNATURES = {
                                   C.POINTER(RtStats)]),
     "rt_render_inw": (C.c_int, [_FP, C.c_uint32, C.c_int, _FP, _FP, C.c_uint32, C.POINTER(RtCamera),
                                 C.POINTER(RtParams), _FP, _FP, C.POINTER(RtStats)]),
+    "rt_render_inw_tex": (C.c_int, [_FP, C.c_uint32, C.c_int, _FP, _FP, C.c_uint32, C.POINTER(RtTexture), C.c_int,
+                                    C.POINTER(RtCamera), C.POINTER(RtParams), _FP, _FP, C.POINTER(RtStats)]),
+    "rt_noise_texture": (C.c_int, [C.c_int, C.c_int, C.c_int, _FP, C.c_int, C.c_float, C.c_float, C.c_float,
+                                   C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_double)]),
+    "rt_noise_workspace_bytes": (C.c_size_t, [C.c_int, C.c_int]),
+    "rt_noise_texture_async": (C.c_int, [C.c_int, C.c_int, C.c_int, _FP, C.c_int, C.c_float, C.c_float, C.c_float,
+                                         C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "rt_texture_remap": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                   C.POINTER(C.c_double)]),
+    "rt_remap_workspace_bytes": (C.c_size_t, [C.c_int, C.c_int]),
+    "rt_texture_remap_async": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                         C.c_void_p, C.c_size_t, C.c_void_p]),
     "rt_lbvh_build": (C.c_int, [_FP, C.c_uint32, _FP]),
     "rt_lbvh_workspace_bytes": (C.c_size_t, [C.c_uint32]),
     "rt_lbvh_build_async": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "rt_lbvh_build_gpu": (C.c_int, [_FP, C.c_uint32, _FP, C.c_int, C.POINTER(C.c_double)]),
     "rt_dev_scene_iow03": (C.c_void_p, [_FP, _FP, C.c_uint32, C.c_int, C.c_int]),
     "rt_dev_scene_inw": (C.c_void_p, [_FP, C.c_uint32, C.c_int, _FP, _FP, C.c_uint32, C.c_int, C.c_int]),
+    "rt_dev_scene_inw_tex": (C.c_void_p, [_FP, C.c_uint32, C.c_int, _FP, _FP, C.c_uint32, C.POINTER(RtTexture),
+                                          C.c_int, C.c_int, C.c_int]),
     "rt_dev_scene_free": (None, [C.c_void_p]),
     "rt_render_tiles_async": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.POINTER(RtParams), C.c_void_p,
                                         C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -95,6 +113,11 @@ SIGNATURES = {
     "rt_pack_iow03": (C.c_int, [C.POINTER(RtGeomDesc), C.c_uint32, _FP, _FP]),
     "rt_pack_inw": (C.c_int, [C.POINTER(RtGeomDesc), C.c_uint32, C.c_int, _FP, _FP, _FP, _U32P]),
     "rt_sample_tables": (C.c_int, [C.c_int, _FP, _FP, _IP]),
+    "rt_tile_spiral": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _IP, C.c_int]),
+    "rt_render_spiral_async": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.POINTER(RtParams), C.c_int, C.c_int,
+                                         C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_display_rgba8_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                         C.c_void_p]),
     "rt_debug_counters": (C.c_int, [C.c_void_p]),
     "rt_debug_pixel_rays": (C.c_int, [C.c_void_p]),
     "rt_debug_rounds": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
@@ -157,6 +180,7 @@ class Scene:
     nodes: np.ndarray | None = None    # INW (2N-1,8)
     lights: np.ndarray | None = None   # INW-04 (L,7)
     n_lights: int = 0
+    textures: list | None = None       # INW-04 u_MaterialTextures: (H, W, 3|4) uint8 images
 
     @property
     def layout(self) -> int:
@@ -218,6 +242,52 @@ def make_scene(preset: int, seed: int = 0, n_hint: int = 0, **param_overrides) -
     return sc
 
 
+def texture_array(textures):
+    """rt_texture[] for a list of (H, W, 3|4) uint8 images (row 0 first); returns (array, keep-alive)."""
+    keep = [np.ascontiguousarray(t, np.uint8) for t in textures]
+    arr = (RtTexture * max(1, len(keep)))()
+    for i, t in enumerate(keep):
+        assert t.ndim == 3 and t.shape[2] in (3, 4), t.shape
+        arr[i] = RtTexture(t.ctypes.data, t.shape[1], t.shape[0], t.shape[2])
+    return arr, keep
+
+
+NOISE_SIMPLEX, NOISE_FBM, NOISE_TURBULENCE = 0, 1, 2
+MAP_MERCATOR, MAP_CUBIC = 0, 1
+
+
+def noise_texture(width=600, height=100, kind=NOISE_SIMPLEX, gradient=((0, 0, 0), (1, 1, 1)), freq=0.01,
+                  lac=2.0, gain=0.5, octaves=5, device: int = -1):
+    """GPU Helper::Noise::MakeTexture<glm::vec3> (rt_noise_texture): (height, width, 3) uint8, ms."""
+    g = np.ascontiguousarray(np.asarray(gradient, np.float32).reshape(-1, 3))
+    out = np.zeros((height, width, 3), np.uint8)
+    ms = C.c_double(0.0)
+    check(load().rt_noise_texture(width, height, kind, fptr(g) if len(g) else None, len(g), freq, lac, gain,
+                                  octaves, out.ctypes.data, device, C.byref(ms)), "rt_noise_texture")
+    return out, ms.value
+
+
+def texture_remap(img, load_as, map_to, device: int = -1):
+    """GPU re-projection of LoadFromDiskToGPU(loc, loadAs, mapTo) (rt_texture_remap): image, ms."""
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros_like(img)
+    ms = C.c_double(0.0)
+    check(load().rt_texture_remap(img.ctypes.data, img.shape[1], img.shape[0], img.shape[2], load_as, map_to,
+                                  out.ctypes.data, device, C.byref(ms)), "rt_texture_remap")
+    return out, ms.value
+
+
+def tile_spiral(width: int, height: int, tile_w: int = 100, tile_h: int = 100) -> np.ndarray:
+    """Progressive tile order of Adding_Materials::OnUpdate (rt_tile_spiral): (n, 4) int32 rows
+    (tx, ty, dispatch_w, dispatch_h)."""
+    lib = load()
+    n = lib.rt_tile_spiral(width, height, tile_w, tile_h, None, 0)
+    check(min(n, 0), "rt_tile_spiral")
+    out = np.zeros((max(n, 1), 4), np.int32)
+    lib.rt_tile_spiral(width, height, tile_w, tile_h, out.ctypes.data_as(_IP), n)
+    return out[:n]
+
+
 def lbvh_build_gpu(aabbs, device: int = -1):
     """GPU LBVH (rt_lbvh_build_gpu): same (2N-1) x 8 node buffer as lbvh_build; returns (nodes, ms)."""
     aabbs = np.ascontiguousarray(aabbs, np.float32)
@@ -261,8 +331,15 @@ def render(sc: Scene, params: RtParams | None = None, sphere=None):
     else:
         depth = np.zeros((p.height, p.width), np.float32)
         lights = sc.lights if sc.lights is not None and len(sc.lights) else None
-        rc = lib.rt_render_inw(fptr(sc.geom), sc.n, sc.layout, fptr(sc.nodes), fptr(lights), sc.n_lights,
-                               C.byref(sc.camera), C.byref(p), fptr(rgba), fptr(depth), C.byref(st))
+        tex = getattr(sc, "textures", None) or []
+        if tex:
+            arr, keep = texture_array(tex)
+            rc = lib.rt_render_inw_tex(fptr(sc.geom), sc.n, sc.layout, fptr(sc.nodes), fptr(lights), sc.n_lights,
+                                       arr, len(tex), C.byref(sc.camera), C.byref(p), fptr(rgba), fptr(depth),
+                                       C.byref(st))
+        else:
+            rc = lib.rt_render_inw(fptr(sc.geom), sc.n, sc.layout, fptr(sc.nodes), fptr(lights), sc.n_lights,
+                                   C.byref(sc.camera), C.byref(p), fptr(rgba), fptr(depth), C.byref(st))
     check(rc, "render")
     return rgba, depth, st.as_dict()
 

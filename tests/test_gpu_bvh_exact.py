@@ -4,7 +4,10 @@
 - RT_IOW_NARROW=1: the byte-bounce stack layout (12-deep BVH stack) instead of the 9-float one;
 - RT_ROUNDS=0:     no tail compaction (no parking / resume launches);
 - RT_IOW_SPEC=0:   the sequential per-pixel kernel instead of sample-parallel speculation;
-- RT_SPEC_ITERS=0/1: fewer resolve passes, more pixels finished by the sequential kernel;
+- RT_SPEC_ITERS=0/3/10: other numbers of resolve passes (default 1), more pixels finished by the sequential kernel (which
+  takes the still-exact records; RT_SPEC_VALIDATE=0 re-runs every sample from the first bad one);
+- RT_SPEC_PRIOR_FROM: from which sample on the scene's RI prior is guessed for entries sample 0
+  left unwritten (default 2; 10^6 = never, with the former 10 re-run passes);
 - RT_SPEC_GROUPS=2/7: pixel groups on separate streams;
 - RT_IOW_ASYNC=1: asynchronous windows (per-wave frontiers) instead of global resolve passes;
 - RT_SPEC_FIX=1: mid-pass correction of parked samples (patch / restart with the exact state);
@@ -45,7 +48,8 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     out = str(tmp_path / f"img_{len(os.listdir(tmp_path))}.npy")
     env = dict(os.environ)
     for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS", "RT_IOW_SPEC", "RT_SPEC_ITERS",
-              "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_SPEC_GROUPS", "RT_IOW_ASYNC", "RT_SPEC_FIX"):
+              "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_SPEC_GROUPS", "RT_IOW_ASYNC", "RT_SPEC_FIX",
+              "RT_SPEC_VALIDATE", "RT_SPEC_PRIOR_FROM"):
         env.pop(k, None)
     env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out, preset=scene[0], seed=scene[1], n_hint=scene[2])
@@ -63,6 +67,9 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     ({"RT_IOW_SPEC": "0"}, 600, 400, 8),
     ({"RT_SPEC_ITERS": "0"}, 300, 200, 16),
     ({"RT_SPEC_ITERS": "1"}, 300, 200, 16),
+    ({"RT_SPEC_ITERS": "0", "RT_SPEC_VALIDATE": "0"}, 300, 200, 16),
+    ({"RT_SPEC_ITERS": "10", "RT_SPEC_PRIOR_FROM": "1000000"}, 300, 200, 16),
+    ({"RT_SPEC_ITERS": "3", "RT_SPEC_PRIOR_FROM": "1"}, 600, 400, 12),
     ({"RT_IOW_ASYNC": "1"}, 600, 400, 8),
     ({"RT_SPEC_FIX": "1"}, 600, 400, 12),
     ({"RT_SPEC_GROUPS": "2"}, 300, 200, 12),

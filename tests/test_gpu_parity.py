@@ -111,6 +111,6 @@ def test_tile_list_matches_full_image(gpu):
 
 def test_unsupported_texture_index_fails_loudly(gpu):
     sc = R.make_scene(R.PRESET_INW04_REFSET, spp=1)
-    sc.geom[2, 27] = 1.0  # TextureIndex > 0: the texture path is out of scope this round
+    sc.geom[2, 27] = 1.0  # TextureIndex > 0 with no texture bound (rt_render_inw_tex binds them)
     with pytest.raises(RuntimeError):
         R.render(sc)
