@@ -90,6 +90,10 @@ rtk::Frame make_frame(const rt_camera *cam, const rt_params *p) {
     f.px_rays = g_px_rays;
     const char *lb = std::getenv("RT_LEAF_BATCH");  // tuning switch (65 = only when no lane can advance)
     f.leaf_batch = (lb && *lb) ? std::max(1, std::atoi(lb)) : 65;
+    // IOW-03: wave-cooperative closest hits for waves with at most this many tracing lanes
+    // (0 = off; every mode is bit-identical, tests/test_gpu_bvh_exact.py)
+    const char *co = std::getenv("RT_COOP");
+    f.coop_max = (co && *co) ? std::max(0, std::atoi(co)) : 4;
     return f;
 }
 
@@ -108,6 +112,7 @@ struct rt_dev_scene {
     int root_link = 0;   // IOW-03 culling BVH: leftData of the root
     float ri_prior = 1.0f;  // IOW-03: most common refractive index (sample-parallel guess)
     DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
+    DevBuf obox;  // IOW-03: per-object culling boxes (2 float4 each) for wave-cooperative queries
     DevBuf tex, tex_info;  // INW-04 material textures (float4 texels, (first, w, h, 0) per texture)
     uint32_t n_tex = 0;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
@@ -235,6 +240,15 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
         if (n < 16384) {
             HIP_OK(s->nodes.upload(wide.data(), wide.size() * sizeof(float)));
             s->root_link = 1;
+            // n float4 (lo.xyz, hi.x), then n float2 (hi.yz)
+            std::vector<float> ob(size_t(n) * 6);
+            for (uint32_t j = 0; j < n; j++) {
+                const float *b = boxes.data() + size_t(j) * 6;
+                for (int k = 0; k < 4; k++) ob[size_t(j) * 4 + k] = b[k];
+                ob[size_t(n) * 4 + size_t(j) * 2] = b[4];
+                ob[size_t(n) * 4 + size_t(j) * 2 + 1] = b[5];
+            }
+            HIP_OK(s->obox.upload(ob.data(), ob.size() * sizeof(float)));
         }
     }
     set_residency(s);
@@ -469,7 +483,8 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             }
             if (s->kind == 3) {
                 rtk::IowScene sc{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
-                                 s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link};
+                                 s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link,
+                                 s->obox.as<float4>()};
                 e = rtk::launch_iow03(f, sc, ch, ct, n_units, s->counter.as<unsigned>(), s->s_stop, cap, st);
             } else {
                 rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
@@ -509,7 +524,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                           s->sp_assume.as<float4>(), P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(),
                           sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), ++s->epoch};
     rtk::IowScene scene{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
-                        s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link};
+                        s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link,
+                                 s->obox.as<float4>()};
     const int cap_s = s->cus * rtk::resident_blocks_per_cu(5);
     const int cap_q = s->cus * rtk::resident_blocks_per_cu(3);
     hipError_t e = hipSuccess;

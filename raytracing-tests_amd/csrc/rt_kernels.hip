@@ -172,11 +172,89 @@ __device__ __forceinline__ void cswap(float &ta, int &ka, float &tb, int &kb) {
     ta = t; ka = k;
 }
 
+// Local ray of an object (the `M*(o-p)`, `normalize(M*d)` of t_RayXObj, 03...glsl:55-73).
+// Objects whose matrix is glm::mat3(1) transform the direction identically, so M*gd and
+// normalize(M*gd) are evaluated once per ray and passed in (same operations, same bits: 1*x
+// folds to x, the 0*y terms are kept because IEEE forbids folding them).
+__device__ __forceinline__ void iow_local(const float *h, const IowObj &ob, f3 go, f3 gd, f3 td_id, f3 nd_id, f3 &to,
+                                          f3 &td, f3 &nd) {
+    const m3 I = m3{f3{1.0f, 0.0f, 0.0f}, f3{0.0f, 1.0f, 0.0f}, f3{0.0f, 0.0f, 1.0f}};
+    if (h[19] != 0.0f) { to = mul(I, go - ob.pos); td = td_id; nd = nd_id; }
+    else { to = mul(ob.M, go - ob.pos); td = mul(ob.M, gd); nd = normalize(td); }
+}
+__device__ __forceinline__ void iow_id_dirs(f3 gd, f3 &td_id, f3 &nd_id) {
+    const m3 I = m3{f3{1.0f, 0.0f, 0.0f}, f3{0.0f, 1.0f, 0.0f}, f3{0.0f, 0.0f, 1.0f}};
+    td_id = mul(I, gd);
+    nd_id = normalize(td_id);
+}
+// exact test of object j; keeps the reference's rule: nearer t, or the lower index on a tie
+__device__ __forceinline__ void iow_test(const IowScene &S, int j, f3 go, f3 gd, f3 td_id, f3 nd_id, float &min_t,
+                                         int &best) {
+    const float *h = S.hot + (size_t)j * kIowHot;
+    const IowObj ob = iow_obj(h);
+    f3 to, td, nd;
+    iow_local(h, ob, go, gd, td_id, nd_id, to, td, nd);
+    float t = -1.0f;
+    if (ob.type == 2) t = t_ellipsoid(to, nd, ob.is);
+    else if (ob.type == 1) t = t_cuboid(to, nd, ob.scale);
+    if (t > 0.0f && (t < min_t || (t == min_t && j < best))) { min_t = t; best = j; }
+}
+
+// Hit attributes of the winner `best` at min_t (LaunchRay's tail, 03...glsl:221-255): the
+// closest hit's normal and attributes are evaluated once after the search.
+// cold = the winner's cold record (colour3, material3, scatter2) when min_t < max_t
+__device__ __forceinline__ RayRet iow_eval_c(const IowScene &S, f3 go, f3 gd, float min_t, int best, float max_t,
+                                             float contrib, float4 c0, float4 c1) {
+    RayRet r;
+    if (min_t < max_t) {
+        const float *hb = S.hot + (size_t)best * kIowHot;
+        const IowObj ob = iow_obj(hb);
+        f3 td_id, nd_id, best_to, best_td, best_nd;
+        iow_id_dirs(gd, td_id, nd_id);
+        iow_local(hb, ob, go, gd, td_id, nd_id, best_to, best_td, best_nd);
+        f3 h = best_to + best_nd * min_t;
+        f3 n = ob.type == 2 ? f3{h.x * ob.is.x * ob.scale.x, h.y * ob.is.y * ob.scale.y, h.z * ob.is.z * ob.scale.z}
+                            : (ob.type == 1 ? cuboid_normal(h, ob.scale) : f3{0, 0, 0});
+        r.color = mk(c0.x, c0.y, c0.z);
+        r.material = mk(c0.w, c1.x, c1.y);
+        r.scat0 = c1.z; r.scat1 = c1.w;
+        const bool inside = dot(n, best_td) > 0.0f;
+        f3 n_ = sel(inside, -n, n);
+        f3 refl = reflect(best_td, n_);
+        if (!inside) {
+            f3 nir = normalize(cross(n_, best_td));
+            f3 nn = normalize(cross(nir, n_));
+            float s = r.scat1;
+            float k = 1.0f / __builtin_sqrtf(1.0f + s * s);
+            f3 mr = n_ * (s * k) + nn * k;
+            refl = sel(dot(refl, n_) > dot(mr, n_), refl, mr);
+        }
+        m3 inv = inverse(ob.M);
+        r.point = go + gd * min_t;
+        r.normal = normalize(mul(inv, n));
+        r.reflected = normalize(mul(inv, refl));
+        r.color = r.color * contrib;
+    } else {
+        r.point = f3{0, 0, 0}; r.normal = f3{0, 0, 0};
+        r.reflected = r.color = r.material = f3{0, 0, 0};
+        r.scat0 = r.scat1 = 0.0f;
+    }
+    return r;
+}
+__device__ __forceinline__ RayRet iow_eval(const IowScene &S, f3 go, f3 gd, float min_t, int best, float max_t,
+                                           float contrib) {
+    float4 c0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), c1 = c0;
+    if (min_t < max_t) {
+        const float4 *cold = reinterpret_cast<const float4 *>(S.cold + (size_t)best * kIowCold);
+        c0 = cold[0]; c1 = cold[1];
+    }
+    return iow_eval_c(S, go, gd, min_t, best, max_t, contrib, c0, c1);
+}
+
 // LaunchRay 03...glsl:196-256.  The reference loops over every object and keeps the first
 // strictly nearer hit, i.e. the minimum t with the lowest index among exact ties.  The BVH
 // walk visits a superset of the objects that can attain that minimum and applies the same
-// (t, index) rule, so it returns the same object and the same t bits.  The closest hit's
-// normal and attributes are evaluated once after the search from the winning object.
+// (t, index) rule, so it returns the same object and the same t bits.
 template <int BCAP>
 __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 gd, float max_t, float contrib,
                                  Ctr &c, short *bstk) {
@@ -184,27 +262,11 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
     float min_t = max_t;
     int best = -1;
     c.seg++;
-    // Objects whose matrix is glm::mat3(1) transform the direction identically, so M*gd and
-    // normalize(M*gd) are evaluated once per ray (same operations, same bits: 1*x folds to x,
-    // the 0*y terms are kept because IEEE forbids folding them).
-    const m3 I = m3{f3{1.0f, 0.0f, 0.0f}, f3{0.0f, 1.0f, 0.0f}, f3{0.0f, 0.0f, 1.0f}};
-    const f3 td_id = mul(I, gd);
-    const f3 nd_id = normalize(td_id);
-    // local ray of object j (a pure function of j and the ray: recomputed for the winner)
-    auto local = [&](const float *h, const IowObj &ob, f3 &to, f3 &td, f3 &nd) {
-        if (h[19] != 0.0f) { to = mul(I, go - ob.pos); td = td_id; nd = nd_id; }
-        else { to = mul(ob.M, go - ob.pos); td = mul(ob.M, gd); nd = normalize(td); }
-    };
+    f3 td_id, nd_id;
+    iow_id_dirs(gd, td_id, nd_id);
     auto test = [&](int j) {
         c.prims++;
-        const float *h = S.hot + (size_t)j * kIowHot;
-        const IowObj ob = iow_obj(h);
-        f3 to, td, nd;
-        local(h, ob, to, td, nd);
-        float t = -1.0f;
-        if (ob.type == 2) t = t_ellipsoid(to, nd, ob.is);
-        else if (ob.type == 1) t = t_cuboid(to, nd, ob.scale);
-        if (t > 0.0f && (t < min_t || (t == min_t && j < best))) { min_t = t; best = j; }
+        iow_test(S, j, go, gd, td_id, nd_id, min_t, best);
     };
     const float dl2 = dot(gd, gd);
     if (!(dl2 > 0.0f)) {
@@ -277,47 +339,124 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
     } else {
         for (uint32_t j = 0; j < S.n; j++) test((int)j);  // also the path for zero / NaN directions
     }
-    RayRet r;
-    if (min_t < max_t) {
-        const float *hb = S.hot + (size_t)best * kIowHot;
-        const IowObj ob = iow_obj(hb);
-        f3 best_to, best_td, best_nd;
-        local(hb, ob, best_to, best_td, best_nd);
-        const float *cold = S.cold + (size_t)best * kIowCold;
-        f3 h = best_to + best_nd * min_t;
-        f3 n = ob.type == 2 ? f3{h.x * ob.is.x * ob.scale.x, h.y * ob.is.y * ob.scale.y, h.z * ob.is.z * ob.scale.z}
-                            : (ob.type == 1 ? cuboid_normal(h, ob.scale) : f3{0, 0, 0});
-        r.color = mk(cold[0], cold[1], cold[2]);
-        r.material = mk(cold[3], cold[4], cold[5]);
-        r.scat0 = cold[6]; r.scat1 = cold[7];
-        const bool inside = dot(n, best_td) > 0.0f;
-        f3 n_ = sel(inside, -n, n);
-        f3 refl = reflect(best_td, n_);
-        if (!inside) {
-            f3 nir = normalize(cross(n_, best_td));
-            f3 nn = normalize(cross(nir, n_));
-            float s = r.scat1;
-            float k = 1.0f / __builtin_sqrtf(1.0f + s * s);
-            f3 mr = n_ * (s * k) + nn * k;
-            refl = sel(dot(refl, n_) > dot(mr, n_), refl, mr);
-        }
-        m3 inv = inverse(ob.M);
-        r.point = go + gd * min_t;
-        r.normal = normalize(mul(inv, n));
-        r.reflected = normalize(mul(inv, refl));
-        r.color = r.color * contrib;
-    } else {
-        r.point = f3{0, 0, 0}; r.normal = f3{0, 0, 0};
-        r.reflected = r.color = r.material = f3{0, 0, 0};
-        r.scat0 = r.scat1 = 0.0f;
-    }
+    RayRet r = iow_eval(S, go, gd, min_t, best, max_t, contrib);
     DBG_CYC(F_, c, kDbgCycRay, t_ray);
     return r;
 }
 
-__device__ __forceinline__ f3 fib_dir(const IowScene &S, int idx, float s, f3 focus) {
-    const float *t = S.fib + 4 * idx;
-    float x = t[0] * s, y = t[1] * s, z = t[2] * s;
+// ---------------------------------------------------------------- wave-cooperative closest hit
+// When only a few lanes of a wave still trace (the long samples at the end of a pass), the
+// wave runs their closest-hit queries one ray at a time with all 64 lanes: every lane culls
+// 1/64 of the objects against their conservative boxes (the BVH's leaf boxes), the survivors
+// are compacted into a wave list in LDS and tested exactly in parallel, and a wave reduction
+// applies the reference's (t, lowest index) rule.  The candidate set is a superset of the one
+// the BVH walk tests, so the winner and its t bits are the same (DESIGN.md "k_iow03s").
+// Requires all 64 lanes active.
+__device__ __forceinline__ float wave_min_all(float v) {
+    v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false)));   // quad [1,0,3,2]
+    v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false)));   // quad [2,3,0,1]
+    v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xf, 0xf, false)));  // row half-mirror
+    v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xf, 0xf, false)));  // row mirror
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return fminf(fminf(r0, r1), fminf(r2, r3));
+}
+__device__ __forceinline__ float bcast_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Closest hit of one (wave-uniform) ray with the whole wave.  wl: the wave's LDS list, entry k
+// at wl[(k >> 6) * kBlock + (k & 63)], cap entries (a multiple of 64 * kCoopR).  Returns the
+// (uniform) winner and its cold record; nbox / nprim are the boxes and objects tested.  The
+// loads of a batch of kCoopR boxes per lane, and a candidate's hot and cold records, are
+// issued together: a lone ray's query costs about two memory latencies, not one per step.
+constexpr int kCoopR = 8;
+__device__ void iow_coop_search(const IowScene &S, f3 go, f3 gd, float max_t, short *wl, int cap, float &t_out,
+                                int &j_out, float4 &c0_out, float4 &c1_out, uint32_t &nbox, uint32_t &nprim) {
+    const int lane = (int)(threadIdx.x & 63);
+    float bt = max_t;
+    int bj = -1;
+    float4 b0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b1 = b0;  // cold record of this lane's best
+    nbox = 0; nprim = 0;
+    t_out = max_t; j_out = -1; c0_out = b0; c1_out = b0;
+    const float dl2 = dot(gd, gd);
+    if (!(dl2 > 0.0f)) {  // zero / NaN direction: no object can hit (see iow_launch_ray)
+        nprim = S.n;
+        return;
+    }
+    f3 td_id, nd_id;
+    iow_id_dirs(gd, td_id, nd_id);
+    const bool cull = S.obox != nullptr && dl2 > 0.998f && dl2 < 1.002f;
+    const f3 id = f3{__builtin_amdgcn_rcpf(gd.x), __builtin_amdgcn_rcpf(gd.y), __builtin_amdgcn_rcpf(gd.z)};
+    const float lim = max_t * 1.0001f + 1e-3f;
+    const uint32_t n = S.n;
+    uint32_t j0 = 0;
+    while (j0 < n) {
+        uint32_t cnt = 0, jb = j0;
+        if (cull) {
+            for (; j0 < n && cnt + 64 * kCoopR <= (uint32_t)cap; j0 += 64 * kCoopR) {
+                const float2 *ob2 = reinterpret_cast<const float2 *>(S.obox + n);
+                float4 a[kCoopR];
+                float2 b[kCoopR];
+#pragma unroll
+                for (int r = 0; r < kCoopR; r++) {
+                    const uint32_t j = j0 + 64 * r + lane, jj = j < n ? j : n - 1;
+                    a[r] = S.obox[jj];
+                    b[r] = ob2[jj];
+                }
+#pragma unroll
+                for (int r = 0; r < kCoopR; r++) {
+                    const uint32_t j = j0 + 64 * r + lane;
+                    const bool cand =
+                        j < n && cull_t(a[r].x, a[r].y, a[r].z, a[r].w, b[r].x, b[r].y, go, id, lim) != kMiss;
+                    const unsigned long long cm = __ballot(cand);
+                    if (cand) {
+                        const uint32_t k = cnt + lanes_below(cm);
+                        wl[(k >> 6) * kBlock + (k & 63)] = (short)j;
+                    }
+                    cnt += (uint32_t)__popcll(cm);
+                }
+            }
+            nbox += (j0 < n ? j0 : n) - jb;
+        } else {
+            cnt = n - j0 < (uint32_t)cap ? n - j0 : (uint32_t)cap;
+            j0 += cnt;
+        }
+        for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            if (k < cnt) {
+                const int j = cull ? (int)wl[(k >> 6) * kBlock + (k & 63)] : (int)(jb + k);
+                const float4 *cold = reinterpret_cast<const float4 *>(S.cold + (size_t)j * kIowCold);
+                const float4 q0 = cold[0], q1 = cold[1];
+                const int was = bj;
+                iow_test(S, j, go, gd, td_id, nd_id, bt, bj);
+                if (bj != was) { b0 = q0; b1 = q1; }
+            }
+        }
+        nprim += cnt;
+    }
+    const float tm = wave_min_all(bj >= 0 ? bt : max_t);
+    unsigned long long m = __ballot(bj >= 0 && bt == tm);
+    if (m == 0) return;
+    int jm = -1, lm = 0;
+    for (; m; m &= m - 1) {  // usually one lane; exact ties keep the lowest object index
+        const int l = __ffsll((long long)m) - 1;
+        const int j = __builtin_amdgcn_readlane(bj, l);
+        if (jm < 0 || j < jm) { jm = j; lm = l; }
+    }
+    t_out = tm;
+    j_out = jm;
+    c0_out = make_float4(bcast_f(b0.x, lm), bcast_f(b0.y, lm), bcast_f(b0.z, lm), bcast_f(b0.w, lm));
+    c1_out = make_float4(bcast_f(b1.x, lm), bcast_f(b1.y, lm), bcast_f(b1.z, lm), bcast_f(b1.w, lm));
+}
+
+__device__ __forceinline__ f3 fib_dir(float4 t, float s, f3 focus) {
+    float x = t.x * s, y = t.y * s, z = t.z * s;
     f3 yc = focus;
     f3 zc = normalize(cross(f3{0, 1.0f, 0}, yc));
     f3 xc = normalize(cross(yc, zc));
@@ -367,16 +506,26 @@ struct IowStack {
     }
 };
 
+// One ray segment of LaunchRays (03...glsl:285-358): pop, closest hit, shade and push.
+struct SegIn { f3 co, cd; float contribution, ri; int bounced; float4 fib; };
 template <bool NARROW>
-__device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, IowStack<NARROW> &K, int &skip,
-                                            f3 &sample, int sidx, Ctr &c, short *bstk) {
-    constexpr int BCAP = (NARROW ? 12 : kIowBvhStack) - 3;  // logical depth; 3 spare push slots
+__device__ __forceinline__ SegIn iow_seg_pop(const IowScene &S, IowStack<NARROW> &K, int sidx) {
     K.size--;
     const int e = K.size;
-    f3 co = mk(K.at(e, 0), K.at(e, 1), K.at(e, 2)), cd = mk(K.at(e, 3), K.at(e, 4), K.at(e, 5));
-    float contribution = K.at(e, 6), ri = K.at(e, 7);
-    int bounced = K.bounced(e);
-    RayRet data = iow_launch_ray<BCAP>(S, F, co, cd, 32000.0f, contribution, c, bstk);
+    SegIn in;
+    in.fib = reinterpret_cast<const float4 *>(S.fib)[sidx];  // fibonacciHemiSpherePtDirn's point (03...glsl:164-184)
+    in.co = mk(K.at(e, 0), K.at(e, 1), K.at(e, 2));
+    in.cd = mk(K.at(e, 3), K.at(e, 4), K.at(e, 5));
+    in.contribution = K.at(e, 6); in.ri = K.at(e, 7);
+    in.bounced = K.bounced(e);
+    return in;
+}
+template <bool NARROW>
+__device__ __forceinline__ void iow_seg_shade(const IowScene &S, const Frame &F, IowStack<NARROW> &K, int &skip,
+                                              f3 &sample, int sidx, Ctr &c, const SegIn &in, const RayRet &data) {
+    const f3 cd = in.cd;
+    const float contribution = in.contribution, ri = in.ri;
+    int bounced = in.bounced;
     const bool hit = dot(data.normal, data.normal) > 0.9f;
     sample = sample + sel(hit, data.color, background(cd, false)) * contribution;
     if (bounced < F.max_bounces && hit) {
@@ -396,7 +545,7 @@ __device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, I
         float refr_c = data.material.x, refl_c = data.material.y;
         f3 n_ = sel(cos_t > 0.0f, data.normal, -data.normal);
         if (cos_t < 0.0f) {
-            refl_dir = fib_dir(S, sidx, data.scat1, data.reflected); spawnRefl = true;
+            refl_dir = fib_dir(in.fib, data.scat1, data.reflected); spawnRefl = true;
             float inc = refr_c * schlick(-cos_t, ri * rcp(target_ri));
             refr_c -= inc; refl_c += inc;
         } else if (rr > 1.0f) {
@@ -406,7 +555,7 @@ __device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, I
             f3 yc = n_ * cos_t, xc = cd - yc;
             spawnRefr = true;
             refr_dir = n_ * rr + xc * __builtin_sqrtf(1.0f - rr * rr);
-            refr_dir = fib_dir(S, sidx, data.scat0, refr_dir);
+            refr_dir = fib_dir(in.fib, data.scat0, refr_dir);
         }
         skip = (spawnRefl && spawnRefr) ? skip - 1 : (spawnRefl ? skip : (spawnRefr ? skip + 1 : 0));
         if (spawnRefl) {
@@ -418,6 +567,58 @@ __device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, I
             K.push(data.point + n_ * 0.000015f, refr_dir, contribution * refr_c, target_ri, bounced, c);
         }
     } else skip = 0;
+}
+template <bool NARROW>
+__device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, IowStack<NARROW> &K, int &skip,
+                                            f3 &sample, int sidx, Ctr &c, short *bstk) {
+    constexpr int BCAP = (NARROW ? 12 : kIowBvhStack) - 3;  // logical depth; 3 spare push slots
+    const SegIn in = iow_seg_pop(S, K, sidx);
+    const RayRet data = iow_launch_ray<BCAP>(S, F, in.co, in.cd, 32000.0f, in.contribution, c, bstk);
+    iow_seg_shade(S, F, K, skip, sample, sidx, c, in, data);
+}
+// The segment step of a work loop, called with every lane of the wave (seg: this lane has a
+// ray to trace).  With at most F.coop_max tracing lanes the wave runs their closest-hit
+// queries cooperatively (iow_coop_search), one ray after another; otherwise each lane walks
+// the BVH for its own ray.
+template <bool NARROW>
+__device__ __forceinline__ void iow_seg_step(const IowScene &S, const Frame &F, IowStack<NARROW> &K, int &skip,
+                                             f3 &sample, int sidx, Ctr &c, short *bstk, bool seg) {
+    const unsigned long long m = __ballot(seg);
+    if (m == 0) return;
+    if (__popcll(m) > F.coop_max) {
+        if (seg) iow_segment(S, F, K, skip, sample, sidx, c, bstk);
+        return;
+    }
+    constexpr int kCap = (NARROW ? 12 : kIowBvhStack) * 64;  // the wave's BVH-stack slots, as a list
+    short *wl = bstk - (threadIdx.x & 63);
+    DBG_T0(F, t_pop);
+    SegIn in{};
+    if (seg) in = iow_seg_pop(S, K, sidx);
+    DBG_CYC(F, c, kDbgCycSpare2, t_pop);
+    DBG_T0(F, t_q);
+    float my_t = 32000.0f;
+    int my_j = -1;
+    float4 my_c0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), my_c1 = my_c0;
+    uint32_t my_box = 0, my_prim = 0;
+    for (unsigned long long mm = m; mm; mm &= mm - 1) {
+        const int L = __ffsll((long long)mm) - 1;
+        const f3 go = f3{bcast_f(in.co.x, L), bcast_f(in.co.y, L), bcast_f(in.co.z, L)};
+        const f3 gd = f3{bcast_f(in.cd.x, L), bcast_f(in.cd.y, L), bcast_f(in.cd.z, L)};
+        float t;
+        int j;
+        float4 c0, c1;
+        uint32_t nb, np;
+        iow_coop_search(S, go, gd, 32000.0f, wl, kCap, t, j, c0, c1, nb, np);
+        if ((int)(threadIdx.x & 63) == L) { my_t = t; my_j = j; my_c0 = c0; my_c1 = c1; my_box = nb; my_prim = np; }
+    }
+    DBG_CYC(F, c, kDbgCycSpare0, t_q);
+    DBG_T0(F, t_sh);
+    if (seg) {
+        c.seg++; c.nodes += my_box; c.prims += my_prim;
+        const RayRet data = iow_eval_c(S, in.co, in.cd, my_t, my_j, 32000.0f, in.contribution, my_c0, my_c1);
+        iow_seg_shade(S, F, K, skip, sample, sidx, c, in, data);
+    }
+    DBG_CYC(F, c, kDbgCycSpare1, t_sh);
 }
 
 // ---------------------------------------------------------------- persistent work queue
@@ -534,6 +735,7 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
     f3 fc = f3{0, 0, 0}, sample = f3{0, 0, 0};
     int s = 0, skip = 0;
     for (;;) {
+        DBG_T0(f, t_loop);
         const uint32_t q = fetch_unit(counter, live && !busy);
         if (live && !busy) {
             if (q >= total) live = false;
@@ -593,7 +795,6 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
             break;
         }
         DBG_TALLY(f, c, kDbgOuter, busy);
-        DBG_T0(f, t_loop);
         if (ch.rec_col) {
             // take every following sample whose speculative record assumed the exact stack
             // state (the RI of the entries it read before writing them) from its record
@@ -633,10 +834,13 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
         DBG_TALLY(f, c, kDbgSeg, busy && K.size > 0);
         DBG_CYC(f, c, kDbgCycCam, t_loop);
         DBG_T0(f, t_seg);
-        if (busy && K.size > 0) {
-            iow_segment(S, f, K, skip, sample, s, c, bstk);
-            urays++;
-            if (K.size == 0) { fc = fc + sample; s++; }
+        {
+            const bool seg = busy && K.size > 0;
+            iow_seg_step(S, f, K, skip, sample, s, c, bstk, seg);
+            if (seg) {
+                urays++;
+                if (K.size == 0) { fc = fc + sample; s++; }
+            }
         }
         DBG_CYC(f, c, kDbgCycSeg, t_seg);
         if (busy && K.size == 0 && s >= s_end) {
@@ -777,9 +981,10 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         DBG_TALLY(f, c, kDbgOuter, busy);
         DBG_TALLY(f, c, kDbgSeg, busy && K.size > 0);
         DBG_T0(f, t_seg);
-        if (busy && K.size > 0) {
-            iow_segment(S, f, K, skip, sample, (int)(u / R.P), c, bstk);
-            urays++;
+        {
+            const bool seg = busy && K.size > 0;
+            iow_seg_step(S, f, K, skip, sample, (int)(u / R.P), c, bstk, seg);
+            if (seg) urays++;
         }
         DBG_CYC(f, c, kDbgCycSeg, t_seg);
         if (busy && K.size == 0) {  // sample done: record it

@@ -22,6 +22,7 @@ struct Frame {
     unsigned long long *dbg;  // optional lane-occupancy counters (kDbg* slots), null in production
     int leaf_batch;           // IOW-03 walk: test postponed leaves once this many lanes hold one
     unsigned *px_rays;        // optional: rays cast per work unit, written when its pixel completes
+    int coop_max;             // IOW-03: wave-cooperative closest hits when at most this many lanes trace
 };
 // lane-occupancy counters (per wave-iteration: 1 and popcount of the participating lanes)
 enum { kDbgOuter = 0, kDbgOuterLanes, kDbgTrav, kDbgTravLanes, kDbgLeaf, kDbgLeafLanes, kDbgSeg, kDbgSegLanes,
@@ -46,6 +47,7 @@ struct IowScene {
     const float *fib;        // spp*4 (xyz + pad)
     const int *ring;         // spp*2
     int root_link;           // link of the BVH root (wide node 0 -> 1)
+    const float4 *obox;      // the BVH leaves' conservative boxes: n float4 (lo.xyz, hi.x), n float2 (hi.yz); or null
 };
 struct InwScene {
     const float4 *hot;       // n * 7 float4

@@ -21,12 +21,20 @@ u = int(torch.argmax(pr).item()); mx = int(pr.max().item())
 b, l = u >> 6, u & 63; nbx = (tw + 7) >> 3
 px, py = x0 + (b % nbx) * 8 + (l & 7), y0 + (b // nbx) * 8 + (l >> 3)
 out = {"pixel": [px, py], "rays": mx}
-for mode in ("0", "1"):
+for coop, mode in (("0", "0"), ("4", "0"), ("0", "1"), ("4", "1")):
     os.environ["RT_IOW_SPEC"] = mode
+    os.environ["RT_COOP"] = coop
     q = R.RtParams(); C.memmove(C.addressof(q), C.addressof(sc.params), C.sizeof(q))
     q.tile_x0, q.tile_y0, q.tile_w, q.tile_h = px, py, 1, 1
     R.render(sc, q)
+    dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
+    lib.rt_debug_counters(dbg.data_ptr())
     t0 = time.perf_counter(); _, _, st = R.render(sc, q); dt = time.perf_counter() - t0
-    out["spec" + mode] = {"ms": st["ms"], "wall_ms": dt * 1e3, "segments": st["segments"],
-                          "us_per_segment": st["ms"] * 1e3 / max(1, st["segments"])}
+    lib.rt_debug_counters(None)
+    d = dbg.cpu().numpy().tolist()
+    names = ["outer", "outer_lanes", "trav", "trav_lanes", "leaf", "leaf_lanes", "seg", "seg_lanes",
+             "cyc_loop_top", "cyc_ray", "cyc_trav", "cyc_leaf", "cyc_seg", "cyc_coop_query", "cyc_coop_shade", "cyc_pop"]
+    out["spec" + mode + "_coop" + coop] = {"ms": st["ms"], "wall_ms": dt * 1e3, "segments": st["segments"],
+                          "us_per_segment": st["ms"] * 1e3 / max(1, st["segments"]),
+                          "dbg_per_segment": {k: round(v / max(1, st["segments"]), 1) for k, v in zip(names, d)}}
 print(json.dumps(out))
