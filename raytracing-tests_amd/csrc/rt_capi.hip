@@ -110,6 +110,7 @@ struct rt_dev_scene {
     int blocks_cap = 0;  // persistent grid size: resident blocks the device can hold (max over variants)
     int cus = 0;
     int root_link = 0;   // IOW-03 culling BVH: leftData of the root
+    uint32_t n_wide = 0; // IOW-03 culling BVH: 4-wide nodes
     float ri_prior = 1.0f;  // IOW-03: most common refractive index (sample-parallel guess)
     DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
     DevBuf obox;  // IOW-03: per-object culling boxes (2 float4 each) for wave-cooperative queries
@@ -240,6 +241,7 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
         if (n < 16384) {
             HIP_OK(s->nodes.upload(wide.data(), wide.size() * sizeof(float)));
             s->root_link = 1;
+            s->n_wide = uint32_t(wide.size() / 32);
             // n float4 (lo.xyz, hi.x), then n float2 (hi.yz)
             std::vector<float> ob(size_t(n) * 6);
             for (uint32_t j = 0; j < n; j++) {
@@ -450,7 +452,16 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // compaction can no longer shorten the critical path; the last round never parks.
     const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 6)));  // <= 14: one count slot per round
     // grid of this frame's kernel variant
-    const int cap = s->kind == 3 ? s->cus * rtk::resident_blocks_per_cu(rtk::iow_narrow(f) ? 4 : 3) : s->blocks_cap;
+    int cap = s->kind == 3 ? s->cus * rtk::resident_blocks_per_cu(rtk::iow_narrow(f) ? 4 : 3) : s->blocks_cap;
+    if (s->kind == 3 && !rtk::iow_narrow(f)) {
+        rtk::IowScene probe{};
+        probe.nodes = s->nodes.as<float4>();
+        probe.n_nodes = s->n_wide;
+        if (rtk::iow_lds(probe)) {
+            cap = s->cus * 3 * rtk::resident_blocks_per_cu(9);  // 256-lane slots of the 768-lane blocks
+            s->last_kernel = "k_iow03L";
+        }
+    }
     const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
     if (rounds > 0) {
         int rc = ensure_cont(s);
@@ -484,7 +495,7 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             if (s->kind == 3) {
                 rtk::IowScene sc{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
                                  s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link,
-                                 s->obox.as<float4>()};
+                                 s->obox.as<float4>(), s->n_wide};
                 e = rtk::launch_iow03(f, sc, ch, ct, n_units, s->counter.as<unsigned>(), s->s_stop, cap, st);
             } else {
                 rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
@@ -525,9 +536,11 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                           sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), ++s->epoch};
     rtk::IowScene scene{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
                         s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link,
-                                 s->obox.as<float4>()};
-    const int cap_s = s->cus * rtk::resident_blocks_per_cu(5);
-    const int cap_q = s->cus * rtk::resident_blocks_per_cu(3);
+                                 s->obox.as<float4>(), s->n_wide};
+    // caps in 256-lane slots; the LDS-BVH kernels run 768-lane blocks
+    const bool lds = rtk::iow_lds(scene);
+    const int cap_s = s->cus * (lds ? 3 * rtk::resident_blocks_per_cu(10) : rtk::resident_blocks_per_cu(5));
+    const int cap_q = s->cus * (lds ? 3 * rtk::resident_blocks_per_cu(9) : rtk::resident_blocks_per_cu(3));
     hipError_t e = hipSuccess;
     // one compacted pass on a stream with its own queue counter and continuation buffers: the
     // first launch takes `n0` units, resume launches take the parked lanes
@@ -564,7 +577,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             return rtk::launch_iow03_spec(f, scene, RR, mode, ct, n, q.counter, cap_s, q.st);
         };
     };
-    s->last_kernel = "k_iow03s";
+    s->last_kernel = lds ? "k_iow03sL" : "k_iow03s";
     s->last_launches = (1 + rounds) * (1 + groups * ((S > 1 ? 1 : 0) + iters));
     // (1) on the caller's stream: sample 0 of every pixel (exact), the guesses for the other
     // samples, and the pixel order (heaviest sample 0 first)

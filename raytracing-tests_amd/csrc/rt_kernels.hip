@@ -255,9 +255,10 @@ __device__ __forceinline__ RayRet iow_eval(const IowScene &S, f3 go, f3 gd, floa
 // strictly nearer hit, i.e. the minimum t with the lowest index among exact ties.  The BVH
 // walk visits a superset of the objects that can attain that minimum and applies the same
 // (t, index) rule, so it returns the same object and the same t bits.
-template <int BCAP>
+// nodes: the 4-wide BVH (NS float4 per node: in LDS, 7; in global memory, 8), or null.
+template <int BCAP, int NS = 8>
 __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 gd, float max_t, float contrib,
-                                 Ctr &c, short *bstk) {
+                                 Ctr &c, short *bstk, const float4 *nodes) {
     DBG_T0(F_, t_ray);
     float min_t = max_t;
     int best = -1;
@@ -274,7 +275,7 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
         // 03...glsl:331-332): normalize(M*gd) is NaN for every object, so every t is -1 and
         // the reference's loop finds no hit -- skip it.
         c.prims += S.n;
-    } else if (S.nodes != nullptr && dl2 > 0.998f && dl2 < 1.002f) {
+    } else if (nodes != nullptr && dl2 > 0.998f && dl2 < 1.002f) {
         // Ordered walk with postponed leaves (speculative traversal): a lane that reaches a
         // leaf parks it and keeps walking inner nodes; primitive tests run when every lane
         // of the wave holds one (or has finished), so they execute with full lanes.
@@ -291,7 +292,7 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
             if (walking) {
                 bool pop;
                 if (cur > 0) {
-                    const float4 *nd = S.nodes + 8 * (size_t)(cur - 1);
+                    const float4 *nd = nodes + NS * (cur - 1);
                     const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
                     const float4 lk = nd[6];
                     c.nodes += 4;
@@ -568,28 +569,28 @@ __device__ __forceinline__ void iow_seg_shade(const IowScene &S, const Frame &F,
         }
     } else skip = 0;
 }
-template <bool NARROW>
+// BS: BVH-stack slots per lane (logical depth BS - 3: 3 spare push slots); NS: node stride
+template <bool NARROW, int BS, int NS>
 __device__ __forceinline__ void iow_segment(const IowScene &S, const Frame &F, IowStack<NARROW> &K, int &skip,
-                                            f3 &sample, int sidx, Ctr &c, short *bstk) {
-    constexpr int BCAP = (NARROW ? 12 : kIowBvhStack) - 3;  // logical depth; 3 spare push slots
+                                            f3 &sample, int sidx, Ctr &c, short *bstk, const float4 *nodes) {
     const SegIn in = iow_seg_pop(S, K, sidx);
-    const RayRet data = iow_launch_ray<BCAP>(S, F, in.co, in.cd, 32000.0f, in.contribution, c, bstk);
+    const RayRet data = iow_launch_ray<BS - 3, NS>(S, F, in.co, in.cd, 32000.0f, in.contribution, c, bstk, nodes);
     iow_seg_shade(S, F, K, skip, sample, sidx, c, in, data);
 }
 // The segment step of a work loop, called with every lane of the wave (seg: this lane has a
 // ray to trace).  With at most F.coop_max tracing lanes the wave runs their closest-hit
 // queries cooperatively (iow_coop_search), one ray after another; otherwise each lane walks
 // the BVH for its own ray.
-template <bool NARROW>
+template <bool NARROW, int BS, int NS>
 __device__ __forceinline__ void iow_seg_step(const IowScene &S, const Frame &F, IowStack<NARROW> &K, int &skip,
-                                             f3 &sample, int sidx, Ctr &c, short *bstk, bool seg) {
+                                             f3 &sample, int sidx, Ctr &c, short *bstk, const float4 *nodes, bool seg) {
     const unsigned long long m = __ballot(seg);
     if (m == 0) return;
     if (__popcll(m) > F.coop_max) {
-        if (seg) iow_segment(S, F, K, skip, sample, sidx, c, bstk);
+        if (seg) iow_segment<NARROW, BS, NS>(S, F, K, skip, sample, sidx, c, bstk, nodes);
         return;
     }
-    constexpr int kCap = (NARROW ? 12 : kIowBvhStack) * 64;  // the wave's BVH-stack slots, as a list
+    constexpr int kCap = BS * 64;  // the wave's BVH-stack slots, as a list
     short *wl = bstk - (threadIdx.x & 63);
     DBG_T0(F, t_pop);
     SegIn in{};
@@ -702,22 +703,49 @@ __device__ __forceinline__ uint32_t park_slot(unsigned *count, bool need) {
 __device__ __forceinline__ float ibits(int v) { return __int_as_float(v); }
 __device__ __forceinline__ float ubits(uint32_t v) { return __uint_as_float(v); }
 
-template <bool NARROW>
+// Kernel configurations of the IOW-03 work loops.  SUB: 256-thread sub-blocks per block, each
+// with its own [slot][thread] stack arrays (stride kBlock).  LN: the whole 4-wide BVH is copied
+// into the block's LDS (7 float4 per node) when it has at most kIowLdsNodes nodes: one
+// 768-thread block per CU shares it, so node fetches cost LDS latency instead of L2 latency.
+constexpr int kIowLdsNodes = 240;
+template <bool NARROW, int SUB, bool LN>
+struct IowCfg {
+    static constexpr int BS = LN ? 16 : (NARROW ? 12 : kIowBvhStack);  // BVH-stack slots per lane
+    static constexpr int NS = LN ? 7 : 8;                               // float4 per BVH node
+    static constexpr int kThreads = SUB * kBlock;
+};
+// copy the BVH into LDS (7 float4 per node, dropping the pad) and return the node base
+template <bool LN>
+__device__ __forceinline__ const float4 *iow_stage_nodes(const IowScene &S, float4 *s_nodes) {
+    if constexpr (!LN) return S.nodes;
+    else {
+        const uint32_t total = S.n_nodes * 7u;
+        for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) s_nodes[i] = S.nodes[(i / 7u) * 8u + i % 7u];
+        __syncthreads();
+        return s_nodes;
+    }
+}
+
+template <bool NARROW, int SUB, bool LN>
 __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, const Chunk &ch, const Cont &ct,
                                            unsigned *counter, int s_stop) {
     using Stack = IowStack<NARROW>;
+    using Cfg = IowCfg<NARROW, SUB, LN>;
     constexpr int kFl = kIowStack * Stack::kSlot;  // stack floats per lane
-    __shared__ float lds[kFl * kBlock];
-    __shared__ unsigned char lds_b[NARROW ? kIowStack * kBlock : 1];
-    __shared__ short lds_bvh[(NARROW ? 12 : kIowBvhStack) * kBlock];
-    short *bstk = lds_bvh + threadIdx.x;
-    __shared__ unsigned long long s_dbg[kBlock / 64][kDbgSlots];
+    __shared__ float lds[SUB * kFl * kBlock];
+    __shared__ unsigned char lds_b[NARROW ? SUB * kIowStack * kBlock : 1];
+    __shared__ short lds_bvh[SUB * Cfg::BS * kBlock];
+    __shared__ unsigned long long s_dbg[SUB * kBlock / 64][kDbgSlots];
+    __shared__ float4 s_nodes[LN ? kIowLdsNodes * 7 : 1];
+    const int sb = (int)(threadIdx.x / kBlock), tl = (int)(threadIdx.x % kBlock);
+    short *bstk = lds_bvh + sb * Cfg::BS * kBlock + tl;
+    const float4 *nodes = iow_stage_nodes<LN>(S, s_nodes);
     Ctr c;
     if (f.dbg) {
         c.wdbg = s_dbg[threadIdx.x >> 6];
         if ((threadIdx.x & 63) < kDbgSlots) c.wdbg[threadIdx.x & 63] = 0;
     }
-    Stack K{lds + threadIdx.x, lds_b + threadIdx.x, 0};
+    Stack K{lds + sb * kFl * kBlock + tl, lds_b + (NARROW ? sb * kIowStack * kBlock + tl : 0), 0};
     const uint32_t total = ct.in ? *ct.in_count : (ch.order_count ? *ch.order_count : units_total(f));
     const bool may_park = ct.out != nullptr && total >= ct.park_min;
     const int W = f.W, H = f.H, spp = f.spp;
@@ -822,7 +850,7 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
             f3 ro, rd;
             iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
             if (f.show_normal) {
-                fc = fc + iow_launch_ray<(NARROW ? 12 : kIowBvhStack) - 3>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
+                fc = fc + iow_launch_ray<Cfg::BS - 3, Cfg::NS>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk, nodes).normal;
                 s++;
                 urays++;
             } else {
@@ -836,7 +864,7 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
         DBG_T0(f, t_seg);
         {
             const bool seg = busy && K.size > 0;
-            iow_seg_step(S, f, K, skip, sample, s, c, bstk, seg);
+            iow_seg_step<NARROW, Cfg::BS, Cfg::NS>(S, f, K, skip, sample, s, c, bstk, nodes, seg);
             if (seg) {
                 urays++;
                 if (K.size == 0) { fc = fc + sample; s++; }
@@ -861,15 +889,18 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
     flush(f, c);
 }
 
-__global__ __launch_bounds__(kBlock) void k_iow03(Frame f, IowScene S, Chunk ch, Cont ct, unsigned *counter,
-                                                  int s_stop) {
-    iow03_body<false>(f, S, ch, ct, counter, s_stop);
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
+void k_iow03(Frame f, IowScene S, Chunk ch, Cont ct, unsigned *counter, int s_stop) {
+    iow03_body<false, 1, false>(f, S, ch, ct, counter, s_stop);
 }
-// u_NumOfBounce <= 255: byte bounce counts + 12-deep BVH stack -> 39 KB LDS per block, and a
-// 128-VGPR budget, so 4 waves per SIMD stay resident
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(3 * kBlock) void k_iow03L(Frame f, IowScene S, Chunk ch, Cont ct, unsigned *counter,
+                                                       int s_stop) {
+    iow03_body<false, 3, true>(f, S, ch, ct, counter, s_stop);
+}
+// u_NumOfBounce <= 255: byte bounce counts + 12-deep BVH stack -> 39 KB LDS per block (A/B layout)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
 void k_iow03n(Frame f, IowScene S, Chunk ch, Cont ct, unsigned *counter, int s_stop) {
-    iow03_body<true>(f, S, ch, ct, counter, s_stop);
+    iow03_body<true, 1, false>(f, S, ch, ct, counter, s_stop);
 }
 
 // ============================================================================ IOW-03, sample-parallel
@@ -880,23 +911,27 @@ void k_iow03n(Frame f, IowScene S, Chunk ch, Cont ct, unsigned *counter, int s_s
 // those entries (zeros in the first pass, else what the last resolve computed) and records
 // which entries it read before writing (rmask) and which it wrote (wmask); the resolve replays
 // the pixel in sample order and re-queues exactly the samples whose assumption was wrong.
-template <bool NARROW>
+template <bool NARROW, int SUB, bool LN>
 __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, const SpecRecs &R, int mode,
                                             const Cont &ct, unsigned *counter) {
     using Stack = IowStack<NARROW>;
+    using Cfg = IowCfg<NARROW, SUB, LN>;
     constexpr int kFl = kIowStack * Stack::kSlot;
-    constexpr int BCAP = (NARROW ? 12 : kIowBvhStack) - 3;
-    __shared__ float lds[kFl * kBlock];
-    __shared__ unsigned char lds_b[NARROW ? kIowStack * kBlock : 1];
-    __shared__ short lds_bvh[(NARROW ? 12 : kIowBvhStack) * kBlock];
-    short *bstk = lds_bvh + threadIdx.x;
-    __shared__ unsigned long long s_dbg[kBlock / 64][kDbgSlots];
+    constexpr int BCAP = Cfg::BS - 3;
+    __shared__ float lds[SUB * kFl * kBlock];
+    __shared__ unsigned char lds_b[NARROW ? SUB * kIowStack * kBlock : 1];
+    __shared__ short lds_bvh[SUB * Cfg::BS * kBlock];
+    __shared__ unsigned long long s_dbg[SUB * kBlock / 64][kDbgSlots];
+    __shared__ float4 s_nodes[LN ? kIowLdsNodes * 7 : 1];
+    const int sb = (int)(threadIdx.x / kBlock), tl = (int)(threadIdx.x % kBlock);
+    short *bstk = lds_bvh + sb * Cfg::BS * kBlock + tl;
+    const float4 *nodes = iow_stage_nodes<LN>(S, s_nodes);
     Ctr c;  // per unit here: written to the unit's record, never flushed
     if (f.dbg) {
         c.wdbg = s_dbg[threadIdx.x >> 6];
         if ((threadIdx.x & 63) < kDbgSlots) c.wdbg[threadIdx.x & 63] = 0;
     }
-    Stack K{lds + threadIdx.x, lds_b + threadIdx.x, 0};
+    Stack K{lds + sb * kFl * kBlock + tl, lds_b + (NARROW ? sb * kIowStack * kBlock + tl : 0), 0};
     const uint32_t total = ct.in ? *ct.in_count
                          : (mode == kSpecList ? *R.list_count : (mode == kSpecFirst ? R.P : R.order_n * (R.S - 1)));
     const bool may_park = ct.out != nullptr && total >= ct.park_min;
@@ -929,7 +964,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         f3 ro, rd;
         iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
         if (f.show_normal) {  // one ray, no stack: the normal is the sample
-            sample = iow_launch_ray<BCAP>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
+            sample = iow_launch_ray<BCAP, Cfg::NS>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk, nodes).normal;
             urays = 1;
         } else K.push(ro, rd, 1.0f, 1.0f, 0, c);
     };
@@ -983,7 +1018,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         DBG_T0(f, t_seg);
         {
             const bool seg = busy && K.size > 0;
-            iow_seg_step(S, f, K, skip, sample, (int)(u / R.P), c, bstk, seg);
+            iow_seg_step<NARROW, Cfg::BS, Cfg::NS>(S, f, K, skip, sample, (int)(u / R.P), c, bstk, nodes, seg);
             if (seg) urays++;
         }
         DBG_CYC(f, c, kDbgCycSeg, t_seg);
@@ -1050,7 +1085,11 @@ __global__ __launch_bounds__(kBlock) void k_iow03_fix(Frame f, SpecRecs R, float
 
 __global__ __launch_bounds__(kBlock) void k_iow03s(Frame f, IowScene S, SpecRecs R, int mode, Cont ct,
                                                    unsigned *counter) {
-    iow03s_body<false>(f, S, R, mode, ct, counter);
+    iow03s_body<false, 1, false>(f, S, R, mode, ct, counter);
+}
+__global__ __launch_bounds__(3 * kBlock) void k_iow03sL(Frame f, IowScene S, SpecRecs R, int mode, Cont ct,
+                                                        unsigned *counter) {
+    iow03s_body<false, 3, true>(f, S, R, mode, ct, counter);
 }
 
 // After the sample-0 pass: every later sample of a pixel assumes, for each stack entry 1..3,
@@ -1603,7 +1642,7 @@ __global__ __launch_bounds__(kBlock) void k_iow03a(Frame f, IowScene S, SpecRecs
         const float sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
         f3 ro, rd;
         iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
-        if (f.show_normal) sample = iow_launch_ray<BCAP>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk).normal;
+        if (f.show_normal) sample = iow_launch_ray<BCAP>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk, S.nodes).normal;
         else K.push(ro, rd, 1.0f, 1.0f, 0, c);
     };
     for (;;) {
@@ -1676,7 +1715,7 @@ __global__ __launch_bounds__(kBlock) void k_iow03a(Frame f, IowScene S, SpecRecs
         DBG_TALLY(f, c, kDbgOuter, busy);
         DBG_TALLY(f, c, kDbgSeg, busy && K.size > 0);
         DBG_T0(f, t_seg);
-        if (busy && K.size > 0) iow_segment(S, f, K, skip, sample, s, c, bstk);
+        if (busy && K.size > 0) iow_segment<false, kBvA, 8>(S, f, K, skip, sample, s, c, bstk, S.nodes);
         DBG_CYC(f, c, kDbgCycSeg, t_seg);
         // (4) finished samples write their record
         const bool fin = busy && K.size == 0;
@@ -1881,10 +1920,18 @@ bool iow_narrow(const Frame &f) {
     return f.max_bounces <= 255 && v && v[0] == '1';
 }
 
+// the LDS-node kernels (k_iow03L / k_iow03sL) when the BVH fits and RT_IOW_LDS is not 0
+bool iow_lds(const IowScene &sc) {
+    static const int on = [] { const char *v = std::getenv("RT_IOW_LDS"); return (v && v[0] == '0') ? 0 : 1; }();
+    return on && sc.nodes != nullptr && sc.n_nodes > 0 && sc.n_nodes <= (uint32_t)kIowLdsNodes;
+}
+
 int resident_blocks_per_cu(int kind) {
     int nb = 0;
     hipError_t e;
     if (kind == 3) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03, kBlock, 0);
+    else if (kind == 9) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03L, 3 * kBlock, 0);
+    else if (kind == 10) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03sL, 3 * kBlock, 0);
     else if (kind == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03n, kBlock, 0);
     else if (kind == 5) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03s, kBlock, 0);
     else if (kind == 8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03a, kBlock, 0);
@@ -1903,6 +1950,11 @@ hipError_t launch_iow03(const Frame &f, const IowScene &sc, const Chunk &ch, con
                         unsigned *counter, int s_stop, int blocks_cap, hipStream_t s) {
     hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
     if (e != hipSuccess) return e;
+    if (!iow_narrow(f) && iow_lds(sc)) {
+        const dim3 g(grid_of((n_units + 2) / 3, blocks_cap / 3));  // blocks_cap counts 256-lane slots
+        hipLaunchKernelGGL(k_iow03L, g, dim3(3 * kBlock), 0, s, f, sc, ch, ct, counter, s_stop);
+        return hipGetLastError();
+    }
     const dim3 g(grid_of(n_units, blocks_cap));
     if (iow_narrow(f)) hipLaunchKernelGGL(k_iow03n, g, dim3(kBlock), 0, s, f, sc, ch, ct, counter, s_stop);
     else hipLaunchKernelGGL(k_iow03, g, dim3(kBlock), 0, s, f, sc, ch, ct, counter, s_stop);
@@ -1912,7 +1964,12 @@ hipError_t launch_iow03_spec(const Frame &f, const IowScene &sc, const SpecRecs 
                              uint32_t n_units, unsigned *counter, int blocks_cap, hipStream_t s) {
     hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_iow03s, dim3(grid_of(n_units, blocks_cap)), dim3(kBlock), 0, s, f, sc, R, mode, ct, counter);
+    if (iow_lds(sc))
+        hipLaunchKernelGGL(k_iow03sL, dim3(grid_of((n_units + 2) / 3, blocks_cap / 3)), dim3(3 * kBlock), 0, s, f, sc, R,
+                           mode, ct, counter);
+    else
+        hipLaunchKernelGGL(k_iow03s, dim3(grid_of(n_units, blocks_cap)), dim3(kBlock), 0, s, f, sc, R, mode, ct,
+                           counter);
     return hipGetLastError();
 }
 // diagnostics: log2 histogram of rays per sample over the last sample-parallel render

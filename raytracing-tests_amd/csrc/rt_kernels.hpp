@@ -48,6 +48,7 @@ struct IowScene {
     const int *ring;         // spp*2
     int root_link;           // link of the BVH root (wide node 0 -> 1)
     const float4 *obox;      // the BVH leaves' conservative boxes: n float4 (lo.xyz, hi.x), n float2 (hi.yz); or null
+    uint32_t n_nodes;        // 4-wide BVH nodes
 };
 struct InwScene {
     const float4 *hot;       // n * 7 float4
@@ -183,6 +184,7 @@ int resident_blocks_per_cu(int kind);  // 5 = sample-parallel IOW-03, 6/7 = samp
 // IOW-03 kernel variant for this frame: narrow (byte bounce counts, 12-deep BVH stack, 4 waves
 // per SIMD with spills) when RT_IOW_NARROW=1 and u_NumOfBounce <= 255; wide otherwise
 bool iow_narrow(const Frame &f);
+bool iow_lds(const IowScene &sc);  // k_iow03L / k_iow03sL (BVH in LDS) apply; their blocks_cap counts 256-lane slots
 // order[i] = unit ids sorted by cost, most expensive first (hipcub radix sort)
 hipError_t sort_units_by_cost(const unsigned *cost, unsigned *keys_tmp, const unsigned *iota, unsigned *order,
                               uint32_t n, void *temp, size_t temp_bytes, hipStream_t s);

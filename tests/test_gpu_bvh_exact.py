@@ -11,6 +11,7 @@
 - RT_SPEC_GROUPS=2/7: pixel groups on separate streams;
 - RT_IOW_ASYNC=1: asynchronous windows (per-wave frontiers) instead of global resolve passes;
 - RT_SPEC_FIX=1: mid-pass correction of parked samples (patch / restart with the exact state);
+- RT_IOW_LDS=0: the BVH read from global memory instead of staged in LDS (768-lane blocks);
 - RT_COOP=0/64: no wave-cooperative closest hits / every closest hit wave-cooperative (default:
   waves with at most 4 tracing lanes);
 - INW: RT_INW_SPEC=0 (per-pixel sequential samples) and RT_SPEC_MAX_GB tiny (sample chunks).
@@ -51,7 +52,7 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     env = dict(os.environ)
     for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS", "RT_IOW_SPEC", "RT_SPEC_ITERS",
               "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_SPEC_GROUPS", "RT_IOW_ASYNC", "RT_SPEC_FIX",
-              "RT_SPEC_VALIDATE", "RT_SPEC_PRIOR_FROM", "RT_COOP"):
+              "RT_SPEC_VALIDATE", "RT_SPEC_PRIOR_FROM", "RT_COOP", "RT_IOW_LDS"):
         env.pop(k, None)
     env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out, preset=scene[0], seed=scene[1], n_hint=scene[2])
@@ -76,6 +77,8 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     ({"RT_SPEC_FIX": "1"}, 600, 400, 12),
     ({"RT_SPEC_GROUPS": "2"}, 300, 200, 12),
     ({"RT_COOP": "0"}, 600, 400, 8),
+    ({"RT_IOW_LDS": "0"}, 600, 400, 8),
+    ({"RT_IOW_LDS": "0", "RT_IOW_SPEC": "0"}, 300, 200, 8),
     ({"RT_COOP": "64"}, 300, 200, 4),
     ({"RT_COOP": "64", "RT_IOW_SPEC": "0"}, 300, 200, 4),
     ({"RT_COOP": "64", "RT_IOW_LINEAR": "1"}, 200, 100, 2),
