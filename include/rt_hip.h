@@ -100,6 +100,18 @@ int  rt_device_info(int device, char *name_out, int name_cap, int *cu_count);
 int rt_render_iow01(const rt_camera *cam, const float sphere[4] /* centre xyz, radius */,
                     const rt_params *p, float *rgba /* W*H*4 */, rt_stats *st);
 
+/* IOW-00: the base stage's default compute shader (In-One-Weekend/base.cpp:7-28, dispatched
+ * W x H by 00_Image/image.cpp:46-53): rgba = (x/(W-1), y/(H-1), 0.25, 1). */
+int rt_render_iow00(const rt_params *p, float *rgba /* W*H*4 */);
+
+/* IOW-02 groups stage (02_Groups/computeShaderSrc.glsl; host groups.cpp:56-84, CopyObjBuffer
+ * :250-285): records N x 18 = position, inverse rotation (glm column-major), scale, colour
+ * (groups.h:11-17 GeometryBuff; the first 18 floats of an IOW-03 record), types 1 = CUBOID,
+ * 2 = ELLIPSOID; u_Cull_Front / u_Cull_Back; u_NumOfBounce = p->max_bounces, u_FocusDist =
+ * cam->focus_dist.  st->segments = bounce iterations (closest-hit queries). */
+int rt_render_iow02(const float *types, const float *records /* N*18 */, uint32_t n, const rt_camera *cam,
+                    const rt_params *p, int cull_front, int cull_back, float *rgba, rt_stats *st);
+
 int rt_render_iow03(const float *types /* N, float(Geom_type) */,
                     const float *records /* N*24, materials.h:11-19 */, uint32_t n,
                     const rt_camera *cam, const rt_params *p, float *rgba, rt_stats *st);
@@ -111,6 +123,13 @@ int rt_render_inw(const float *geom /* N*28, layout 1 (BVH.h:12-19) or 4 (lights
                   uint32_t n_lights,
                   const rt_camera *cam, const rt_params *p,
                   float *rgba /* W*H*4 */, float *depth /* W*H, may be NULL */, rt_stats *st);
+
+/* INW-01 (layout 1) with the shader's "#if MULTIFOCUS" branch compiled in
+ * (01_BoundingVolumeHierarchy/computeShaderSrc.glsl:388-404, 424-428, 479-481, 505-549; the
+ * reference never defines MULTIFOCUS): u_Camera.FocusDist[0..n_focus-1] = focus, 1..9 values
+ * (u_NumOfFocusDist, In-Next-Week/base.h:458-473).  cam->focus_dist is not used. */
+int rt_render_inw_mf(const float *geom /* N*28, layout 1 */, uint32_t n, const float *nodes, const rt_camera *cam,
+                     const float *focus, int n_focus, const rt_params *p, float *rgba, float *depth, rt_stats *st);
 
 /* ---- textures --------------------------------------------------------
  * INW-04 material textures, u_MaterialTextures[u_NumOfTexture2D]

@@ -24,6 +24,7 @@ extern "C" {
 
 /* Stage (which shader / record layout a description is packed for). */
 #define RT_STAGE_IOW01 1
+#define RT_STAGE_IOW02 2
 #define RT_STAGE_IOW03 3
 #define RT_STAGE_INW01 11
 #define RT_STAGE_INW04 14
@@ -75,6 +76,8 @@ int rt_camera_from_desc(const rt_cam_desc *d, int stage, rt_camera *out);
 
 /* IOW-03: types[N] (float type code), records[N*24] (Geometry::FillBuffer). */
 int rt_pack_iow03(const rt_geom_desc *g, uint32_t n, float *types, float *records);
+/* IOW-02: types[N], records[N*18] (Groups::Geometry::FillBuffer, groups.h:45-64). */
+int rt_pack_iow02(const rt_geom_desc *g, uint32_t n, float *types, float *records);
 
 /* INW: geom[N*28] in layout 1 or 4, aabbs[N*6] (CalculateBBMinMax of that layout),
  * lights[N*7] (only the first *n_lights used; LightClass with idx bit-cast) may be NULL. */

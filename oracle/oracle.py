@@ -26,7 +26,8 @@ def load():
         lib.orc_set_threads.argtypes = [C.c_int]
         for fn in ("orc_render_iow01", "orc_render_iow03", "orc_render_inw", "orc_lbvh_build",
                    "orc_pack_iow03", "orc_pack_inw", "orc_sample_tables", "orc_render_inw_tex",
-                   "orc_noise_texture", "orc_texture_remap"):
+                   "orc_noise_texture", "orc_texture_remap", "orc_render_iow00", "orc_render_iow02",
+                   "orc_render_inw_mf"):
             getattr(lib, fn).restype = C.c_int
         lib.orc_noise_texture.argtypes = [C.c_int, C.c_int, C.c_int, _FP, C.c_int, C.c_float, C.c_float,
                                           C.c_float, C.c_int, C.c_void_p]
@@ -73,6 +74,42 @@ def render_iow01(camera, sphere, params):
     if rc:
         raise RuntimeError(f"orc_render_iow01 -> {rc}")
     return rgba, _sd(st)
+
+
+def render_iow00(params):
+    """IOW-00: the base stage's default compute shader (base.cpp:7-28)."""
+    rgba = np.zeros((params.height, params.width, 4), np.float32)
+    rc = load().orc_render_iow00(C.byref(params), _f(rgba))
+    if rc:
+        raise RuntimeError(f"orc_render_iow00 -> {rc}")
+    return rgba
+
+
+def render_iow02(types, records, camera, params, cull_front=0, cull_back=1):
+    """IOW-02 groups stage (02_Groups/computeShaderSrc.glsl); records N x 18."""
+    types = np.ascontiguousarray(types, np.float32)
+    records = np.ascontiguousarray(records, np.float32).reshape(-1, 18)
+    rgba = np.zeros((params.height, params.width, 4), np.float32)
+    st = _stats_struct()
+    rc = load().orc_render_iow02(_f(types), _f(records), C.c_uint32(len(types)), C.byref(camera), C.byref(params),
+                                 C.c_int(cull_front), C.c_int(cull_back), _f(rgba), C.byref(st))
+    if rc:
+        raise RuntimeError(f"orc_render_iow02 -> {rc}")
+    return rgba, _sd(st)
+
+
+def render_inw_mf(scene, focus, params=None):
+    """INW-01 with its MULTIFOCUS branch (01_BVH...glsl:388-404, 505-549) and focus distances `focus`."""
+    p = params or scene.params
+    f = np.ascontiguousarray(focus, np.float32)
+    rgba = np.zeros((p.height, p.width, 4), np.float32)
+    depth = np.zeros((p.height, p.width), np.float32)
+    st = _stats_struct()
+    rc = load().orc_render_inw_mf(_f(scene.geom), C.c_uint32(scene.n), _f(scene.nodes), C.byref(scene.camera),
+                                  _f(f), C.c_int(len(f)), C.byref(p), _f(rgba), _f(depth), C.byref(st))
+    if rc:
+        raise RuntimeError(f"orc_render_inw_mf -> {rc}")
+    return rgba, depth, _sd(st)
 
 
 def render(scene, params=None):

@@ -7,6 +7,8 @@
  *   "01.glsl"  = In-One-Weekend/01_Adding_Sphere/computeShaderSrc.glsl
  *   "BVH.glsl" = In-Next-Week/01_BoundingVolumeHierarchy/computeShaderSrc.glsl
  *   "04.glsl"  = In-Next-Week/04_Lights_Camera_And_Action/computeShaderSrc.glsl
+ *   "02.glsl"  = In-One-Weekend/02_Groups/computeShaderSrc.glsl
+ *   "base.cpp" = In-One-Weekend/base.cpp (the default compute shader, IOW-00)
  */
 #include "rt_oracle.h"
 #include "rt_oracle_common.h"
@@ -471,6 +473,8 @@ typedef struct {
     v3 camdir;
     const orc_texture *tex; /* u_MaterialTextures[u_NumOfTexture2D] (04.glsl:10) */
     uint32_t n_tex;
+    int n_focus;            /* MULTIFOCUS (BVH.glsl:388-404, 425-427, 479-481, 505-536, 544-549): 0 = off */
+    float focus[9];         /* u_Camera.FocusDist[u_NumOfFocusDist] (BVH.glsl:220,226; base.h:458-473) */
 } inw_scene;
 
 typedef struct { v3 pos, scale, delta; m3 R; int type; float extra; } xform_t;
@@ -697,10 +701,22 @@ static void inw_sample(const inw_scene *S, int px, int py, int W, int H, float s
         cam.d = normalize(add(add(mul(D, sd), mul(cr, srx)), mul(cu, sry)));
         float ox = S->sf[2 * s] * (aperture * 0.5f), oy = S->sf[2 * s + 1] * (aperture * 0.5f);
         v3 rr = cross(cam.d, up), ru = cross(rr, cam.d);
-        v3 tip = add(add(add(cam.o, cam.d), mul(rr, ox)), mul(ru, oy));
-        v3 la = normalize(sub(add(cam.o, mul(cam.d, focus)), tip));
-        cam.o = sub(tip, la);
-        cam.d = la;
+        if (S->n_focus > 0) { /* MULTIFOCUS lens set-up, BVH.glsl:388-400 */
+            float first_limit = S->focus[0] * 0.5f;
+            v3 nd = normalize(add(add(mul(cam.d, first_limit), mul(rr, ox)), mul(ru, oy)));
+            v3 rn = normalize(sub(mul(neg(rr), ox), mul(ru, oy)));
+            float mult = 1.0f / dot(cam.d, nd);
+            cam.d = nd;
+            stk_push(&K, rn.x, c); stk_push(&K, rn.y, c); stk_push(&K, rn.z, c); /* 0..2 */
+            stk_push(&K, mult, c);                                              /* 3 */
+            stk_push(&K, first_limit, c);                                       /* 4 */
+            stk_push(&K, 0.0f, c);                                              /* 5 crossedLens */
+        } else {
+            v3 tip = add(add(add(cam.o, cam.d), mul(rr, ox)), mul(ru, oy));
+            v3 la = normalize(sub(add(cam.o, mul(cam.d, focus)), tip));
+            cam.o = sub(tip, la);
+            cam.d = la;
+        }
         stk_push_ray(&K, cam, 1.0f, 0.0f, c);
     }
     const int L4 = S->layout == 4;
@@ -718,12 +734,15 @@ static void inw_sample(const inw_scene *S, int px, int py, int W, int H, float s
             contribution = d[6]; bounced = (float)(int)d[7];
         }
         c->seg++;
-        float tlim = MAX_T_DEPTH;
+        /* SET LIMIT BVH.glsl:424-428: the primary ray of a MULTIFOCUS sample stops at the lens */
+        const int mf0 = S->n_focus > 0 && (int)(bounced + 0.1f) == 0;
+        const float tlim0 = mf0 ? K.data[4] : MAX_T_DEPTH;
+        float tlim = tlim0;
         float extra = 0.0f;
         float fg = traverse(S, &K, cur, ratio, &tlim, &normal, &extra, L4 ? -1.0f : 0.0f, 0, c);
         incoming = cur.d;
         hitpoint = add(cur.o, mul(cur.d, tlim));
-        if (tlim < MAX_T_DEPTH) {
+        if (tlim < tlim0) {
             const float *f = S->geom + (size_t)fg * 28;
             if (!L4) { /* FillHitData BVH.glsl:349-361 */
                 m_ri = f[20]; m_refr = f[21]; m_refl = f[22]; m_srfr = f[23]; m_srfl = f[24];
@@ -738,11 +757,29 @@ static void inw_sample(const inw_scene *S, int px, int py, int W, int H, float s
                 }
             }
             surr = surrounding_ri(S, &K, add(hitpoint, mul(normal, 0.001f)), ratio, c);
+        } else if (mf0 && (int)(K.data[5] + 0.1f) < S->n_focus) {
+            /* move to the next focal lens, BVH.glsl:506-528 */
+            v3 rn = V3(K.data[0], K.data[1], K.data[2]);
+            K.data[0] = -K.data[0]; K.data[1] = -K.data[1]; K.data[2] = -K.data[2];
+            float mult = K.data[3], dist = K.data[4];
+            cur.o = add(cur.o, mul(cur.d, mult * dist));
+            cur.d = reflect3(cur.d, rn);
+            int lens = (int)(K.data[5] + 0.1f);
+            if (lens < S->n_focus - 1)
+                K.data[4] = (S->focus[lens + 1] - S->focus[lens]) * 0.5f +
+                            (S->focus[lens] - (lens > 0 ? S->focus[lens - 1 > 0 ? lens - 1 : 0] : 0.0f)) * 0.5f;
+            else K.data[4] = MAX_T_DEPTH - mult * K.data[4];
+            K.data[5] += 1.0f;
+            K.size = 6;
+            stk_push_ray(&K, cur, 1.0f, 0.0f, c);
+            continue;
         } else {
             color = add(color, mul(background(cur.d, L4 && S->n_lights > 0), contribution));
             depth = tlim;
+            if (mf0) K.size = 0; /* BVH.glsl:531-535 */
             continue;
         }
+        if (mf0) K.size = 0;     /* BVH.glsl:544-549: the lens record is dropped after a primary hit */
         if (L4) { /* 04.glsl:604-665 */
             uint32_t is_lit = S->n_lights > 0 ? 0u : (uint32_t)is_lit_geom(S, f2u(fg + 0.1f));
             if (is_lit == 0) {
@@ -807,10 +844,27 @@ static void inw_sample(const inw_scene *S, int px, int py, int W, int H, float s
     *out_depth = depth;
 }
 
+/* MULTIFOCUS focus list of the next orc_render_inw_tex call (set by orc_render_inw_mf only) */
+static _Thread_local int g_mf_n = 0;
+static _Thread_local float g_mf_focus[9];
+
 int orc_render_inw(const float *geom, uint32_t n, int layout, const float *nodes,
                    const float *lights, uint32_t n_lights, const orc_camera *cam,
                    const orc_params *p, float *rgba, float *depth, orc_stats *st) {
     return orc_render_inw_tex(geom, n, layout, nodes, lights, n_lights, NULL, 0, cam, p, rgba, depth, st);
+}
+
+/* INW-01 with the MULTIFOCUS branch compiled in (BVH.glsl:388-404 etc.; the reference ships
+ * it as "#if MULTIFOCUS", never defined): n_focus in 1..9 focus distances. */
+int orc_render_inw_mf(const float *geom, uint32_t n, const float *nodes, const orc_camera *cam,
+                      const float *focus, int n_focus, const orc_params *p, float *rgba, float *depth,
+                      orc_stats *st) {
+    if (!focus || n_focus < 1 || n_focus > 9) return -1;
+    g_mf_n = n_focus;
+    memcpy(g_mf_focus, focus, sizeof(float) * (size_t)n_focus);
+    int rc = orc_render_inw_tex(geom, n, 1, nodes, NULL, 0, NULL, 0, cam, p, rgba, depth, st);
+    g_mf_n = 0;
+    return rc;
 }
 
 int orc_render_inw_tex(const float *geom, uint32_t n, int layout, const float *nodes,
@@ -839,6 +893,11 @@ int orc_render_inw_tex(const float *geom, uint32_t n, int layout, const float *n
     S.camdir = V3(cam->dir[0], cam->dir[1], cam->dir[2]);
     S.tex = layout == 4 ? tex : NULL;
     S.n_tex = layout == 4 ? n_tex : 0;
+    S.n_focus = 0;
+    if (g_mf_n > 0 && layout == 1) {
+        S.n_focus = g_mf_n;
+        memcpy(S.focus, g_mf_focus, sizeof(float) * (size_t)g_mf_n);
+    }
     const float sd = 1.0f / (2.0f * (float)tan((double)(cam->fov_y_rad * 0.5f)));
     const v3 P = V3(cam->pos[0], cam->pos[1], cam->pos[2]);
     ctr total = {0, 0, 0, 0, 0, 0};
@@ -873,5 +932,146 @@ int orc_render_inw_tex(const float *geom, uint32_t n, int layout, const float *n
     }
     free(sf);
     if (st) { memset(st, 0, sizeof(*st)); ctr_add(st, &total); st->ms = now_ms() - t0; }
+    return 0;
+}
+
+/* ===================================================================================
+ * IOW-00: the base stage's default compute shader (base.cpp:7-28): a UV gradient
+ * =================================================================================== */
+int orc_render_iow00(const orc_params *p, float *rgba) {
+    if (!p || !rgba || p->width <= 0 || p->height <= 0) return -1;
+    const int W = p->width, H = p->height;
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            float *o = rgba + ((size_t)y * W + x) * 4;
+            o[0] = (float)x * rcp((float)W - 1.0f); /* pixel_coords.x / (imageSize.x - 1.0) :13 */
+            o[1] = (float)y * rcp((float)H - 1.0f); /* :14 */
+            o[2] = 0.25f;
+            o[3] = 1.0f;
+        }
+    return 0;
+}
+
+/* ===================================================================================
+ * IOW-02: 02.glsl (groups.h:11-17 record: position, inverse rotation mat3, scale, colour)
+ * =================================================================================== */
+/* t_RayXObj 02.glsl:37-94, with the u_Cull_Front / u_Cull_Back modes */
+static float t_ray_obj_cull(ray_t r, int type, v3 s, int cull_front, int cull_back) {
+    float t = -1.0f;
+    if (type == IOW_ELLIPSOID) {
+        v3 a2 = V3(r.o.x * rcp(s.x), r.o.y * rcp(s.y), r.o.z * rcp(s.z));
+        v3 a3 = V3(r.d.x * rcp(s.x), r.d.y * rcp(s.y), r.d.z * rcp(s.z));
+        float hb = dot(a2, a3), a = dot(a3, a3), c = dot(a2, a2) - 1.0f;
+        float det = hb * hb - a * c;
+        if (det > 0) {
+            float t0 = (-hb - sqrtf(det)) * rcp(a), t1 = (-hb + sqrtf(det)) * rcp(a);
+            if (!cull_back && !cull_front) t = (t0 > t1 || t0 < 0) ? t1 : t0;
+            else if (!cull_front) t = fmin_(t0, t1);
+            else if (!cull_back) t = fmax_(t0, t1);
+        }
+    } else if (type == IOW_CUBOID) {
+        v3 bmin = mul(neg(s), 0.5f), bmax = mul(s, 0.5f);
+        float t1 = (bmin.x - r.o.x) * rcp(r.d.x), t2 = (bmax.x - r.o.x) * rcp(r.d.x);
+        float tmin = fmin_(t1, t2), tmax = fmax_(t1, t2);
+        for (int i = 1; i < 3; ++i) {
+            t1 = (v3get(bmin, i) - v3get(r.o, i)) * rcp(v3get(r.d, i));
+            t2 = (v3get(bmax, i) - v3get(r.o, i)) * rcp(v3get(r.d, i));
+            tmin = fmax_(tmin, fmin_(fmin_(t1, t2), tmax));
+            tmax = fmin_(tmax, fmax_(fmax_(t1, t2), tmin));
+        }
+        if (tmax > fmax_(tmin, 0.0f)) {
+            if (!cull_back && !cull_front) t = tmin > 0 ? tmin : tmax;
+            else if (!cull_front) t = tmin;
+            else if (!cull_back) t = tmax;
+        }
+    }
+    return t > 0 ? t : -1.0f;
+}
+
+int orc_render_iow02(const float *types, const float *records, uint32_t n, const orc_camera *cam,
+                     const orc_params *p, int cull_front, int cull_back, float *rgba, orc_stats *st) {
+    if ((n > 0 && (!types || !records)) || !cam || !p || !rgba || p->width <= 0 || p->height <= 0 || p->spp < 1 ||
+        p->max_bounces < 0)
+        return -1;
+    double t0 = now_ms();
+    const int W = p->width, H = p->height, spp = p->spp, nb = p->max_bounces;
+    int x0 = p->tile_x0, y0 = p->tile_y0, tw = p->tile_w, th = p->tile_h;
+    if (tw <= 0 || th <= 0) { x0 = 0; y0 = 0; tw = W; th = H; }
+    int *ring = (int *)malloc(sizeof(int) * 2 * (size_t)spp);
+    float *pw = (float *)malloc(sizeof(float) * (size_t)(nb > 0 ? nb : 1));
+    orc_sample_tables(spp, NULL, NULL, ring);
+    for (int i = 0; i < nb; i++) pw[i] = (float)pow((double)0.4f, (double)i); /* pow(0.4, i) :206 */
+    const v3 D = V3(cam->dir[0], cam->dir[1], cam->dir[2]);
+    const v3 P = V3(cam->pos[0], cam->pos[1], cam->pos[2]);
+    int grid = 1;
+    while (grid * grid < spp) grid++;
+    uint64_t seg_total = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(orc_num_threads()) reduction(+ : seg_total)
+    for (int yy = y0; yy < y0 + th; yy++) {
+        for (int xx = x0; xx < x0 + tw; xx++) {
+            if (xx < 0 || yy < 0 || xx >= W || yy >= H) continue;
+            float aspect = (float)W * rcp((float)H);                          /* :133 */
+            const v3 up = V3(0, 1, 0);
+            float sx = ((float)xx * 2.0f - (float)W) * rcp(2.0f * (float)W);  /* :135 */
+            sx *= aspect;
+            float sy = ((float)yy * 2.0f - (float)H) * rcp(2.0f * (float)H);  /* :137 */
+            v3 fc = V3(0, 0, 0);
+            int s = 0, early = 0;
+            for (; s < spp; s++) {
+                v3 ro = P, rd;
+                {
+                    v3 cr = cross(D, up), cu = cross(cr, D);
+                    if (ring[2 * s] < 0) { early = 1; break; } /* :156: return final_color/samples_processed */
+                    float dx = aspect * rcp((float)(W * grid));
+                    float dy = 1.0f * rcp((float)(H * grid));
+                    rd = normalize(add(add(mul(D, cam->focus_dist), mul(cr, sx + dx * (float)ring[2 * s])),
+                                       mul(cu, sy + dy * (float)ring[2 * s + 1])));
+                }
+                float min_t = 32000.0f;
+                v3 nrm = D;
+                v3 fsc = V3(0, 0, 0);
+                for (int i = 0; i < nb; i++) {
+                    v3 sc = background(rd, 0);                                /* :172-175 */
+                    m3 hit_m = {{{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}};
+                    seg_total++;
+                    for (uint32_t j = 0; j < n; j++) {
+                        const float *r = records + (size_t)j * 18;
+                        int type = (int)types[j];
+                        v3 pos = V3(r[0], r[1], r[2]);
+                        m3 M = rec_m3(r + 3);
+                        v3 scale = V3(r[12], r[13], r[14]), col = V3(r[15], r[16], r[17]);
+                        ray_t tr = {m3mul(M, sub(ro, pos)), normalize(m3mul(M, rd))}; /* :194-198 */
+                        float t = t_ray_obj_cull(tr, type, scale, cull_front, cull_back);
+                        if (min_t > t && t > 0) {
+                            nrm = iow_normal(t, tr, type, scale);
+                            sc = col;
+                            hit_m = M;
+                            min_t = t;
+                        }
+                    }
+                    fsc = add(fsc, mul(sc, pw[i]));                           /* :206 */
+                    if (p->show_normal) { fsc = nrm; break; }
+                    if (min_t > 30000.0f) break;
+                    ro = add(ro, mul(rd, min_t - 0.00005f));                  /* :215 */
+                    v3 tn = normalize(m3mul(m3inverse(hit_m), nrm));
+                    rd = reflect3(rd, tn);
+                    nrm = V3(0, 0, 0);
+                    min_t = 32000.0f;
+                }
+                fc = add(fc, fsc);
+            }
+            v3 out = early ? mul(fc, rcp((float)s)) : mul(fc, rcp((float)spp));
+            float *o = rgba + ((size_t)yy * W + xx) * 4;
+            o[0] = out.x; o[1] = out.y; o[2] = out.z; o[3] = 1.0f;
+        }
+    }
+    free(ring);
+    free(pw);
+    if (st) {
+        memset(st, 0, sizeof(*st));
+        st->segments = seg_total;
+        st->prim_tests = seg_total * n;
+        st->ms = now_ms() - t0;
+    }
     return 0;
 }

@@ -7,9 +7,12 @@
  *
  * What it is: a line-by-line C restatement of the reference GLSL compute shaders and of
  * the host code that feeds them (paths relative to /root/reference/Raytracing-Sandbox/Src/):
+ *   IOW-00  In-One-Weekend/base.cpp:7-28 (default compute shader)          (orc_render_iow00)
  *   IOW-01  In-One-Weekend/01_Adding_Sphere/computeShaderSrc.glsl            (orc_render_iow01)
+ *   IOW-02  In-One-Weekend/02_Groups/computeShaderSrc.glsl                   (orc_render_iow02)
  *   IOW-03  In-One-Weekend/03_Shadows_and_Materials/computeShaderSrc.glsl    (orc_render_iow03)
- *   INW-01  In-Next-Week/01_BoundingVolumeHierarchy/computeShaderSrc.glsl    (orc_render_inw, layout 1)
+ *   INW-01  In-Next-Week/01_BoundingVolumeHierarchy/computeShaderSrc.glsl    (orc_render_inw, layout 1;
+ *           its "#if MULTIFOCUS" branch: orc_render_inw_mf)
  *   INW-04  In-Next-Week/04_Lights_Camera_And_Action/computeShaderSrc.glsl   (orc_render_inw, layout 4)
  *   LBVH    In-Next-Week/LBVH/lbvh.h                                         (orc_lbvh_build)
  *   packers materials.h:48-86, base.h:24-71, BVH.h:47-58, lights.h:40-141, utility.cpp:489-516
@@ -50,13 +53,22 @@ typedef struct {
 int orc_num_threads(void);
 void orc_set_threads(int n);
 
+int orc_render_iow00(const orc_params *p, float *rgba);
 int orc_render_iow01(const orc_camera *cam, const float sphere[4], const orc_params *p,
                      float *rgba, orc_stats *st);
+/* IOW-02 records: N x 18 floats = position, inverse rotation (glm column-major), scale, colour
+ * (groups.h:11-17, the first 18 floats of an IOW-03 record); types 1 = CUBOID, 2 = ELLIPSOID */
+int orc_render_iow02(const float *types, const float *records, uint32_t n, const orc_camera *cam,
+                     const orc_params *p, int cull_front, int cull_back, float *rgba, orc_stats *st);
 int orc_render_iow03(const float *types, const float *records, uint32_t n,
                      const orc_camera *cam, const orc_params *p, float *rgba, orc_stats *st);
 int orc_render_inw(const float *geom, uint32_t n, int layout, const float *nodes,
                    const float *lights, uint32_t n_lights, const orc_camera *cam,
                    const orc_params *p, float *rgba, float *depth, orc_stats *st);
+/* INW-01 (layout 1) with MULTIFOCUS compiled in: focus[0..n_focus-1], 1 <= n_focus <= 9 */
+int orc_render_inw_mf(const float *geom, uint32_t n, const float *nodes, const orc_camera *cam,
+                      const float *focus, int n_focus, const orc_params *p, float *rgba, float *depth,
+                      orc_stats *st);
 
 /* INW-04 material textures: texels row 0 first (GL upload order), channels 3 (RGB8) or 4 (RGBA8) */
 typedef struct { const uint8_t *texels; int width, height, channels; } orc_texture;

@@ -112,6 +112,8 @@ struct rt_dev_scene {
     int root_link = 0;   // IOW-03 culling BVH: leftData of the root
     uint32_t n_wide = 0; // IOW-03 culling BVH: 4-wide nodes
     float ri_prior = 1.0f;  // IOW-03: most common refractive index (sample-parallel guess)
+    int n_focus = 0;        // INW-01 MULTIFOCUS lens chain (0 = the reference's single focus)
+    float focus[9] = {};
     DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
     DevBuf obox;  // IOW-03: per-object culling boxes (2 float4 each) for wave-cooperative queries
     DevBuf tex, tex_info;  // INW-04 material textures (float4 texels, (first, w, h, 0) per texture)
@@ -431,6 +433,8 @@ int launch_scene_inw_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st, int ns
 int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st);
 
 int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
+    f.n_focus = (s->kind != 3 && s->layout == 1) ? s->n_focus : 0;
+    std::memcpy(f.focus_list, s->focus, sizeof(f.focus_list));
     if (s->kind == 3 && env_int("RT_IOW_SPEC", 1) != 0 && !rtk::iow_narrow(f) && s->s_stop > 0 &&
         ensure_spec(s, rtk::units_of(f), uint32_t(s->s_stop)))
         return launch_scene_spec(s, f, st);
@@ -1236,7 +1240,7 @@ int rt_scene_preset(int preset, uint32_t seed, int n_hint, rt_geom_desc *out, in
 
 int rt_camera_from_desc(const rt_cam_desc *d, int stage, rt_camera *out) {
     if (!d || !out) return RT_E_ARG;
-    const bool iow = stage == RT_STAGE_IOW01 || stage == RT_STAGE_IOW03;
+    const bool iow = stage == RT_STAGE_IOW01 || stage == RT_STAGE_IOW02 || stage == RT_STAGE_IOW03;
     if (!iow && stage != RT_STAGE_INW01 && stage != RT_STAGE_INW04) return RT_E_ARG;
     rtamd::Vec3 fr = rtamd::front_from_pitch_yaw(d->pitch_deg, d->yaw_deg, iow);
     std::memcpy(out->pos, d->position, sizeof(out->pos));
@@ -1252,6 +1256,20 @@ int rt_pack_iow03(const rt_geom_desc *g, uint32_t n, float *types, float *record
     for (uint32_t k = 0; k < n; k++) {
         rtamd::IowGeometry geo = rtamd::to_iow(g[k]);
         geo.fill_buffer(records + size_t(k) * 24);
+        types[k] = float(geo.type);
+    }
+    return RT_OK;
+}
+
+// Groups::Geometry::FillBuffer (groups.h:45-64) packs the same position / inverse rotation /
+// scale / colour as the IOW-03 Geometry::FillBuffer (materials.h:48-76): its first 18 floats.
+int rt_pack_iow02(const rt_geom_desc *g, uint32_t n, float *types, float *records) {
+    if (!g || !types || !records) return RT_E_ARG;
+    float r24[24];
+    for (uint32_t k = 0; k < n; k++) {
+        rtamd::IowGeometry geo = rtamd::to_iow(g[k]);
+        geo.fill_buffer(r24);
+        std::memcpy(records + size_t(k) * 18, r24, 18 * sizeof(float));
         types[k] = float(geo.type);
     }
     return RT_OK;
@@ -1296,6 +1314,84 @@ int rt_sample_tables(int spp, float *sunflower, float *fib, int *ring) {
     if (spp < 1) return RT_E_ARG;
     rtamd::sample_tables(spp, sunflower, fib, ring);
     return RT_OK;
+}
+
+int rt_render_iow00(const rt_params *p, float *rgba) {
+    if (!p || p->width <= 0 || p->height <= 0 || !rgba) return RT_E_ARG;
+    int rc = check_device(p->device);
+    if (rc != RT_OK) return rc;
+    const size_t npx = size_t(p->width) * p->height;
+    DevBuf d_rgba;
+    HIP_OK(d_rgba.alloc(npx * 16));
+    HIP_OK(rtk::launch_iow00(p->width, p->height, d_rgba.as<float>(), nullptr));
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(rgba, d_rgba.p, npx * 16, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_render_iow02(const float *types, const float *records, uint32_t n, const rt_camera *cam, const rt_params *p,
+                    int cull_front, int cull_back, float *rgba, rt_stats *st) {
+    if ((n > 0 && (!types || !records)) || !cam || !params_ok(p) || !rgba) return RT_E_ARG;
+    int rc = check_device(p->device);
+    if (rc != RT_OK) return rc;
+    rtk::Frame f = make_frame(cam, p);
+    const size_t npx = size_t(p->width) * p->height;
+    // host tables: the ring schedule (02.glsl:146-157) and pow(0.4, i) (02.glsl:206), double -> float
+    std::vector<int> ring(size_t(p->spp) * 2);
+    rtamd::sample_tables(p->spp, nullptr, nullptr, ring.data());
+    std::vector<float> pw(size_t(std::max(1, p->max_bounces)));
+    for (int i = 0; i < p->max_bounces; i++) pw[size_t(i)] = float(std::pow(double(0.4f), double(i)));
+    DevBuf d_rgba, d_types, d_rec, d_ring, d_pw, d_ctr;
+    HIP_OK(d_rgba.alloc(npx * 16));
+    HIP_OK(hipMemcpy(d_rgba.p, rgba, npx * 16, hipMemcpyHostToDevice));  // untouched pixels keep their value
+    if (n > 0) {
+        HIP_OK(d_types.upload(types, size_t(n) * sizeof(float)));
+        HIP_OK(d_rec.upload(records, size_t(n) * 18 * sizeof(float)));
+    }
+    HIP_OK(d_ring.upload(ring.data(), ring.size() * sizeof(int)));
+    HIP_OK(d_pw.upload(pw.data(), pw.size() * sizeof(float)));
+    HIP_OK(d_ctr.alloc(6 * sizeof(unsigned long long)));
+    HIP_OK(hipMemset(d_ctr.p, 0, 6 * sizeof(unsigned long long)));
+    f.out_rgba = d_rgba.as<float>();
+    f.counters = d_ctr.as<unsigned long long>();
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventRecord(e0, nullptr));
+    hipError_t e = rtk::launch_iow02(f, d_types.as<float>(), d_rec.as<float>(), n, d_ring.as<int>(), d_pw.as<float>(),
+                                     cull_front, cull_back, nullptr);
+    HIP_OK(hipEventRecord(e1, nullptr));
+    HIP_OK(hipEventSynchronize(e1));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    HIP_OK(e);
+    HIP_OK(hipMemcpy(rgba, d_rgba.p, npx * 16, hipMemcpyDeviceToHost));
+    if (st) {
+        unsigned long long c[6];
+        HIP_OK(hipMemcpy(c, d_ctr.p, sizeof(c), hipMemcpyDeviceToHost));
+        std::memset(st, 0, sizeof(*st));
+        st->segments = c[0];
+        st->prim_tests = c[2];
+        st->ms = ms;
+    }
+    return RT_OK;
+}
+
+int rt_render_inw_mf(const float *geom, uint32_t n, const float *nodes, const rt_camera *cam, const float *focus,
+                     int n_focus, const rt_params *p, float *rgba, float *depth, rt_stats *st) {
+    if (!geom || !nodes || n == 0 || !cam || !params_ok(p) || !rgba || !focus || n_focus < 1 || n_focus > 9)
+        return RT_E_ARG;
+    int rc = check_device(p->device);
+    if (rc != RT_OK) return rc;
+    std::unique_ptr<rt_dev_scene> s(new (std::nothrow) rt_dev_scene());
+    if (!s) return RT_E_ARG;
+    rc = make_inw(s.get(), geom, n, 1, nodes, nullptr, 0, nullptr, 0, p->spp);
+    if (rc != RT_OK) return rc;
+    s->n_focus = n_focus;
+    std::memcpy(s->focus, focus, sizeof(float) * size_t(n_focus));
+    return render_blocking(s.get(), cam, p, rgba, depth, st);
 }
 
 }  // extern "C"

@@ -1339,6 +1339,16 @@ __device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame 
     f3 cd = normalize((D * F.screen_dist + cr * srx) + cu * sry);
     float ox = S.sunflower[2 * s] * (F.aperture * 0.5f), oy = S.sunflower[2 * s + 1] * (F.aperture * 0.5f);
     f3 rr = cross(cd, up), ru = cross(rr, cd);
+    if (F.n_focus > 0) {  // MULTIFOCUS lens record (01_BVH...glsl:388-400): stack floats 0..5
+        const float first_limit = F.focus_list[0] * 0.5f;
+        const f3 nd = normalize((cd * first_limit + rr * ox) + ru * oy);
+        const f3 rn = normalize((-rr) * ox - ru * oy);
+        const float mult = 1.0f / dot(cd, nd);
+        K.push(rn.x, c); K.push(rn.y, c); K.push(rn.z, c);
+        K.push(mult, c); K.push(first_limit, c); K.push(0.0f, c);
+        K.push_ray(co, nd, 1.0f, 0.0f, c);
+        return;
+    }
     f3 tip = ((co + cd) + rr * ox) + ru * oy;
     f3 la = normalize((co + cd * F.focus) - tip);
     K.push_ray(tip - la, la, 1.0f, 0.0f, c);
@@ -1401,13 +1411,33 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         f3 co = mk(K.at(b), K.at(b + 1), K.at(b + 2)), cd = mk(K.at(b + 3), K.at(b + 4), K.at(b + 5));
         float contribution = K.at(b + 6), bounced = (float)(int)K.at(b + 7);
         c.seg++;
-        float tlim = kMaxT, extra = 0.0f;
+        // SET LIMIT (01_BVH...glsl:424-428): a MULTIFOCUS primary ray stops at the lens
+        const bool mf0 = !LIGHTS && F.n_focus > 0 && (int)(bounced + 0.1f) == 0;
+        const float tlim0 = mf0 ? K.at(4) : kMaxT;
+        float tlim = tlim0, extra = 0.0f;
         f3 normal = f3{0, 0, 0};
         float fg = inw_traverse<true>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
         const f3 hitpoint = co + cd * tlim;
-        if (!(tlim < kMaxT)) {
+        if (!(tlim < tlim0)) {
+            if (mf0 && (int)(K.at(5) + 0.1f) < F.n_focus) {  // next focal lens, 01_BVH...glsl:506-528
+                const f3 rn = mk(K.at(0), K.at(1), K.at(2));
+                K.at(0) = -K.at(0); K.at(1) = -K.at(1); K.at(2) = -K.at(2);
+                const float mult = K.at(3), dist = K.at(4);
+                const f3 no = co + cd * (mult * dist), nd = reflect(cd, rn);
+                const int lens = (int)(K.at(5) + 0.1f);
+                if (lens < F.n_focus - 1)
+                    K.at(4) = (F.focus_list[lens + 1] - F.focus_list[lens]) * 0.5f +
+                              (F.focus_list[lens] - (lens > 0 ? F.focus_list[lens - 1 > 0 ? lens - 1 : 0] : 0.0f)) *
+                                  0.5f;
+                else K.at(4) = kMaxT - mult * K.at(4);
+                K.at(5) = K.at(5) + 1.0f;
+                K.size = 6;
+                K.push_ray(no, nd, 1.0f, 0.0f, c);
+                break;
+            }
             color = color + background(cd, LIGHTS && S.n_lights > 0) * contribution;
             depth = tlim;
+            if (mf0) K.size = 0;  // 01_BVH...glsl:531-535
             break;
         }
         const float4 m0 = S.cold[2 * (int)fg], m1 = S.cold[2 * (int)fg + 1];
@@ -1423,6 +1453,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
             }
         }
         const float surr = inw_surrounding_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
+        if (mf0) K.size = 0;  // 01_BVH...glsl:544-549: the lens record goes after a primary hit
         if (LIGHTS) {  // 04...glsl:604-665
             uint32_t is_lit = S.n_lights > 0 ? 0u : (uint32_t)is_lit_geom(S, f2u(fg + 0.1f));
             if (is_lit == 0) {

@@ -23,6 +23,10 @@ struct Frame {
     int leaf_batch;           // IOW-03 walk: test postponed leaves once this many lanes hold one
     unsigned *px_rays;        // optional: rays cast per work unit, written when its pixel completes
     int coop_max;             // IOW-03: wave-cooperative closest hits when at most this many lanes trace
+    // INW-01 MULTIFOCUS (01_BVH...glsl:388-404, 505-549; "#if MULTIFOCUS" in the reference):
+    // n_focus = 0 is the single-focus camera the reference builds, 1..9 the lens chain
+    int n_focus;
+    float focus_list[9];
 };
 // lane-occupancy counters (per wave-iteration: 1 and popcount of the participating lanes)
 enum { kDbgOuter = 0, kDbgOuterLanes, kDbgTrav, kDbgTravLanes, kDbgLeaf, kDbgLeafLanes, kDbgSeg, kDbgSegLanes,
@@ -124,6 +128,11 @@ struct Cont {
 };
 
 hipError_t launch_iow01(const Frame &f, hipStream_t s);
+// rt_stages.hip: IOW-00 gradient, IOW-02 groups (records N x 18, ring = sample-table ring
+// schedule, pw[i] = pow(0.4, i) for i < max_bounces)
+hipError_t launch_iow00(int W, int H, float *out, hipStream_t s);
+hipError_t launch_iow02(const Frame &f, const float *types, const float *rec, uint32_t n, const int *ring,
+                        const float *pw, int cull_front, int cull_back, hipStream_t s);
 // Persistent work-queue launches: `counter` (one u32, device) is zeroed on `s` before the
 // kernel; at most `blocks_cap` blocks are launched (they pull pixels until none are left).
 // n_units: pixel units (cont.in == null) or parked lanes to resume (host-known count)

@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "librt_hip.so")
 RT_OK, RT_E_ARG, RT_E_HIP, RT_E_NODEVICE, RT_E_UNSUPPORTED = 0, -1, -2, -3, -4
 
 RT_STAGE_IOW01, RT_STAGE_IOW03, RT_STAGE_INW01, RT_STAGE_INW04 = 1, 3, 11, 14
+RT_STAGE_IOW02 = 2
 RT_IOW_CUBOID, RT_IOW_ELLIPSOID = 1, 2
 RT_INW_ELLIPSOID, RT_INW_CUBOID = 1, 2
 
@@ -80,6 +81,12 @@ SIGNATURES = {
     "rt_render_iow01": (C.c_int, [C.POINTER(RtCamera), _FP, C.POINTER(RtParams), _FP, C.POINTER(RtStats)]),
     "rt_render_iow03": (C.c_int, [_FP, _FP, C.c_uint32, C.POINTER(RtCamera), C.POINTER(RtParams), _FP,
                                   C.POINTER(RtStats)]),
+    "rt_render_iow00": (C.c_int, [C.POINTER(RtParams), _FP]),
+    "rt_pack_iow02": (C.c_int, [C.c_void_p, C.c_uint32, _FP, _FP]),
+    "rt_render_iow02": (C.c_int, [_FP, _FP, C.c_uint32, C.POINTER(RtCamera), C.POINTER(RtParams), C.c_int, C.c_int,
+                                  _FP, C.POINTER(RtStats)]),
+    "rt_render_inw_mf": (C.c_int, [_FP, C.c_uint32, _FP, C.POINTER(RtCamera), _FP, C.c_int, C.POINTER(RtParams), _FP,
+                                   _FP, C.POINTER(RtStats)]),
     "rt_render_inw": (C.c_int, [_FP, C.c_uint32, C.c_int, _FP, _FP, C.c_uint32, C.POINTER(RtCamera),
                                 C.POINTER(RtParams), _FP, _FP, C.POINTER(RtStats)]),
     "rt_render_inw_tex": (C.c_int, [_FP, C.c_uint32, C.c_int, _FP, _FP, C.c_uint32, C.POINTER(RtTexture), C.c_int,
@@ -348,6 +355,46 @@ def render_iow01(camera: RtCamera, sphere, params: RtParams):
     sc = Scene(stage=RT_STAGE_IOW01, desc=None, n=0, camera=camera, params=params)
     rgba, _, st = render(sc, params, sphere=sphere)
     return rgba, st
+
+
+def render_iow00(params: RtParams) -> np.ndarray:
+    """IOW-00 (In-One-Weekend/base.cpp:7-28): the UV gradient of the base stage."""
+    rgba = np.zeros((params.height, params.width, 4), np.float32)
+    check(load().rt_render_iow00(C.byref(params), fptr(rgba)), "rt_render_iow00")
+    return rgba
+
+
+def pack_iow02(desc, n: int) -> tuple[np.ndarray, np.ndarray]:
+    """Groups::Geometry::FillBuffer (groups.h:45-64): types[N], records[N, 18]."""
+    types = np.zeros(n, np.float32)
+    rec = np.zeros((n, 18), np.float32)
+    check(load().rt_pack_iow02(desc, n, fptr(types), fptr(rec)), "rt_pack_iow02")
+    return types, rec
+
+
+def render_iow02(types, records, camera: RtCamera, params: RtParams, cull_front: int = 0, cull_back: int = 1):
+    """IOW-02 groups stage (02_Groups/computeShaderSrc.glsl); defaults cull the back side
+    (groups.h:91-92)."""
+    types = np.ascontiguousarray(types, np.float32)
+    records = np.ascontiguousarray(records, np.float32).reshape(-1, 18)
+    rgba = np.zeros((params.height, params.width, 4), np.float32)
+    st = RtStats()
+    check(load().rt_render_iow02(fptr(types), fptr(records), len(types), C.byref(camera), C.byref(params),
+                                 int(cull_front), int(cull_back), fptr(rgba), C.byref(st)), "rt_render_iow02")
+    return rgba, st.as_dict()
+
+
+def render_inw_mf(sc: "Scene", focus, params: RtParams | None = None):
+    """INW-01 with the shader's MULTIFOCUS branch (01_BVH...glsl:388-404, 505-549), focus distances
+    `focus` (1..9)."""
+    p = params or sc.params
+    f = np.ascontiguousarray(focus, np.float32)
+    rgba = np.zeros((p.height, p.width, 4), np.float32)
+    depth = np.zeros((p.height, p.width), np.float32)
+    st = RtStats()
+    check(load().rt_render_inw_mf(fptr(sc.geom), sc.n, fptr(sc.nodes), C.byref(sc.camera), fptr(f), len(f),
+                                  C.byref(p), fptr(rgba), fptr(depth), C.byref(st)), "rt_render_inw_mf")
+    return rgba, depth, st.as_dict()
 
 
 def iow01_defaults(width: int = 400, height: int = 225) -> tuple[RtCamera, np.ndarray, RtParams]:

@@ -15,12 +15,18 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "raytracing-tests_amd"), os.path.dirname(HERE)]
 
 import cases  # noqa: E402
+import stages  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 
 def main():
-    for name in cases.GOLDEN_CASES:
-        if name == "iow01_c1":
+    only = set(sys.argv[1:])  # optional: regenerate just these cases
+    for name in cases.GOLDEN_CASES + stages.GOLDEN_STAGE_CASES:
+        if only and name not in only:
+            continue
+        if name in stages.GOLDEN_STAGE_CASES:
+            rgba, depth, st = stages.render_oracle(name)
+        elif name == "iow01_c1":
             cam, sph, p = cases.iow01_c1()
             rgba, st = O.render_iow01(cam, sph, p)
             depth = None
