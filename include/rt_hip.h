@@ -261,6 +261,13 @@ int rt_debug_rounds(rt_dev_scene *s, uint32_t *out, int cap);
  * out[0] = max, out[1] = samples, out[2+b] = samples with 2^b <= rays < 2^(b+1),
  * out[34+b] = rays in those samples.  66 entries. */
 int rt_debug_spec_hist(rt_dev_scene *s, uint64_t *out);
+/* Per pixel unit of the last sample-parallel IOW-03 render, 4 x u32: sample-0 rays, the most
+ * rays of one sample, that sample's index, and (column 3 of row r) the pixel at rank r of the
+ * heaviest-first order.  Returns the number of units (<= cap_units) or an error. */
+int rt_debug_spec_pixels(rt_dev_scene *s, uint32_t *out, uint32_t cap_units);
+/* Same 66 x u64 layout as rt_debug_spec_hist, over the samples of group 0's last re-execution
+ * list (their final executions). */
+int rt_debug_spec_list_hist(rt_dev_scene *s, uint64_t *out);
 /* Main render kernel of the scene's last render and how many times it was launched (the
  * bench's per-launch roofline figures divide by this).  Returns the count; writes the name. */
 int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap);

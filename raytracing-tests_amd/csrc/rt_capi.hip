@@ -129,6 +129,7 @@ struct rt_dev_scene {
     DevBuf sp_col, sp_fin, sp_ctr, sp_assume, sp_list, sp_fb, sp_counts;
     DevBuf sp_keys, sp_keys2, sp_list2, sp_temp;  // longest-first ordering of the re-execution list
     DevBuf sp_pstate;  // asynchronous windows: per-pixel frontier state
+    DevBuf sp_front;   // checkpoint rounds: per-pixel frontier (uint4)
     size_t sp_temp_bytes = 0;
     // launches of the render's main kernel in the last render (rt_debug_launches)
     int last_launches = 0;
@@ -347,6 +348,8 @@ int ensure_cont(rt_dev_scene *s) {
     return RT_OK;
 }
 
+constexpr int kCountSlots = 160;  // round counts per group lane, 64 B apart
+
 // group lanes of the sample-parallel pipeline; temp_bytes = sort scratch each lane needs
 int ensure_lanes(rt_dev_scene *s, int groups, size_t temp_bytes) {
     if (!s->ev_start) HIP_OK(hipEventCreateWithFlags(&s->ev_start, hipEventDisableTiming));
@@ -356,8 +359,9 @@ int ensure_lanes(rt_dev_scene *s, int groups, size_t temp_bytes) {
         HIP_OK(hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking));
         HIP_OK(hipEventCreateWithFlags(&L->done, hipEventDisableTiming));
         HIP_OK(L->counter.alloc(64));
-        for (auto &b : L->cont) HIP_OK(b.alloc(slots * rtk::kContSlots * sizeof(float4)));
-        HIP_OK(L->cont_count.alloc(64 * 16));
+        // 2x: parked lanes (<= resident lanes) plus restarts queued between checkpoint rounds
+        for (auto &b : L->cont) HIP_OK(b.alloc(2 * slots * rtk::kContSlots * sizeof(float4)));
+        HIP_OK(L->cont_count.alloc(kCountSlots * 64));
         s->lanes.push_back(std::move(L));
     }
     for (int g = 0; g < groups; g++) {
@@ -382,7 +386,7 @@ bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || bytes > free_b / 2) return false;
     for (DevBuf *b : {&s->sp_col, &s->sp_fin, &s->sp_ctr, &s->sp_assume, &s->sp_list, &s->sp_fb, &s->sp_counts,
-                      &s->sp_keys, &s->sp_keys2, &s->sp_list2, &s->sp_temp, &s->sp_pstate}) {
+                      &s->sp_keys, &s->sp_keys2, &s->sp_list2, &s->sp_temp, &s->sp_pstate, &s->sp_front}) {
         b->~DevBuf();
         new (b) DevBuf();
     }
@@ -392,6 +396,7 @@ bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
         s->sp_counts.alloc(64 * 64) != hipSuccess || s->sp_keys.alloc(n * 4) != hipSuccess ||
         s->sp_keys2.alloc(n * 4) != hipSuccess || s->sp_list2.alloc(n * 4) != hipSuccess ||
         s->sp_pstate.alloc(size_t(P) * 3 * sizeof(uint4)) != hipSuccess ||
+        s->sp_front.alloc(size_t(P) * sizeof(uint4)) != hipSuccess ||
         s->sp_temp.alloc(s->sp_temp_bytes = rtk::sort_pairs_temp_bytes(n, 24)) != hipSuccess) {
         s->spec_cap = s->spec_units = 0;
         return false;
@@ -537,7 +542,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     unsigned *sc = s->sp_counts.as<unsigned>();  // group g: [32g] list count, [32g+16] fallback count
     const rtk::SpecRecs R{s->sp_col.as<float4>(), s->sp_fin.as<float4>(), s->sp_ctr.as<uint4>(),
                           s->sp_assume.as<float4>(), P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(),
-                          sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), ++s->epoch};
+                          sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), ++s->epoch,
+                          s->sp_front.as<uint4>()};
     rtk::IowScene scene{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
                         s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link,
                                  s->obox.as<float4>(), s->n_wide};
@@ -581,8 +587,53 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             return rtk::launch_iow03_spec(f, scene, RR, mode, ct, n, q.counter, cap_s, q.st);
         };
     };
+    // Checkpoint rounds (RT_SPEC_ROUNDS = k > 0): the speculative pass over samples 1.. runs as k
+    // launches, each taking the lanes the previous one parked plus the next slice of fresh units
+    // and parking every lane once its queue drains; between launches the pixel frontiers advance
+    // and mispredicted samples at a frontier are re-run at once (k_iow03_frontier,
+    // k_iow03_fixf).  The tail then runs as before (compaction rounds).
+    const int ckpt = S > 1 ? std::max(0, std::min(kCountSlots - 16, env_int("RT_SPEC_ROUNDS", 24))) : 0;
+    auto ckpt_pass = [&](const Lane &q, const rtk::SpecRecs &RG, uint32_t n_fresh) {
+        const uint32_t slots = uint32_t(s->blocks_cap) * rtk::kBlock, cap_cont = 2 * slots;
+        int b = 0;  // continuation buffer written last
+        for (int r = 0; r < ckpt && e == hipSuccess; r++) {
+            rtk::Cont ct{};
+            if (r > 0) { ct.in = q.cont[(r - 1) & 1].as<float4>(); ct.in_count = q.cnt + 16 * (r - 1); }
+            ct.out = q.cont[r & 1].as<float4>();
+            ct.out_count = q.cnt + 16 * r;
+            ct.mixed = 1;
+            ct.park_below = 65;  // park every busy lane once the queue drains
+            ct.fresh_lo = uint32_t(uint64_t(n_fresh) * r / ckpt);
+            ct.fresh_hi = uint32_t(uint64_t(n_fresh) * (r + 1) / ckpt);
+            if (r == ckpt - 1) ct.park_below = 0;  // the last round compacts as the tail rounds do
+            ct.park_min = r == ckpt - 1 ? uint32_t(std::max(0, env_int("RT_PARK_MIN", cap_s * rtk::kBlock / 8))) : 0u;
+            e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), q.st);
+            if (e == hipSuccess) e = rtk::launch_iow03_spec(f, scene, RG, rtk::kSpecRest, ct, uint32_t(cap_s) * rtk::kBlock,
+                                                            q.counter, cap_s, q.st);
+            if (e == hipSuccess) e = rtk::launch_iow03_frontier(f, RG, ct.out, ct.out_count, cap_cont, q.st);
+            if (e == hipSuccess) e = rtk::launch_iow03_fixf(f, RG, ct.out, ct.out_count, int(cap_cont), q.st);
+            b = r & 1;
+        }
+        // tail: resume rounds with compaction, the last one running to completion
+        const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap_s * rtk::kBlock / 8)));
+        for (int t = 0; t <= rounds && e == hipSuccess; t++) {
+            const int r = ckpt + t;
+            rtk::Cont ct{};
+            ct.in = q.cont[b].as<float4>();
+            ct.in_count = q.cnt + 16 * (r - 1);
+            if (t < rounds) {
+                ct.out = q.cont[b ^ 1].as<float4>();
+                ct.out_count = q.cnt + 16 * r;
+                ct.park_min = park_min;
+                e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), q.st);
+            }
+            if (e == hipSuccess) e = rtk::launch_iow03_spec(f, scene, RG, rtk::kSpecRest, ct, uint32_t(cap_s) * rtk::kBlock,
+                                                            q.counter, cap_s, q.st);
+            b ^= 1;
+        }
+    };
     s->last_kernel = lds ? "k_iow03sL" : "k_iow03s";
-    s->last_launches = (1 + rounds) * (1 + groups * ((S > 1 ? 1 : 0) + iters));
+    s->last_launches = (1 + rounds) * (1 + groups * ((S > 1 ? 1 : 0) + iters)) + (ckpt > 0 ? groups * ckpt : 0);
     // (1) on the caller's stream: sample 0 of every pixel (exact), the guesses for the other
     // samples, and the pixel order (heaviest sample 0 first)
     const Lane L0{st, s->counter.as<unsigned>(), s->cont, s->cont_count.as<unsigned>()};
@@ -635,7 +686,10 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         RG.fb_count = sc + 32 * g + 16;
         const size_t nmax = size_t(cnt_g) * S;  // list bound for this group
         e = hipStreamWaitEvent(L.st, s->ev_start, 0);
-        if (S > 1 && e == hipSuccess) pass(L, spec(RG, rtk::kSpecRest), cnt_g * (S - 1), cap_s, true);
+        if (S > 1 && e == hipSuccess) {
+            if (ckpt > 0) ckpt_pass(L, RG, cnt_g * (S - 1));
+            else pass(L, spec(RG, rtk::kSpecRest), cnt_g * (S - 1), cap_s, true);
+        }
         for (int it = 0; it < iters && e == hipSuccess; it++) {
             e = hipMemsetAsync(RG.list_count, 0, sizeof(unsigned), L.st);
             if (e == hipSuccess) e = rtk::launch_iow03_resolve(f, RG, false, nullptr, L.st);
@@ -886,6 +940,30 @@ int rt_debug_spec_hist(rt_dev_scene *s, uint64_t *out) {
     HIP_OK(rtk::spec_hist(s->sp_ctr.as<uint4>(), s->spec_cap, d.as<unsigned long long>(), nullptr));
     HIP_OK(hipMemcpy(out, d.p, 66 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return RT_OK;
+}
+
+int rt_debug_spec_list_hist(rt_dev_scene *s, uint64_t *out) {
+    if (!s || !out) return RT_E_ARG;
+    std::memset(out, 0, 66 * sizeof(uint64_t));
+    if (!s->spec_cap) return RT_OK;
+    DevBuf d;
+    HIP_OK(d.alloc(66 * sizeof(uint64_t)));
+    HIP_OK(hipMemset(d.p, 0, 66 * sizeof(uint64_t)));
+    HIP_OK(rtk::spec_list_hist(s->sp_ctr.as<uint4>(), s->sp_list.as<uint32_t>(), s->sp_counts.as<unsigned>(),
+                               d.as<unsigned long long>(), nullptr));
+    HIP_OK(hipMemcpy(out, d.p, 66 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_debug_spec_pixels(rt_dev_scene *s, uint32_t *out, uint32_t cap_units) {
+    if (!s || !out) return RT_E_ARG;
+    if (!s->spec_cap || !s->spec_units || s->spec_units > cap_units) return RT_E_ARG;
+    const uint32_t P = s->spec_units, S = uint32_t(s->spec_cap / P);
+    DevBuf d;
+    HIP_OK(d.alloc(size_t(P) * 16));
+    HIP_OK(rtk::spec_pixels(s->sp_ctr.as<uint4>(), P, S, s->ws_order.as<uint32_t>(), d.as<uint32_t>(), nullptr));
+    HIP_OK(hipMemcpy(out, d.p, size_t(P) * 16, hipMemcpyDeviceToHost));
+    return int(P);
 }
 
 int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {

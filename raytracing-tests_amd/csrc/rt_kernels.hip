@@ -932,9 +932,16 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         if ((threadIdx.x & 63) < kDbgSlots) c.wdbg[threadIdx.x & 63] = 0;
     }
     Stack K{lds + sb * kFl * kBlock + tl, lds_b + (NARROW ? sb * kIowStack * kBlock + tl : 0), 0};
-    const uint32_t total = ct.in ? *ct.in_count
-                         : (mode == kSpecList ? *R.list_count : (mode == kSpecFirst ? R.P : R.order_n * (R.S - 1)));
+    // units: the parked lanes of ct.in first, then fresh units of the mode ([fresh_lo, fresh_hi)
+    // in a mixed launch; all of them in a first launch; none in a plain resume launch)
+    const uint32_t nin = ct.in ? *ct.in_count : 0u;
+    const uint32_t f_lo = ct.mixed ? ct.fresh_lo : 0u;
+    const uint32_t f_n = ct.mixed ? ct.fresh_hi - ct.fresh_lo
+                       : (ct.in ? 0u : (mode == kSpecList ? *R.list_count
+                                                          : (mode == kSpecFirst ? R.P : R.order_n * (R.S - 1))));
+    const uint32_t total = nin + f_n;
     const bool may_park = ct.out != nullptr && total >= ct.park_min;
+    const int park_below = ct.park_below ? ct.park_below : kParkBelow;
     const int W = f.W, H = f.H, spp = f.spp;
     int grid = 1;
     while (grid * grid < spp) grid++;
@@ -972,10 +979,10 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         const uint32_t q = fetch_unit(counter, live && !busy);
         if (live && !busy) {
             if (q >= total) live = false;
-            else if (ct.in && ct.in[(size_t)q * kContSlots + 12].y != 0.0f) {  // doomed while parked: restart exact
+            else if (q < nin && ct.in[(size_t)q * kContSlots + 12].y != 0.0f) {  // doomed while parked: restart exact
                 u = __float_as_uint(ct.in[(size_t)q * kContSlots].x);
                 begin(u, R.assume[u]);
-            } else if (ct.in) {  // resume a parked lane
+            } else if (q < nin) {  // resume a parked lane
                 const float4 *p = ct.in + (size_t)q * kContSlots;
                 const float4 m = p[0], a = p[1], b = p[2];
                 u = __float_as_uint(m.x); skip = __float_as_int(m.y); K.size = __float_as_int(m.z);
@@ -991,14 +998,15 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
             } else {
                 // kSpecFirst: sample 0 of every pixel; kSpecRest: samples 1.. pixel-major, pixels
                 // in R.order (heaviest sample 0 first); kSpecList: the re-execution list
-                u = mode == kSpecList ? R.list[q]
-                    : (mode == kSpecFirst ? q : (1u + q % (R.S - 1)) * R.P + R.order[R.order_base + q / (R.S - 1)]);
+                const uint32_t qf = f_lo + (q - nin);
+                u = mode == kSpecList ? R.list[qf]
+                    : (mode == kSpecFirst ? qf : (1u + qf % (R.S - 1)) * R.P + R.order[R.order_base + qf / (R.S - 1)]);
                 if (unit_pixel(f, u % R.P).in_image)
                     begin(u, mode == kSpecFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : R.assume[u]);
             }
         }
         if (__ballot(live) == 0) break;
-        if (may_park && __ballot(!live) != 0 && __popcll(__ballot(busy)) < kParkBelow) {
+        if (may_park && __ballot(!live) != 0 && __popcll(__ballot(busy)) < park_below) {
             const uint32_t slot = park_slot(ct.out_count, busy);
             if (busy) {
                 float4 *p = ct.out + (size_t)slot * kContSlots;
@@ -1108,7 +1116,88 @@ __global__ __launch_bounds__(kBlock) void k_iow03_prep(Frame f, SpecRecs R, unsi
     const float4 e0 = make_float4((wm & 2u) ? fn.x : 0.0f, (wm & 4u) ? fn.y : 0.0f, (wm & 8u) ? fn.z : 0.0f, 0.0f);
     const float4 e1 = make_float4((wm & 2u) ? fn.x : prior, (wm & 4u) ? fn.y : prior, (wm & 8u) ? fn.z : prior, 0.0f);
     for (uint32_t s = 1; s < R.S; s++) R.assume[(size_t)s * R.P + pu] = s >= prior_from ? e1 : e0;
+    if (R.front)  // sample 0 is exact: the frontier starts at sample 1 with its final entries
+        R.front[pu] = make_uint4(1u, __float_as_uint(e0.x), __float_as_uint(e0.y), __float_as_uint(e0.z));
     key[pu] = R.ctr[pu].x;
+}
+
+// ---------------------------------------------------------------- checkpoint rounds
+// Between the rounds of the speculative pass (kernel boundaries, so every finished record is
+// visible), each pixel's frontier advances over its finished samples in sample order while
+// their assumptions match the exact state E.  The first finished sample whose assumption was
+// wrong gets E and is queued at once for an exact re-run in the next round (its record is
+// marked unfinished until then), so a mispredicted sample -- long ones especially -- is re-run
+// while the pass still has other work, not in a re-execution pass after it.  Samples behind the
+// frontier keep speculating; the resolve after the pass checks everything again.
+__global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, float4 *cont, unsigned *count,
+                                                           uint32_t cap) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = R.order_n ? R.order_n : R.P;
+    if (i >= n) return;  // no cross-lane work in this kernel
+    const uint32_t pu = R.order_n ? R.order[R.order_base + i] : i;
+    if (!unit_pixel(f, pu).in_image) return;
+    uint4 st = R.front[pu];
+    if (st.x >= R.S) return;
+    const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
+    uint32_t s = st.x;
+    for (; s < R.S; s++) {
+        const size_t u = (size_t)s * R.P + pu;
+        const unsigned fl = __float_as_uint(R.col[u].w);
+        if ((fl & 0xffff0100u) != done_tag) break;  // still running (or queued)
+        const float4 a = R.assume[u];
+        const unsigned rm = fl & 15u, wm = (fl >> 4) & 15u;
+        if (((rm & 2u) && __float_as_uint(a.x) != st.y) || ((rm & 4u) && __float_as_uint(a.y) != st.z) ||
+            ((rm & 8u) && __float_as_uint(a.z) != st.w)) {
+            const uint32_t slot = atomicAdd(count, 1u);
+            if (slot >= cap) atomicSub(count, 1u);  // full: leave it to the resolve after the pass
+            else {
+                R.assume[u] = make_float4(__uint_as_float(st.y), __uint_as_float(st.z), __uint_as_float(st.w), 0.0f);
+                R.col[u].w = 0.0f;  // unfinished until the re-run records it
+                float4 *p = cont + (size_t)slot * kContSlots;
+                p[0] = make_float4(__uint_as_float((uint32_t)u), 0.0f, 0.0f, 0.0f);
+                p[12] = make_float4(0.0f, 1.0f, 0.0f, 0.0f);  // restart with the (now exact) assumption
+            }
+            break;
+        }
+        const float4 fn = R.fin[u];
+        if (wm & 2u) st.y = __float_as_uint(fn.x);
+        if (wm & 4u) st.z = __float_as_uint(fn.y);
+        if (wm & 8u) st.w = __float_as_uint(fn.z);
+    }
+    st.x = s;
+    R.front[pu] = st;
+}
+// Parked samples at their pixel's frontier: the exact incoming state E is known.  As in
+// k_iow03_fix: entries the sample neither read nor wrote get E; if an entry it read differs
+// from E it restarts with E.  Either way its assumption becomes exact.
+__global__ __launch_bounds__(kBlock) void k_iow03_fixf(Frame f, SpecRecs R, float4 *cont, const unsigned *count) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= *count) return;  // no cross-lane work in this kernel
+    float4 *p = cont + (size_t)i * kContSlots;
+    if (p[12].y != 0.0f) return;  // a restart already
+    const uint32_t u = __float_as_uint(p[0].x);
+    const uint32_t pu = u % R.P, s = u / R.P;
+    const uint4 st = R.front[pu];
+    if (st.x != s) return;
+    const unsigned E[3] = {st.y, st.z, st.w};
+    const unsigned masks = __float_as_uint(p[0].w), wm = masks & 15u, rm = masks >> 4;
+    float4 a = R.assume[u];
+    float *av = &a.x;
+    bool doomed = false;
+    for (int k = 1; k <= 3; k++)
+        if (((rm >> k) & 1u) && __float_as_uint(av[k - 1]) != E[k - 1]) doomed = true;
+    if (doomed) {
+        R.assume[u] = make_float4(__uint_as_float(E[0]), __uint_as_float(E[1]), __uint_as_float(E[2]), 0.0f);
+        p[12].y = 1.0f;
+        return;
+    }
+    float *fl = reinterpret_cast<float *>(p + 3);  // parked stack, [entry*9 + field], RI = field 7
+    for (int k = 1; k <= 3; k++)
+        if (!((wm >> k) & 1u) && !((rm >> k) & 1u)) {
+            fl[k * 9 + 7] = __uint_as_float(E[k - 1]);
+            av[k - 1] = __uint_as_float(E[k - 1]);
+        }
+    R.assume[u] = a;
 }
 
 // Replay of each pixel's samples in order (one lane per pixel unit; records are [s][pu], so
@@ -2015,6 +2104,44 @@ __global__ void k_spec_hist(const uint4 *ctr, size_t n, unsigned long long *out)
         atomicAdd(out + 1, 1ull);
     }
 }
+// diagnostics: per pixel unit (sample-0 rays, max rays of a sample, that sample, rank in `order`)
+__global__ void k_spec_pixels(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *order, uint32_t *out) {
+    const uint32_t pu = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pu >= P) return;  // no cross-lane work in this kernel
+    uint32_t mx = 0, arg = 0;
+    for (uint32_t s = 0; s < S; s++) {
+        const uint32_t v = ctr[(size_t)s * P + pu].x;
+        if (v > mx) { mx = v; arg = s; }
+    }
+    out[4 * (size_t)pu] = ctr[pu].x;
+    out[4 * (size_t)pu + 1] = mx;
+    out[4 * (size_t)pu + 2] = arg;
+    out[4 * (size_t)order[pu] + 3] = pu;  // out[.3] of row r = the pixel at order rank r
+}
+hipError_t spec_pixels(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *order, uint32_t *d_out,
+                       hipStream_t s) {
+    hipLaunchKernelGGL(k_spec_pixels, dim3((P + 255) / 256), dim3(256), 0, s, ctr, P, S, order, d_out);
+    return hipGetLastError();
+}
+// diagnostics: log2 histogram of the rays of the samples on the (first) re-execution list
+__global__ void k_spec_list_hist(const uint4 *ctr, const uint32_t *list, const unsigned *count,
+                                 unsigned long long *out) {
+    const unsigned n = *count;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const unsigned v = ctr[list[i]].x;
+        if (v == 0) continue;
+        const int b = 31 - __clz(v);
+        atomicAdd(out + 2 + b, 1ull);
+        atomicAdd(out + 34 + b, (unsigned long long)v);
+        atomicMax(out, (unsigned long long)v);
+        atomicAdd(out + 1, 1ull);
+    }
+}
+hipError_t spec_list_hist(const uint4 *ctr, const uint32_t *list, const unsigned *count, unsigned long long *d_out,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(k_spec_list_hist, dim3(1024), dim3(256), 0, s, ctr, list, count, d_out);
+    return hipGetLastError();
+}
 hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipStream_t s) {
     hipLaunchKernelGGL(k_spec_hist, dim3(2048), dim3(256), 0, s, ctr, n, d_out);
     return hipGetLastError();
@@ -2044,6 +2171,18 @@ hipError_t launch_iow03_fix(const Frame &f, const SpecRecs &R, float4 *cont, con
 hipError_t launch_iow03_keys0(const Frame &f, const SpecRecs &R, unsigned *key, hipStream_t s) {
     const unsigned blocks = (R.P + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_iow03_keys0, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, key);
+    return hipGetLastError();
+}
+hipError_t launch_iow03_frontier(const Frame &f, const SpecRecs &R, float4 *cont, unsigned *count, uint32_t cap,
+                                 hipStream_t s) {
+    const uint32_t n = R.order_n ? R.order_n : R.P;
+    hipLaunchKernelGGL(k_iow03_frontier, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, f, R, cont, count, cap);
+    return hipGetLastError();
+}
+hipError_t launch_iow03_fixf(const Frame &f, const SpecRecs &R, float4 *cont, const unsigned *count, int max_lanes,
+                             hipStream_t s) {
+    const unsigned blocks = (unsigned)((max_lanes + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_iow03_fixf, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, cont, count);
     return hipGetLastError();
 }
 hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,

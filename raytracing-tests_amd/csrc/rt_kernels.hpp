@@ -108,6 +108,7 @@ struct SpecRecs {
     uint32_t order_base, order_n;  // this group's slice of `order` (order_n == 0: all P units)
     uint4 *pstate;     // asynchronous windows: per pixel unit 3 x uint4 of frontier state
     uint32_t epoch;    // frame tag: finished records carry it in their flags
+    uint4 *front;      // checkpoint rounds: per pixel unit (first unvalidated sample, exact RI bits of entries 1..3)
 };
 enum { kSpecFirst = 0, kSpecRest = 1, kSpecList = 2 };
 
@@ -125,6 +126,11 @@ struct Cont {
     float4 *out;
     unsigned *out_count;
     uint32_t park_min;
+    // sample-parallel checkpoint rounds: a launch takes the parked lanes of `in` first, then the
+    // fresh units [fresh_lo, fresh_hi) of its mode (mixed != 0); park_below = 65 parks every
+    // busy lane once the queue drains (0 = kParkBelow, the tail-compaction rule)
+    int mixed, park_below;
+    uint32_t fresh_lo, fresh_hi;
 };
 
 hipError_t launch_iow01(const Frame &f, hipStream_t s);
@@ -162,6 +168,10 @@ size_t remap_workspace_bytes(int W, int H);
 hipError_t texture_remap(const uint8_t *d_in, int W, int H, int C, int load_as, uint8_t *d_out, void *d_ws,
                          hipStream_t s);
 hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipStream_t s);  // diagnostics
+hipError_t spec_list_hist(const uint4 *ctr, const uint32_t *list, const unsigned *count, unsigned long long *d_out,
+                          hipStream_t s);  // diagnostics
+hipError_t spec_pixels(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *order, uint32_t *d_out,
+                       hipStream_t s);  // diagnostics
 // asynchronous-window IOW-03 over samples 1.. (after the kSpecFirst pass and the pixel order):
 // every pixel's samples, validation and re-runs inside one persistent launch; writes the pixels
 hipError_t launch_iow03_async(const Frame &f, const IowScene &sc, const SpecRecs &R, unsigned *counter,
@@ -173,6 +183,14 @@ hipError_t launch_iow03_fix(const Frame &f, const SpecRecs &R, float4 *cont, con
 // sort keys = sample 0's ray count per pixel unit (0 for tile padding)
 hipError_t launch_iow03_keys0(const Frame &f, const SpecRecs &R, unsigned *key, hipStream_t s);
 // after the kSpecFirst pass: assumptions for samples 1.. and the per-pixel ordering keys
+// checkpoint rounds: advance each pixel's frontier over finished, valid samples and
+// queue a finished sample at the frontier whose assumption was wrong for an exact re-run
+// (appended to cont as a restart, at most cap entries in all); then make parked samples at the
+// frontier exact (patch unread entries, or restart)
+hipError_t launch_iow03_frontier(const Frame &f, const SpecRecs &R, float4 *cont, unsigned *count, uint32_t cap,
+                                 hipStream_t s);
+hipError_t launch_iow03_fixf(const Frame &f, const SpecRecs &R, float4 *cont, const unsigned *count, int max_lanes,
+                             hipStream_t s);
 hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,
                              hipStream_t s);
 // replay each pixel's samples: re-queue wrong assumptions; final: write clean pixels, hand

@@ -11,6 +11,8 @@
 - RT_SPEC_GROUPS=2/7: pixel groups on separate streams;
 - RT_IOW_ASYNC=1: asynchronous windows (per-wave frontiers) instead of global resolve passes;
 - RT_SPEC_FIX=1: mid-pass correction of parked samples (patch / restart with the exact state);
+- RT_SPEC_ROUNDS=k: the speculative pass as k checkpoint rounds (default 24; 0 = one launch)
+  with pixel frontiers and immediate exact re-runs of mispredicted samples;
 - RT_IOW_LDS=0: the BVH read from global memory instead of staged in LDS (768-lane blocks);
 - RT_COOP=0/64: no wave-cooperative closest hits / every closest hit wave-cooperative (default:
   waves with at most 4 tracing lanes);
@@ -52,7 +54,8 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     env = dict(os.environ)
     for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS", "RT_IOW_SPEC", "RT_SPEC_ITERS",
               "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_SPEC_GROUPS", "RT_IOW_ASYNC", "RT_SPEC_FIX",
-              "RT_SPEC_VALIDATE", "RT_SPEC_PRIOR_FROM", "RT_COOP", "RT_IOW_LDS"):
+              "RT_SPEC_VALIDATE", "RT_SPEC_PRIOR_FROM", "RT_COOP", "RT_IOW_LDS",
+              "RT_SPEC_ROUNDS"):
         env.pop(k, None)
     env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out, preset=scene[0], seed=scene[1], n_hint=scene[2])
@@ -78,6 +81,10 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     ({"RT_SPEC_GROUPS": "2"}, 300, 200, 12),
     ({"RT_COOP": "0"}, 600, 400, 8),
     ({"RT_IOW_LDS": "0"}, 600, 400, 8),
+    ({"RT_SPEC_ROUNDS": "0"}, 600, 400, 12),
+    ({"RT_SPEC_ROUNDS": "8"}, 600, 400, 12),
+    ({"RT_SPEC_ROUNDS": "24", "RT_SPEC_PRIOR_FROM": "1"}, 300, 200, 16),
+    ({"RT_SPEC_ROUNDS": "5", "RT_SPEC_GROUPS": "3"}, 300, 200, 9),
     ({"RT_IOW_LDS": "0", "RT_IOW_SPEC": "0"}, 300, 200, 8),
     ({"RT_COOP": "64"}, 300, 200, 4),
     ({"RT_COOP": "64", "RT_IOW_SPEC": "0"}, 300, 200, 4),
