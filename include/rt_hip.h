@@ -268,9 +268,19 @@ int rt_debug_spec_pixels(rt_dev_scene *s, uint32_t *out, uint32_t cap_units);
 /* Same 66 x u64 layout as rt_debug_spec_hist, over the samples of group 0's last re-execution
  * list (their final executions). */
 int rt_debug_spec_list_hist(rt_dev_scene *s, uint64_t *out);
+/* With RT_DEBUG_FIRST_STALE=1 (which repurposes the stack-drop counter): out[b] / out[16+b] =
+ * samples / rays of the re-execution list whose first stale stack read came in the b-th 16th
+ * of their segments. */
+int rt_debug_spec_list_stale(rt_dev_scene *s, uint64_t *out);
 /* Main render kernel of the scene's last render and how many times it was launched (the
  * bench's per-launch roofline figures divide by this).  Returns the count; writes the name. */
 int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap);
+/* Kernel timing (diagnostics / bench): with rt_debug_time_kernels(1), every launch of the main
+ * sample-parallel IOW-03 kernel (rt_debug_launches' name) is bracketed by HIP events on its
+ * stream; rt_debug_kernel_time returns the summed durations and the launch count of the
+ * scene's last render (waits for it). */
+int rt_debug_time_kernels(int on);
+int rt_debug_kernel_time(rt_dev_scene *s, double *ms_total, int *launches);
 
 #ifdef __cplusplus
 }

@@ -94,6 +94,8 @@ rtk::Frame make_frame(const rt_camera *cam, const rt_params *p) {
     // (0 = off; every mode is bit-identical, tests/test_gpu_bvh_exact.py)
     const char *co = std::getenv("RT_COOP");
     f.coop_max = (co && *co) ? std::max(0, std::atoi(co)) : 4;
+    const char *fs = std::getenv("RT_DEBUG_FIRST_STALE");
+    f.dbg_first_stale = (fs && fs[0] == '1') ? 1 : 0;
     return f;
 }
 
@@ -130,6 +132,7 @@ struct rt_dev_scene {
     DevBuf sp_keys, sp_keys2, sp_list2, sp_temp;  // longest-first ordering of the re-execution list
     DevBuf sp_pstate;  // asynchronous windows: per-pixel frontier state
     DevBuf sp_front;   // checkpoint rounds: per-pixel frontier (uint4)
+    DevBuf sp_sorder, sp_fcost;  // heavy-first enumeration: sample indices by cost, their costs
     size_t sp_temp_bytes = 0;
     // launches of the render's main kernel in the last render (rt_debug_launches)
     int last_launches = 0;
@@ -148,6 +151,9 @@ struct rt_dev_scene {
     };
     std::vector<std::unique_ptr<GroupLane>> lanes;
     hipEvent_t ev_start = nullptr;
+    // rt_debug_time_kernels: HIP events around every launch of the main sample-parallel kernel
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> kt_ev;
+    size_t kt_used = 0;
     unsigned epoch = 0;  // frame tag of the asynchronous-window records
     ~rt_dev_scene() {
         if (ev_start) (void)hipEventDestroy(ev_start);
@@ -386,7 +392,8 @@ bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || bytes > free_b / 2) return false;
     for (DevBuf *b : {&s->sp_col, &s->sp_fin, &s->sp_ctr, &s->sp_assume, &s->sp_list, &s->sp_fb, &s->sp_counts,
-                      &s->sp_keys, &s->sp_keys2, &s->sp_list2, &s->sp_temp, &s->sp_pstate, &s->sp_front}) {
+                      &s->sp_keys, &s->sp_keys2, &s->sp_list2, &s->sp_temp, &s->sp_pstate, &s->sp_front,
+                      &s->sp_sorder, &s->sp_fcost}) {
         b->~DevBuf();
         new (b) DevBuf();
     }
@@ -397,6 +404,8 @@ bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
         s->sp_keys2.alloc(n * 4) != hipSuccess || s->sp_list2.alloc(n * 4) != hipSuccess ||
         s->sp_pstate.alloc(size_t(P) * 3 * sizeof(uint4)) != hipSuccess ||
         s->sp_front.alloc(size_t(P) * sizeof(uint4)) != hipSuccess ||
+        s->sp_sorder.alloc(size_t(S) * sizeof(uint32_t)) != hipSuccess ||
+        s->sp_fcost.alloc(size_t(S) * sizeof(unsigned long long)) != hipSuccess ||
         s->sp_temp.alloc(s->sp_temp_bytes = rtk::sort_pairs_temp_bytes(n, 24)) != hipSuccess) {
         s->spec_cap = s->spec_units = 0;
         return false;
@@ -529,8 +538,30 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
 // samples whose assumed incoming stack state was wrong (RT_SPEC_ITERS passes), and hand any
 // pixel still unresolved to the sequential kernel from its first unresolved sample.  All
 // launches are enqueued on `st`; counts stay on the device.
+bool g_time_kernels = false;  // rt_debug_time_kernels
+
+// k_iow03s(L) launch, bracketed by events on its stream when kernel timing is on
+hipError_t spec_launch(rt_dev_scene *s, const rtk::Frame &f, const rtk::IowScene &sc, const rtk::SpecRecs &R, int mode,
+                       const rtk::Cont &ct, uint32_t n, unsigned *counter, int cap, hipStream_t st) {
+    std::pair<hipEvent_t, hipEvent_t> *ev = nullptr;
+    if (g_time_kernels) {
+        if (s->kt_used == s->kt_ev.size()) {
+            std::pair<hipEvent_t, hipEvent_t> p{nullptr, nullptr};
+            if (hipEventCreate(&p.first) != hipSuccess || hipEventCreate(&p.second) != hipSuccess) return hipErrorUnknown;
+            s->kt_ev.push_back(p);
+        }
+        ev = &s->kt_ev[s->kt_used++];
+        hipError_t e = hipEventRecord(ev->first, st);
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = rtk::launch_iow03_spec(f, sc, R, mode, ct, n, counter, cap, st);
+    if (e == hipSuccess && ev) e = hipEventRecord(ev->second, st);
+    return e;
+}
+
 int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const uint32_t P = rtk::units_of(f), S = uint32_t(s->s_stop);
+    s->kt_used = 0;
     int rc = ensure_workspace(s, P);
     if (rc != RT_OK) return rc;
     const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 6)));
@@ -543,7 +574,11 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const rtk::SpecRecs R{s->sp_col.as<float4>(), s->sp_fin.as<float4>(), s->sp_ctr.as<uint4>(),
                           s->sp_assume.as<float4>(), P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(),
                           sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), ++s->epoch,
-                          s->sp_front.as<uint4>()};
+                          s->sp_front.as<uint4>(), s->sp_sorder.as<uint32_t>(),
+                          uint32_t(std::max(1, env_int("RT_SPEC_PROBE", 64))),
+                          S > 2 && groups == 1 ? uint32_t(std::min(int(S) - 2, std::max(0, env_int("RT_SPEC_HEAVY",
+                                                                                                  int(S - 1) / 20))))
+                                               : 0u};
     rtk::IowScene scene{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
                         s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link,
                                  s->obox.as<float4>(), s->n_wide};
@@ -557,6 +592,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     struct Lane { hipStream_t st; unsigned *counter; const DevBuf *cont; unsigned *cnt; };
     // fix = true: before each resume launch, make the parked samples exact where possible
     const bool fix_on = env_int("RT_SPEC_FIX", 0) != 0;  // measured neutral: off by default
+    const bool spread_last = env_int("RT_SPEC_SPREAD", 1) != 0;
     auto pass = [&](const Lane &q, auto &&launch, uint32_t n0, int cap, bool fix = false) {
         const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
         for (int r = 0; r <= rounds && e == hipSuccess; r++) {
@@ -578,13 +614,13 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                 ct.park_min = park_min;
                 e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), q.st);
                 if (e != hipSuccess) break;
-            }
+            } else if (r > 0 && spread_last) ct.spread = 1;  // the last round: long samples get a wave each
             e = launch(q, ct, n_units);
         }
     };
     auto spec = [&](const rtk::SpecRecs &RR, int mode) {
         return [&, RR, mode](const Lane &q, const rtk::Cont &ct, uint32_t n) {
-            return rtk::launch_iow03_spec(f, scene, RR, mode, ct, n, q.counter, cap_s, q.st);
+            return spec_launch(s, f, scene, RR, mode, ct, n, q.counter, cap_s, q.st);
         };
     };
     // Checkpoint rounds (RT_SPEC_ROUNDS = k > 0): the speculative pass over samples 1.. runs as k
@@ -593,8 +629,31 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // and mispredicted samples at a frontier are re-run at once (k_iow03_frontier,
     // k_iow03_fixf).  The tail then runs as before (compaction rounds).
     const int ckpt = S > 1 ? std::max(0, std::min(kCountSlots - 16, env_int("RT_SPEC_ROUNDS", 24))) : 0;
+    // Heavy-first (R.n_heavy = K > 0): round 0 runs every sample of every R.probe_stride-th pixel;
+    // the measured cost per sample index orders the indices (k_sample_rank); the next rounds run
+    // the K costliest indices for every pixel (sample-major, so the long samples start first);
+    // the pixels are then re-sorted by the rays of those samples and the remaining indices run
+    // pixel-major (so each heavy pixel's frontier reaches its long samples early).
     auto ckpt_pass = [&](const Lane &q, const rtk::SpecRecs &RG, uint32_t n_fresh) {
         const uint32_t slots = uint32_t(s->blocks_cap) * rtk::kBlock, cap_cont = 2 * slots;
+        struct Rnd { int mode; uint32_t lo, hi; };
+        std::vector<Rnd> plan;
+        const uint32_t n_px = RG.order_n ? RG.order_n : RG.P, K = RG.n_heavy;
+        int r_heavy_end = -1;  // last round of the heavy phase
+        if (K > 0 && ckpt >= 3) {
+            const uint32_t n_probe = (n_px + RG.probe_stride - 1) / RG.probe_stride * (S - 1);
+            plan.push_back({1, 0, n_probe});
+            const int rest = ckpt - 1;
+            const int ra = std::max(1, std::min(rest - 1, int(std::lround(double(rest) * K / (S - 1)))));
+            const uint64_t nh = uint64_t(K) * n_px, nr = uint64_t(S - 1 - K) * n_px;
+            for (int r = 0; r < ra; r++) plan.push_back({2, uint32_t(nh * r / ra), uint32_t(nh * (r + 1) / ra)});
+            r_heavy_end = ra;
+            for (int r = 0; r < rest - ra; r++)
+                plan.push_back({3, uint32_t(nr * r / (rest - ra)), uint32_t(nr * (r + 1) / (rest - ra))});
+        } else {
+            for (int r = 0; r < ckpt; r++)
+                plan.push_back({0, uint32_t(uint64_t(n_fresh) * r / ckpt), uint32_t(uint64_t(n_fresh) * (r + 1) / ckpt)});
+        }
         int b = 0;  // continuation buffer written last
         for (int r = 0; r < ckpt && e == hipSuccess; r++) {
             rtk::Cont ct{};
@@ -603,32 +662,61 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             ct.out_count = q.cnt + 16 * r;
             ct.mixed = 1;
             ct.park_below = 65;  // park every busy lane once the queue drains
-            ct.fresh_lo = uint32_t(uint64_t(n_fresh) * r / ckpt);
-            ct.fresh_hi = uint32_t(uint64_t(n_fresh) * (r + 1) / ckpt);
+            ct.fresh_mode = plan[size_t(r)].mode;
+            ct.fresh_lo = plan[size_t(r)].lo;
+            ct.fresh_hi = plan[size_t(r)].hi;
             if (r == ckpt - 1) ct.park_below = 0;  // the last round compacts as the tail rounds do
             ct.park_min = r == ckpt - 1 ? uint32_t(std::max(0, env_int("RT_PARK_MIN", cap_s * rtk::kBlock / 8))) : 0u;
             e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), q.st);
-            if (e == hipSuccess) e = rtk::launch_iow03_spec(f, scene, RG, rtk::kSpecRest, ct, uint32_t(cap_s) * rtk::kBlock,
-                                                            q.counter, cap_s, q.st);
+            if (e == hipSuccess) e = spec_launch(s, f, scene, RG, rtk::kSpecRest, ct, uint32_t(cap_s) * rtk::kBlock,
+                                                 q.counter, cap_s, q.st);
             if (e == hipSuccess) e = rtk::launch_iow03_frontier(f, RG, ct.out, ct.out_count, cap_cont, q.st);
             if (e == hipSuccess) e = rtk::launch_iow03_fixf(f, RG, ct.out, ct.out_count, int(cap_cont), q.st);
+            if (e == hipSuccess && r == 0 && r_heavy_end > 0)
+                e = rtk::launch_iow03_sample_order(f, RG, ct.out, ct.out_count, int(cap_cont),
+                                                   s->sp_fcost.as<unsigned long long>(), s->sp_sorder.as<uint32_t>(),
+                                                   q.st);
+            if (e == hipSuccess && r == r_heavy_end) {
+                e = rtk::launch_iow03_pixel_key(f, RG, ct.out, ct.out_count, int(cap_cont), s->ws_cost.as<unsigned>(),
+                                                q.st);
+                if (e == hipSuccess)
+                    e = rtk::sort_units_by_cost(s->ws_cost.as<unsigned>(), s->ws_keys.as<unsigned>(),
+                                                s->ws_iota.as<unsigned>(), s->ws_order.as<unsigned>(), P,
+                                                s->ws_temp.p, s->ws_temp_bytes, q.st);
+            }
             b = r & 1;
         }
-        // tail: resume rounds with compaction, the last one running to completion
+        // tail: resume rounds with compaction; the first `tb` of them are budgeted (every unit
+        // parks after RT_SPEC_TAIL_BUDGET segments) and followed by the frontier, so a sample found
+        // mispredicted re-runs while the long samples are still running; the last round runs to
+        // completion
         const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap_s * rtk::kBlock / 8)));
-        for (int t = 0; t <= rounds && e == hipSuccess; t++) {
+        const int tb = std::max(0, std::min(kCountSlots - 16 - ckpt - rounds, env_int("RT_SPEC_TAIL_ROUNDS", 0)));
+        const uint32_t budget = uint32_t(std::max(1, env_int("RT_SPEC_TAIL_BUDGET", 4096)));
+        const int n_tail = tb + rounds;
+        const bool spread = spread_last;
+        for (int t = 0; t <= n_tail && e == hipSuccess; t++) {
             const int r = ckpt + t;
             rtk::Cont ct{};
             ct.in = q.cont[b].as<float4>();
             ct.in_count = q.cnt + 16 * (r - 1);
-            if (t < rounds) {
+            if (t < n_tail) {
                 ct.out = q.cont[b ^ 1].as<float4>();
                 ct.out_count = q.cnt + 16 * r;
                 ct.park_min = park_min;
+                if (t < tb) {
+                    ct.seg_budget = budget;
+                    if (spread) { ct.spread = 1; ct.park_min = 0xffffffffu; }  // no compaction parking
+                }
                 e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), q.st);
             }
-            if (e == hipSuccess) e = rtk::launch_iow03_spec(f, scene, RG, rtk::kSpecRest, ct, uint32_t(cap_s) * rtk::kBlock,
-                                                            q.counter, cap_s, q.st);
+            if (t == n_tail && spread) ct.spread = 1;  // the last round: long samples get a wave each
+            if (e == hipSuccess) e = spec_launch(s, f, scene, RG, rtk::kSpecRest, ct, uint32_t(cap_s) * rtk::kBlock,
+                                                 q.counter, cap_s, q.st);
+            if (e == hipSuccess && t < tb) {
+                e = rtk::launch_iow03_frontier(f, RG, ct.out, ct.out_count, cap_cont, q.st);
+                if (e == hipSuccess) e = rtk::launch_iow03_fixf(f, RG, ct.out, ct.out_count, int(cap_cont), q.st);
+            }
             b ^= 1;
         }
     };
@@ -955,6 +1043,19 @@ int rt_debug_spec_list_hist(rt_dev_scene *s, uint64_t *out) {
     return RT_OK;
 }
 
+int rt_debug_spec_list_stale(rt_dev_scene *s, uint64_t *out) {
+    if (!s || !out) return RT_E_ARG;
+    std::memset(out, 0, 32 * sizeof(uint64_t));
+    if (!s->spec_cap) return RT_OK;
+    DevBuf d;
+    HIP_OK(d.alloc(32 * sizeof(uint64_t)));
+    HIP_OK(hipMemset(d.p, 0, 32 * sizeof(uint64_t)));
+    HIP_OK(rtk::spec_list_stale(s->sp_ctr.as<uint4>(), s->sp_list.as<uint32_t>(), s->sp_counts.as<unsigned>(),
+                                d.as<unsigned long long>(), nullptr));
+    HIP_OK(hipMemcpy(out, d.p, 32 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
 int rt_debug_spec_pixels(rt_dev_scene *s, uint32_t *out, uint32_t cap_units) {
     if (!s || !out) return RT_E_ARG;
     if (!s->spec_cap || !s->spec_units || s->spec_units > cap_units) return RT_E_ARG;
@@ -973,6 +1074,25 @@ int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {
         name_out[name_cap - 1] = 0;
     }
     return s->last_launches;
+}
+
+int rt_debug_time_kernels(int on) {
+    g_time_kernels = on != 0;
+    return RT_OK;
+}
+
+int rt_debug_kernel_time(rt_dev_scene *s, double *ms_total, int *launches) {
+    if (!s || !ms_total || !launches) return RT_E_ARG;
+    double t = 0.0;
+    for (size_t i = 0; i < s->kt_used; i++) {
+        HIP_OK(hipEventSynchronize(s->kt_ev[i].second));
+        float ms = 0.0f;
+        HIP_OK(hipEventElapsedTime(&ms, s->kt_ev[i].first, s->kt_ev[i].second));
+        t += ms;
+    }
+    *ms_total = t;
+    *launches = int(s->kt_used);
+    return RT_OK;
 }
 
 int rt_debug_counters(uint64_t *d_buf) {

@@ -540,7 +540,12 @@ __device__ __forceinline__ void iow_seg_shade(const IowScene &S, const Frame &F,
             int pi = K.size - 1 - skip;
             float parent = (pi < 0) ? 1.0f : (pi < kIowStack ? K.at(pi, 7) : 0.0f);
             target_ri = cos_t > 0.0f ? parent : data.material.z;
-            if (cos_t > 0.0f && pi >= 0 && pi < kIowStack && !((K.wmask >> pi) & 1u)) K.rmask |= 1u << pi;
+            if (cos_t > 0.0f && pi >= 0 && pi < kIowStack && !((K.wmask >> pi) & 1u)) {
+                // diagnostics (RT_DEBUG_FIRST_STALE): the segment of the first stale read replaces
+                // the unit's drop counter
+                if (F.dbg_first_stale && K.rmask == 0u) c.drops = 0x80000000u | c.seg;
+                K.rmask |= 1u << pi;
+            }
         }
         float rr = (ri * rcp(target_ri)) * sin_t;
         float refr_c = data.material.x, refl_c = data.material.y;
@@ -942,6 +947,8 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     const uint32_t total = nin + f_n;
     const bool may_park = ct.out != nullptr && total >= ct.park_min;
     const int park_below = ct.park_below ? ct.park_below : kParkBelow;
+    const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t wcap = ct.spread ? max(1u, (total + n_waves - 1u) / n_waves) : 64u;
     const int W = f.W, H = f.H, spp = f.spp;
     int grid = 1;
     while (grid * grid < spp) grid++;
@@ -953,6 +960,19 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     int skip = 0;
     f3 sample = f3{0, 0, 0};
     const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
+    const unsigned started_tag = (1u << 9) | ((R.epoch & 0xffffu) << 16);  // heavy-first: taken, unfinished
+    uint32_t useg = 0;  // segments of the current unit in this launch (ct.seg_budget)
+    // the lane's state at a segment boundary -> a continuation slot (13 float4)
+    auto park = [&](float4 *p) {
+        p[0] = make_float4(ubits(u), ibits(skip), ibits(K.size), ubits(K.wmask | (K.rmask << 4)));
+        p[1] = make_float4(sample.x, sample.y, sample.z, ubits(urays));
+        p[2] = make_float4(ubits(c.seg), ubits(c.nodes), ubits(c.prims), ubits(c.drops));
+        p[12] = make_float4(ubits(c.nans), 0.0f, 0.0f, 0.0f);  // .y: restart flag (k_iow03_fix)
+        float *fl = reinterpret_cast<float *>(p + 3);
+        for (int k = 0; k < kFl; k++) fl[k] = K.base[k * kBlock];
+        if constexpr (NARROW)
+            for (int e = 0; e < kIowStack; e++) fl[kFl + e] = ibits(K.bounced(e));
+    };
     // start unit u (sample s of pixel pu) with assumed stack RI a.xyz in entries 1..3
     auto begin = [&](uint32_t u_, float4 a) {
         u = u_;
@@ -962,6 +982,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         busy = true;
         c.seg = c.nodes = c.prims = c.drops = c.nans = 0;
         urays = 0;
+        useg = 0;
         skip = 0;
         sample = f3{0, 0, 0};
         K.size = 0; K.wmask = 0; K.rmask = 0;
@@ -976,8 +997,15 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         } else K.push(ro, rd, 1.0f, 1.0f, 0, c);
     };
     for (;;) {
-        const uint32_t q = fetch_unit(counter, live && !busy);
-        if (live && !busy) {
+        // spread: a wave holds at most wcap units, so a few long samples get a wave each (and the
+        // wave-cooperative closest hits) instead of sharing one
+        bool want = live && !busy;
+        if (wcap < 64u) {
+            const int room = (int)wcap - __popcll(__ballot(busy));
+            want = want && (int)lanes_below(__ballot(want)) < room;
+        }
+        const uint32_t q = fetch_unit(counter, want);
+        if (want) {
             if (q >= total) live = false;
             else if (q < nin && ct.in[(size_t)q * kContSlots + 12].y != 0.0f) {  // doomed while parked: restart exact
                 u = __float_as_uint(ct.in[(size_t)q * kContSlots].x);
@@ -994,31 +1022,36 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 for (int k = 0; k < kFl; k++) K.base[k * kBlock] = fl[k];
                 if constexpr (NARROW)
                     for (int e = 0; e < kIowStack; e++) K.set_bounced(e, __float_as_int(fl[kFl + e]));
+                useg = 0;
                 busy = true;
             } else {
                 // kSpecFirst: sample 0 of every pixel; kSpecRest: samples 1.. pixel-major, pixels
                 // in R.order (heaviest sample 0 first); kSpecList: the re-execution list
                 const uint32_t qf = f_lo + (q - nin);
-                u = mode == kSpecList ? R.list[qf]
-                    : (mode == kSpecFirst ? qf : (1u + qf % (R.S - 1)) * R.P + R.order[R.order_base + qf / (R.S - 1)]);
-                if (unit_pixel(f, u % R.P).in_image)
+                bool fresh = true;
+                if (ct.fresh_mode == 0) {
+                    u = mode == kSpecList ? R.list[qf]
+                        : (mode == kSpecFirst ? qf : (1u + qf % (R.S - 1)) * R.P + R.order[R.order_base + qf / (R.S - 1)]);
+                } else {  // heavy-first enumerations of kSpecRest (a unit may come up twice: run it once)
+                    const uint32_t n_px = R.order_n ? R.order_n : R.P, nr = R.S - 1u - R.n_heavy;
+                    uint32_t s_, rank;
+                    if (ct.fresh_mode == 1) { rank = (qf / (R.S - 1u)) * R.probe_stride; s_ = 1u + qf % (R.S - 1u); }
+                    else if (ct.fresh_mode == 2) { s_ = R.sorder[qf / n_px]; rank = qf % n_px; }
+                    else { s_ = R.sorder[R.n_heavy + qf % nr]; rank = qf / nr; }
+                    u = s_ * R.P + R.order[R.order_base + rank];
+                    const uint32_t tag = __float_as_uint(R.col[u].w);
+                    fresh = !((tag >> 16) == (R.epoch & 0xffffu) && (tag & 0x300u) != 0u);
+                }
+                if (fresh && unit_pixel(f, u % R.P).in_image) {
+                    if (ct.fresh_mode != 0) R.col[u].w = ubits(started_tag);
                     begin(u, mode == kSpecFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : R.assume[u]);
+                }
             }
         }
         if (__ballot(live) == 0) break;
         if (may_park && __ballot(!live) != 0 && __popcll(__ballot(busy)) < park_below) {
             const uint32_t slot = park_slot(ct.out_count, busy);
-            if (busy) {
-                float4 *p = ct.out + (size_t)slot * kContSlots;
-                p[0] = make_float4(ubits(u), ibits(skip), ibits(K.size), ubits(K.wmask | (K.rmask << 4)));
-                p[1] = make_float4(sample.x, sample.y, sample.z, ubits(urays));
-                p[2] = make_float4(ubits(c.seg), ubits(c.nodes), ubits(c.prims), ubits(c.drops));
-                p[12] = make_float4(ubits(c.nans), 0.0f, 0.0f, 0.0f);  // .y: restart flag (k_iow03_fix)
-                float *fl = reinterpret_cast<float *>(p + 3);
-                for (int k = 0; k < kFl; k++) fl[k] = K.base[k * kBlock];
-                if constexpr (NARROW)
-                    for (int e = 0; e < kIowStack; e++) fl[kFl + e] = ibits(K.bounced(e));
-            }
+            if (busy) park(ct.out + (size_t)slot * kContSlots);
             break;
         }
         DBG_TALLY(f, c, kDbgOuter, busy);
@@ -1027,9 +1060,16 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         {
             const bool seg = busy && K.size > 0;
             iow_seg_step<NARROW, Cfg::BS, Cfg::NS>(S, f, K, skip, sample, (int)(u / R.P), c, bstk, nodes, seg);
-            if (seg) urays++;
+            if (seg) { urays++; useg++; }
         }
         DBG_CYC(f, c, kDbgCycSeg, t_seg);
+        if (ct.seg_budget) {  // budgeted round: a unit that used its segments parks (per lane)
+            const bool over = busy && K.size > 0 && useg >= ct.seg_budget;
+            if (__ballot(over) != 0) {
+                const uint32_t slot = park_slot(ct.out_count, over);
+                if (over) { park(ct.out + (size_t)slot * kContSlots); busy = false; }
+            }
+        }
         if (busy && K.size == 0) {  // sample done: record it
             R.col[u] = make_float4(sample.x, sample.y, sample.z, ubits(K.rmask | (K.wmask << 4) | done_tag));
             R.fin[u] = make_float4(K.at(1, 7), K.at(2, 7), K.at(3, 7), ubits(c.prims));
@@ -1152,7 +1192,7 @@ __global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, 
             if (slot >= cap) atomicSub(count, 1u);  // full: leave it to the resolve after the pass
             else {
                 R.assume[u] = make_float4(__uint_as_float(st.y), __uint_as_float(st.z), __uint_as_float(st.w), 0.0f);
-                R.col[u].w = 0.0f;  // unfinished until the re-run records it
+                R.col[u].w = __uint_as_float((1u << 9) | ((R.epoch & 0xffffu) << 16));  // queued: unfinished
                 float4 *p = cont + (size_t)slot * kContSlots;
                 p[0] = make_float4(__uint_as_float((uint32_t)u), 0.0f, 0.0f, 0.0f);
                 p[12] = make_float4(0.0f, 1.0f, 0.0f, 0.0f);  // restart with the (now exact) assumption
@@ -2123,6 +2163,24 @@ hipError_t spec_pixels(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t 
     hipLaunchKernelGGL(k_spec_pixels, dim3((P + 255) / 256), dim3(256), 0, s, ctr, P, S, order, d_out);
     return hipGetLastError();
 }
+// diagnostics: where re-executed samples first read a stale entry (RT_DEBUG_FIRST_STALE runs):
+// out[b] = samples, out[16 + b] = their rays, bucket b = 16 * first_stale_segment / rays
+__global__ void k_spec_list_stale(const uint4 *ctr, const uint32_t *list, const unsigned *count,
+                                  unsigned long long *out) {
+    const unsigned n = *count;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint4 c = ctr[list[i]];
+        if (!(c.y & 0x80000000u) || c.x == 0) continue;
+        const unsigned b = min(15u, (unsigned)(((unsigned long long)(c.y & 0x7fffffffu) * 16ull) / c.x));
+        atomicAdd(out + b, 1ull);
+        atomicAdd(out + 16 + b, (unsigned long long)c.x);
+    }
+}
+hipError_t spec_list_stale(const uint4 *ctr, const uint32_t *list, const unsigned *count, unsigned long long *d_out,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_spec_list_stale, dim3(1024), dim3(256), 0, s, ctr, list, count, d_out);
+    return hipGetLastError();
+}
 // diagnostics: log2 histogram of the rays of the samples on the (first) re-execution list
 __global__ void k_spec_list_hist(const uint4 *ctr, const uint32_t *list, const unsigned *count,
                                  unsigned long long *out) {
@@ -2171,6 +2229,87 @@ hipError_t launch_iow03_fix(const Frame &f, const SpecRecs &R, float4 *cont, con
 hipError_t launch_iow03_keys0(const Frame &f, const SpecRecs &R, unsigned *key, hipStream_t s) {
     const unsigned blocks = (R.P + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_iow03_keys0, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, key);
+    return hipGetLastError();
+}
+// ---------------------------------------------------------------- heavy-first enumeration
+// cost of sample index s (1..S-1) over the probe pixels: finished records (block s-1)
+__global__ __launch_bounds__(kBlock) void k_sample_cost(SpecRecs R, unsigned long long *fcost) {
+    __shared__ unsigned long long part[kBlock / 64];
+    const uint32_t s = blockIdx.x + 1u;
+    const uint32_t n_px = R.order_n ? R.order_n : R.P;
+    const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
+    unsigned long long acc = 0;
+    for (uint32_t i = threadIdx.x; (size_t)i * R.probe_stride < n_px; i += kBlock) {
+        const size_t u = (size_t)s * R.P + R.order[R.order_base + i * R.probe_stride];
+        if ((__float_as_uint(R.col[u].w) & 0xffff0100u) == done_tag) acc += R.ctr[u].x;
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kBlock / 64; w++) t += part[w];
+        atomicAdd(fcost + s, t);
+    }
+}
+// progress of the parked lanes (the long samples still running) counts toward their index
+__global__ __launch_bounds__(kBlock) void k_sample_cost_parked(SpecRecs R, const float4 *cont, const unsigned *count,
+                                                               unsigned long long *fcost) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= *count) return;  // no cross-lane work in this kernel
+    const float4 *p = cont + (size_t)i * kContSlots;
+    if (p[12].y != 0.0f) return;
+    const uint32_t u = __float_as_uint(p[0].x);
+    atomicAdd(fcost + u / R.P, (unsigned long long)__float_as_uint(p[2].x));
+}
+// rank the indices 1..S-1 by cost, most expensive first (ties: lower index first)
+__global__ __launch_bounds__(1024) void k_sample_rank(SpecRecs R, const unsigned long long *fcost, uint32_t *sorder) {
+    for (uint32_t s = 1u + threadIdx.x; s < R.S; s += 1024u) {
+        const unsigned long long c = fcost[s];
+        uint32_t rank = 0;
+        for (uint32_t t = 1; t < R.S; t++) rank += (fcost[t] > c || (fcost[t] == c && t < s)) ? 1u : 0u;
+        sorder[rank] = s;
+    }
+}
+// per pixel: the most rays among its heavy samples (finished records), for the re-sort
+__global__ __launch_bounds__(kBlock) void k_pixel_key(Frame f, SpecRecs R, unsigned *key) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n_px = R.order_n ? R.order_n : R.P;
+    if (i >= n_px) return;  // no cross-lane work in this kernel
+    const uint32_t pu = R.order[R.order_base + i];
+    const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
+    unsigned k = R.ctr[pu].x;  // sample 0
+    for (uint32_t j = 0; j < R.n_heavy; j++) {
+        const size_t u = (size_t)R.sorder[j] * R.P + pu;
+        if ((__float_as_uint(R.col[u].w) & 0xffff0100u) == done_tag) k = max(k, R.ctr[u].x);
+    }
+    key[pu] = unit_pixel(f, pu).in_image ? k : 0u;
+}
+__global__ __launch_bounds__(kBlock) void k_pixel_key_parked(SpecRecs R, const float4 *cont, const unsigned *count,
+                                                             unsigned *key) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= *count) return;  // no cross-lane work in this kernel
+    const float4 *p = cont + (size_t)i * kContSlots;
+    if (p[12].y != 0.0f) return;
+    const uint32_t u = __float_as_uint(p[0].x);
+    atomicMax(key + u % R.P, __float_as_uint(p[2].x));
+}
+hipError_t launch_iow03_sample_order(const Frame &f, const SpecRecs &R, const float4 *cont, const unsigned *count,
+                                     int max_lanes, unsigned long long *fcost, uint32_t *sorder, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(fcost, 0, sizeof(unsigned long long) * R.S, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_sample_cost, dim3(R.S - 1u), dim3(kBlock), 0, s, R, fcost);
+    const unsigned blocks = (unsigned)((max_lanes + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_sample_cost_parked, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, R, cont, count, fcost);
+    hipLaunchKernelGGL(k_sample_rank, dim3(1), dim3(1024), 0, s, R, fcost, sorder);
+    return hipGetLastError();
+}
+hipError_t launch_iow03_pixel_key(const Frame &f, const SpecRecs &R, const float4 *cont, const unsigned *count,
+                                  int max_lanes, unsigned *key, hipStream_t s) {
+    const uint32_t n_px = R.order_n ? R.order_n : R.P;
+    hipLaunchKernelGGL(k_pixel_key, dim3((n_px + kBlock - 1) / kBlock), dim3(kBlock), 0, s, f, R, key);
+    const unsigned blocks = (unsigned)((max_lanes + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_pixel_key_parked, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, R, cont, count, key);
     return hipGetLastError();
 }
 hipError_t launch_iow03_frontier(const Frame &f, const SpecRecs &R, float4 *cont, unsigned *count, uint32_t cap,

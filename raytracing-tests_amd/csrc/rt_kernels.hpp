@@ -23,6 +23,7 @@ struct Frame {
     int leaf_batch;           // IOW-03 walk: test postponed leaves once this many lanes hold one
     unsigned *px_rays;        // optional: rays cast per work unit, written when its pixel completes
     int coop_max;             // IOW-03: wave-cooperative closest hits when at most this many lanes trace
+    int dbg_first_stale;      // diagnostics: record the segment of a sample's first stale read (corrupts drops)
     // INW-01 MULTIFOCUS (01_BVH...glsl:388-404, 505-549; "#if MULTIFOCUS" in the reference):
     // n_focus = 0 is the single-focus camera the reference builds, 1..9 the lens chain
     int n_focus;
@@ -109,6 +110,10 @@ struct SpecRecs {
     uint4 *pstate;     // asynchronous windows: per pixel unit 3 x uint4 of frontier state
     uint32_t epoch;    // frame tag: finished records carry it in their flags
     uint4 *front;      // checkpoint rounds: per pixel unit (first unvalidated sample, exact RI bits of entries 1..3)
+    // heavy-first enumeration (fresh_mode 1..3): sample indices 1..S-1 by measured cost, most
+    // expensive first; the first n_heavy of them run for every pixel before the rest
+    const uint32_t *sorder;
+    uint32_t probe_stride, n_heavy;
 };
 enum { kSpecFirst = 0, kSpecRest = 1, kSpecList = 2 };
 
@@ -131,6 +136,12 @@ struct Cont {
     // busy lane once the queue drains (0 = kParkBelow, the tail-compaction rule)
     int mixed, park_below;
     uint32_t fresh_lo, fresh_hi;
+    // fresh units of kSpecRest: 0 = samples 1.. pixel-major in R.order; 1 = probe (every sample
+    // of every probe_stride-th pixel of R.order); 2 = the n_heavy costliest sample indices,
+    // sample-major; 3 = the other indices, pixel-major.  Modes 1-3 skip units already started.
+    int fresh_mode;
+    uint32_t seg_budget;  // > 0: a lane parks its unit after this many segments in the launch
+    int spread;           // a wave takes at most ceil(units / waves) units at a time
 };
 
 hipError_t launch_iow01(const Frame &f, hipStream_t s);
@@ -168,6 +179,8 @@ size_t remap_workspace_bytes(int W, int H);
 hipError_t texture_remap(const uint8_t *d_in, int W, int H, int C, int load_as, uint8_t *d_out, void *d_ws,
                          hipStream_t s);
 hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipStream_t s);  // diagnostics
+hipError_t spec_list_stale(const uint4 *ctr, const uint32_t *list, const unsigned *count, unsigned long long *d_out,
+                           hipStream_t s);  // diagnostics
 hipError_t spec_list_hist(const uint4 *ctr, const uint32_t *list, const unsigned *count, unsigned long long *d_out,
                           hipStream_t s);  // diagnostics
 hipError_t spec_pixels(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *order, uint32_t *d_out,
@@ -191,6 +204,12 @@ hipError_t launch_iow03_frontier(const Frame &f, const SpecRecs &R, float4 *cont
                                  hipStream_t s);
 hipError_t launch_iow03_fixf(const Frame &f, const SpecRecs &R, float4 *cont, const unsigned *count, int max_lanes,
                              hipStream_t s);
+// heavy-first enumeration: per sample index cost from the probe pixels' records and the parked
+// lanes' progress -> R.sorder; per pixel cost of its heavy samples -> key (sort -> R.order)
+hipError_t launch_iow03_sample_order(const Frame &f, const SpecRecs &R, const float4 *cont, const unsigned *count,
+                                     int max_lanes, unsigned long long *fcost, uint32_t *sorder, hipStream_t s);
+hipError_t launch_iow03_pixel_key(const Frame &f, const SpecRecs &R, const float4 *cont, const unsigned *count,
+                                  int max_lanes, unsigned *key, hipStream_t s);
 hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,
                              hipStream_t s);
 // replay each pixel's samples: re-queue wrong assumptions; final: write clean pixels, hand

@@ -53,4 +53,8 @@ h = (C.c_uint64 * 66)()
 lib.rt_debug_spec_list_hist(scene, h)
 res["relist"] = {"samples": int(h[1]), "max_rays": int(h[0]),
                  "log2_hist": {b: [int(h[2 + b]), int(h[34 + b])] for b in range(32) if h[2 + b]}}
+if os.environ.get("RT_DEBUG_FIRST_STALE") == "1":
+    h2 = (C.c_uint64 * 32)()
+    lib.rt_debug_spec_list_stale(scene, h2)
+    res["first_stale_16ths"] = {"samples": [int(h2[b]) for b in range(16)], "rays": [int(h2[16 + b]) for b in range(16)]}
 print(json.dumps(res))
