@@ -291,6 +291,10 @@ def main():
             if lib.rt_debug_spec_hist(scene, h) == 0 and h[1]:
                 out["sample_rays"] = {"max": h[0], "samples": h[1],
                                       "log2_hist": {b: [h[2 + b], h[34 + b]] for b in range(32) if h[2 + b]}}
+            h = (C.c_uint64 * 66)()
+            if lib.rt_debug_spec_list_hist(scene, h) == 0 and h[1]:  # the re-execution list after the pass
+                out["relist_rays"] = {"max": h[0], "samples": h[1],
+                                      "log2_hist": {b: [h[2 + b], h[34 + b]] for b in range(32) if h[2 + b]}}
             cyc = dict(zip(("camera", "closest_hit", "bvh_walk", "leaf_tests", "segment", "coop_query", "coop_shade",
                             "coop_pop"), d[8:16]))
             out["wave_cycles_share"] = {k: round(v / max(1, cyc["camera"] + cyc["segment"]), 4) for k, v in cyc.items()}

@@ -272,6 +272,11 @@ int rt_debug_spec_list_hist(rt_dev_scene *s, uint64_t *out);
  * samples / rays of the re-execution list whose first stale stack read came in the b-th 16th
  * of their segments. */
 int rt_debug_spec_list_stale(rt_dev_scene *s, uint64_t *out);
+/* Rays of every (pixel unit, sample) record of the last sample-parallel IOW-03 render
+ * (rays_out[s * P + pu], cap >= P * S), group 0's last re-execution list (up to list_cap
+ * units) and dims = {P, S, list count, sequential-leftover count}. */
+int rt_debug_spec_dump(rt_dev_scene *s, uint32_t *rays_out, size_t cap, uint32_t *list_out, uint32_t list_cap,
+                       uint32_t *dims);
 /* Main render kernel of the scene's last render and how many times it was launched (the
  * bench's per-launch roofline figures divide by this).  Returns the count; writes the name. */
 int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap);

@@ -564,7 +564,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     s->kt_used = 0;
     int rc = ensure_workspace(s, P);
     if (rc != RT_OK) return rc;
-    const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 6)));
+    const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 1)));
     const int iters = std::max(0, env_int("RT_SPEC_ITERS", 1));
     const int groups = S > 1 ? std::max(1, std::min(32, env_int("RT_SPEC_GROUPS", 1))) : 1;
     const size_t gmax = size_t(P + groups - 1) / groups + 1;  // pixels in the largest group
@@ -593,6 +593,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // fix = true: before each resume launch, make the parked samples exact where possible
     const bool fix_on = env_int("RT_SPEC_FIX", 0) != 0;  // measured neutral: off by default
     const bool spread_last = env_int("RT_SPEC_SPREAD", 1) != 0;
+    // the first launch of the next pass takes its sorted head one unit per wave (Cont.solo_n)
+    uint32_t solo_first = 0;
     auto pass = [&](const Lane &q, auto &&launch, uint32_t n0, int cap, bool fix = false) {
         const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
         for (int r = 0; r <= rounds && e == hipSuccess; r++) {
@@ -615,6 +617,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                 e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), q.st);
                 if (e != hipSuccess) break;
             } else if (r > 0 && spread_last) ct.spread = 1;  // the last round: long samples get a wave each
+            if (r == 0) ct.solo_n = solo_first;
             e = launch(q, ct, n_units);
         }
     };
@@ -792,7 +795,9 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                     e = rtk::sort_pairs_desc(k1, k2, RG.list, l2, nmax, GL.temp.p, GL.temp_bytes, 24, L.st);
                 rtk::SpecRecs R2 = RG;
                 R2.list = l2;
+                solo_first = uint32_t(std::max(0, env_int("RT_SOLO", 4096)));
                 if (e == hipSuccess) pass(L, spec(R2, rtk::kSpecList), uint32_t(nmax), cap_s, true);
+                solo_first = 0;
             } else if (e == hipSuccess) pass(L, spec(RG, rtk::kSpecList), uint32_t(nmax), cap_s, true);
         }
         if (e == hipSuccess) e = hipMemsetAsync(RG.fb_count, 0, sizeof(unsigned), L.st);
@@ -1065,6 +1070,23 @@ int rt_debug_spec_pixels(rt_dev_scene *s, uint32_t *out, uint32_t cap_units) {
     HIP_OK(rtk::spec_pixels(s->sp_ctr.as<uint4>(), P, S, s->ws_order.as<uint32_t>(), d.as<uint32_t>(), nullptr));
     HIP_OK(hipMemcpy(out, d.p, size_t(P) * 16, hipMemcpyDeviceToHost));
     return int(P);
+}
+
+int rt_debug_spec_dump(rt_dev_scene *s, uint32_t *rays_out, size_t cap, uint32_t *list_out, uint32_t list_cap,
+                       uint32_t *dims) {
+    if (!s || !rays_out || !dims) return RT_E_ARG;
+    if (!s->spec_cap || !s->spec_units) return RT_E_ARG;
+    const uint32_t P = uint32_t(s->spec_units), S = uint32_t(s->spec_cap / P);
+    if (size_t(P) * S > cap) return RT_E_ARG;
+    std::vector<uint4> h(size_t(P) * S);
+    HIP_OK(hipMemcpy(h.data(), s->sp_ctr.p, h.size() * sizeof(uint4), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < h.size(); i++) rays_out[i] = h[i].x;
+    unsigned cnt[32] = {};
+    HIP_OK(hipMemcpy(cnt, s->sp_counts.p, sizeof(cnt), hipMemcpyDeviceToHost));
+    const uint32_t nl = std::min(cnt[0], list_cap);
+    if (list_out && nl) HIP_OK(hipMemcpy(list_out, s->sp_list.p, size_t(nl) * 4, hipMemcpyDeviceToHost));
+    dims[0] = P; dims[1] = S; dims[2] = cnt[0]; dims[3] = cnt[16];
+    return RT_OK;
 }
 
 int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {

@@ -956,6 +956,9 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     const float dsx = aspect * rcp((float)(W * grid));
     const float dsy = 1.0f * rcp((float)(H * grid));
     bool live = true, busy = false;
+    bool solo = false;  // wave-uniform: the wave holds one unit from the sorted head
+    const uint32_t solo_n = min(min(ct.solo_n, n_waves / 2u), total);
+    bool solo_open = solo_n != 0;  // wave-uniform: the queue head may still be below solo_n
     uint32_t u = 0, urays = 0;
     int skip = 0;
     f3 sample = f3{0, 0, 0};
@@ -1004,7 +1007,20 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
             const int room = (int)wcap - __popcll(__ballot(busy));
             want = want && (int)lanes_below(__ballot(want)) < room;
         }
+        // solo head: the queue is read only while this wave has not yet seen it pass solo_n (the
+        // counter only grows), so the check costs a load per wave at the start of a launch
+        if (solo) {
+            if (__ballot(busy) != 0) want = false;  // keep the head unit alone
+            else solo = false;
+        }
+        if (!solo && solo_open && __ballot(want) != 0) {
+            const uint32_t head = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (head >= solo_n) solo_open = false;
+            else want = want && __ballot(busy) == 0 && lanes_below(__ballot(want)) == 0;
+        }
         const uint32_t q = fetch_unit(counter, want);
+        if (solo_open && __ballot(want && q < solo_n) != 0) solo = true;
         if (want) {
             if (q >= total) live = false;
             else if (q < nin && ct.in[(size_t)q * kContSlots + 12].y != 0.0f) {  // doomed while parked: restart exact

@@ -142,6 +142,10 @@ struct Cont {
     int fresh_mode;
     uint32_t seg_budget;  // > 0: a lane parks its unit after this many segments in the launch
     int spread;           // a wave takes at most ceil(units / waves) units at a time
+    // units sorted longest first (the LPT re-execution list): while the queue head is below
+    // min(solo_n, waves / 2), an empty wave takes one unit and keeps it alone to the end, so
+    // the longest samples run with the wave-cooperative closest hits instead of sharing a wave
+    uint32_t solo_n;
 };
 
 hipError_t launch_iow01(const Frame &f, hipStream_t s);

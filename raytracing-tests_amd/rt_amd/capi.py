@@ -135,6 +135,7 @@ SIGNATURES = {
     "rt_debug_spec_pixels": (C.c_int, [C.c_void_p, _U32P, C.c_uint32]),
     "rt_debug_spec_list_hist": (C.c_int, [C.c_void_p, _U64P]),
     "rt_debug_spec_list_stale": (C.c_int, [C.c_void_p, _U64P]),
+    "rt_debug_spec_dump": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32, C.c_void_p]),
 }
 
 _lib = None
