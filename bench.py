@@ -39,6 +39,8 @@ import rt_amd as R  # noqa: E402
 TILE = 64
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (= f32 MFMA rate), MI355X_MICROARCH.md
 HBM_PEAK_GBPS = 8000.0     # MI355X HBM3E peak, MI355X_MICROARCH.md
+CUS = 256                  # MI355X compute units
+CLOCK_HZ = 2.4e9           # MI355X peak engine clock
 WORKLOAD = ("In-One-Weekend 03_Adding_Materials final scene (~500 random spheres + ground cuboid), "
             "1200x800, 100 spp, 50 bounces")
 
@@ -230,7 +232,7 @@ def main():
         # sequential leftover pass traces ~2% of them) over the main kernel's launches
         achieved = flops / (main_ms * 1e-3) / 1e12
         balg = algorithmic_bytes(per_step, W * H / world) / launches
-        traffic = None
+        traffic, valu = None, None
         prof = os.path.join(ROOT, "profiles", "pmc_iow03.json")
         if os.path.exists(prof):
             try:
@@ -238,8 +240,16 @@ def main():
                 if pm.get("config") == [W, H, spp]:
                     if pm.get("launches_per_frame") == launches and pm.get("kernel") == kname:
                         traffic = pm.get("hbm_bytes_per_launch")
+                        # VALU issue: a wave64 VALU instruction occupies its SIMD's issue for 2
+                        # cycles (MI355X_MICROARCH.md); capacity = CUs x 4 SIMDs x clock x time
+                        insts = pm["counters"]["SQ_INSTS_VALU"] / pm["frames"]
+                        cap = CUS * 4 * CLOCK_HZ * (main_ms * 1e-3)
+                        valu = {"busy_frac": round(2.0 * insts / cap, 4),
+                                "lane_util": round(pm["valu_lane_utilisation"], 4),
+                                "insts_per_frame": insts, "clock_hz": CLOCK_HZ,
+                                "source": "profiles/pmc_iow03.json (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU)"}
             except Exception:
-                traffic = None
+                traffic, valu = None, None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(sc, args.cpu_threads, args.cpu_px)
@@ -268,6 +278,7 @@ def main():
                          "flops_per_launch": flops / launches,
                          "note": "VALU fp32 kernel (no MFMA on this path); peak = FP32 vector peak; "
                                  "traffic = PMC HBM bytes per launch from profiles/pmc_iow03.json"},
+            "valu": valu,
             "hbm": {"achieved_GBps": round(balg / (main_ms / launches * 1e-3) / 1e9, 1),
                     "peak_GBps": HBM_PEAK_GBPS, "algorithmic_bytes_per_launch": balg},
             "mean_bounces": round(st["segments"] / (W * H * spp * args.steps), 3),
