@@ -2,7 +2,10 @@
 
 - RT_IOW_LINEAR=1: the reference's linear object loop instead of the culling BVH;
 - RT_IOW_NARROW=1: the byte-bounce stack layout (12-deep BVH stack) instead of the 9-float one;
-- RT_ROUNDS=0:     no tail compaction (no parking / resume launches);
+- RT_ROUNDS=0/6:   no tail compaction (no parking / resume launches) / six compaction rounds
+  per pass (default 1 on the sample-parallel path);
+- RT_SOLO=0/10^5:  the re-run pass's longest samples without / with up to waves/2 waves of
+  their own (default 4096, i.e. waves/2 on MI355X; DESIGN.md "Solo head");
 - RT_IOW_SPEC=0:   the sequential per-pixel kernel instead of sample-parallel speculation;
 - RT_SPEC_ITERS=0/3/10: other numbers of resolve passes (default 1), more pixels finished by the sequential kernel (which
   takes the still-exact records; RT_SPEC_VALIDATE=0 re-runs every sample from the first bad one);
@@ -55,7 +58,7 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS", "RT_IOW_SPEC", "RT_SPEC_ITERS",
               "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_SPEC_GROUPS", "RT_IOW_ASYNC", "RT_SPEC_FIX",
               "RT_SPEC_VALIDATE", "RT_SPEC_PRIOR_FROM", "RT_COOP", "RT_IOW_LDS",
-              "RT_SPEC_ROUNDS"):
+              "RT_SPEC_ROUNDS", "RT_SOLO", "RT_SPEC_HEAVY"):
         env.pop(k, None)
     env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out, preset=scene[0], seed=scene[1], n_hint=scene[2])
@@ -90,6 +93,10 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     ({"RT_COOP": "64", "RT_IOW_SPEC": "0"}, 300, 200, 4),
     ({"RT_COOP": "64", "RT_IOW_LINEAR": "1"}, 200, 100, 2),
     ({"RT_SPEC_GROUPS": "7", "RT_SPEC_ITERS": "2"}, 300, 200, 16),
+    ({"RT_ROUNDS": "6"}, 600, 400, 12),
+    ({"RT_SOLO": "0"}, 600, 400, 12),
+    ({"RT_SOLO": "100000", "RT_SPEC_ITERS": "2"}, 300, 200, 16),
+    ({"RT_SPEC_HEAVY": "0"}, 300, 200, 16),
 ])
 def test_strategies_bit_identical(tmp_path, gpu, over, w, h, spp):
     a, sa = _render(tmp_path, {}, w, h, spp)
