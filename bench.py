@@ -36,7 +36,14 @@ import torch.distributed as dist  # noqa: E402
 
 import rt_amd as R  # noqa: E402
 
-TILE = 64
+TILE = 64        # tile edge on one GPU
+TILE_MULTI = 16  # tile edge of a multi-rank partition: finer tiles deal the heavy pixels out more evenly
+
+
+def tile_for(world: int) -> int:
+    """Tile edge (a multiple of 8) for a partition over `world` ranks; RT_BENCH_TILE overrides."""
+    env = os.environ.get("RT_BENCH_TILE", "")
+    return int(env) if env else (TILE if world == 1 else TILE_MULTI)
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (= f32 MFMA rate), MI355X_MICROARCH.md
 HBM_PEAK_GBPS = 8000.0     # MI355X HBM3E peak, MI355X_MICROARCH.md
 CUS = 256                  # MI355X compute units
@@ -55,17 +62,18 @@ def algorithmic_bytes(st: dict, pixels: int) -> float:
     return 32.0 * st["node_visits"] + 96.0 * st["prim_tests"] + 16.0 * pixels
 
 
-def tiles_for_rank(W: int, H: int, world: int, rank: int):
-    nx, ny = math.ceil(W / TILE), math.ceil(H / TILE)
+def tiles_for_rank(W: int, H: int, world: int, rank: int, tile: int = TILE):
+    nx, ny = math.ceil(W / tile), math.ceil(H / tile)
     allt = [(tx, ty) for ty in range(ny) for tx in range(nx)]
     return allt, allt[rank::world], math.ceil(len(allt) / world)
 
 
 def assemble_frame(src, n_tiles: int, nx: int, ny: int):
-    """src: [world, per_rank, TILE, TILE, 4] packed tiles as gathered on rank 0, where tile t of
-    rank r is allt[r + world*t].  Returns the [ny*TILE, nx*TILE, 4] frame (crop to W x H)."""
-    order = src.permute(1, 0, 2, 3, 4).reshape(-1, TILE, TILE, 4)[:n_tiles]
-    return order.view(ny, nx, TILE, TILE, 4).permute(0, 2, 1, 3, 4).reshape(ny * TILE, nx * TILE, 4)
+    """src: [world, per_rank, T, T, 4] packed tiles as gathered on rank 0, where tile t of rank r
+    is allt[r + world*t].  Returns the [ny*T, nx*T, 4] frame (crop to W x H)."""
+    T = src.shape[2]
+    order = src.permute(1, 0, 2, 3, 4).reshape(-1, T, T, 4)[:n_tiles]
+    return order.view(ny, nx, T, T, 4).permute(0, 2, 1, 3, 4).reshape(ny * T, nx * T, 4)
 
 
 def cpu_baseline(sc, threads: int, px: int) -> dict:
@@ -129,27 +137,29 @@ def main():
         over["height"] = args.height
     sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0, **over)
     W, H, spp = sc.params.width, sc.params.height, sc.params.spp
-    allt, mine, per_rank = tiles_for_rank(W, H, world, rank)
+    T = tile_for(world)
+    allt, mine, per_rank = tiles_for_rank(W, H, world, rank, T)
     shard = os.environ.get("RT_BENCH_SHARD", "")  # diagnostic "r/N": one process renders rank r's tiles of N
     if shard and world == 1:
         sr, sn = (int(v) for v in shard.split("/"))
-        allt, mine, per_rank = tiles_for_rank(W, H, sn, sr)
+        T = tile_for(sn)
+        allt, mine, per_rank = tiles_for_rank(W, H, sn, sr, T)
 
     scene = lib.rt_dev_scene_iow03(R.fptr(sc.types), R.fptr(sc.records), sc.n, spp, local)
     if not scene:
         raise RuntimeError("rt_dev_scene_iow03 failed (no gfx950 device?)")
     d_tiles = torch.tensor(mine, dtype=torch.int32, device=dev).reshape(-1, 2).contiguous()
-    packed = torch.zeros((per_rank, TILE, TILE, 4), dtype=torch.float32, device=dev)
+    packed = torch.zeros((per_rank, T, T, 4), dtype=torch.float32, device=dev)
     counters = torch.zeros(6, dtype=torch.int64, device=dev)
     dbg = torch.zeros(16, dtype=torch.int64, device=dev)
-    px_rays = torch.zeros(per_rank * TILE * TILE, dtype=torch.int32, device=dev)
+    px_rays = torch.zeros(per_rank * T * T, dtype=torch.int32, device=dev)
     lib.rt_debug_time_kernels(1)
     if args.occupancy:
         lib.rt_debug_counters(dbg.data_ptr())
         lib.rt_debug_pixel_rays(px_rays.data_ptr())
     gathered = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
-    nx, ny = math.ceil(W / TILE), math.ceil(H / TILE)
-    image = torch.empty((ny * TILE, nx * TILE, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+    nx, ny = math.ceil(W / T), math.ceil(H / T)
+    image = torch.empty((ny * T, nx * T, 4), dtype=torch.float32, device=dev) if rank == 0 else None
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     def step(i=None):
@@ -158,7 +168,7 @@ def main():
             ev[i][0].record(stream)
         if mine:
             rc = lib.rt_render_tiles_async(scene, C.byref(sc.camera), C.byref(sc.params), d_tiles.data_ptr(),
-                                           len(mine), TILE, packed.data_ptr(), None, counters.data_ptr(),
+                                           len(mine), T, packed.data_ptr(), None, counters.data_ptr(),
                                            stream.cuda_stream)
             if rc != 0:
                 raise RuntimeError(f"rt_render_tiles_async -> {rc}")
@@ -267,7 +277,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded final-scene generator, SURVEY 8d seed 20250131)",
             "config": {"workload": WORKLOAD, "width": W, "height": H, "spp": spp,
-                       "max_bounces": sc.params.max_bounces, "objects": sc.n, "tile": TILE,
+                       "max_bounces": sc.params.max_bounces, "objects": sc.n, "tile": T,
                        "parallelism": f"tiles_rr{world}" + ("+rccl_gather" if world > 1 else "")},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),

@@ -1,6 +1,6 @@
 """Multi-GPU partition + exchange, rehearsed on the CPU with gloo (world size 2 and 3).
 
-bench.py deals 64x64 tiles round-robin to ranks, each rank packs its tiles, one gather brings
+bench.py deals tiles round-robin to ranks (64x64 on one GPU, 16x16 across ranks), each rank packs its tiles, one gather brings
 them to rank 0, and rank 0 assembles the frame.  Here every rank "renders" a
 deterministic per-pixel pattern into its packed tiles; the assembled frame must equal the
 pattern everywhere, and the tile lists must cover every tile exactly once.
@@ -30,12 +30,11 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, W, H, q):
+def _worker(rank, world, port, W, H, T, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        allt, mine, per_rank = bench.tiles_for_rank(W, H, world, rank)
-        T = bench.TILE
+        allt, mine, per_rank = bench.tiles_for_rank(W, H, world, rank, T)
         ref = _pattern(W, H)
         packed = torch.zeros((per_rank, T, T, 4))
         for k, (tx, ty) in enumerate(mine):  # what rt_render_tiles_async writes: 0 outside the image
@@ -52,12 +51,13 @@ def _worker(rank, world, port, W, H, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,W,H", [(2, 1200, 800), (3, 200, 130), (2, 64, 64)])
-def test_gather_assembles_frame(world, W, H):
+@pytest.mark.parametrize("world,W,H,T", [(2, 1200, 800, 16), (2, 1200, 800, 64), (3, 200, 130, 16),
+                                         (3, 200, 130, 64), (2, 64, 64, 64)])
+def test_gather_assembles_frame(world, W, H, T):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, T, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -69,10 +69,12 @@ def test_gather_assembles_frame(world, W, H):
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_tiles_cover_frame_once(world):
     W, H = 1200, 800
+    T = bench.tile_for(world)
+    assert T == (64 if world == 1 else 16)
     seen = []
     for r in range(world):
-        allt, mine, per_rank = bench.tiles_for_rank(W, H, world, r)
+        allt, mine, per_rank = bench.tiles_for_rank(W, H, world, r, T)
         assert len(mine) <= per_rank
         seen += mine
     assert sorted(seen) == sorted(allt)
-    assert len(set(seen)) == len(allt) == math.ceil(W / 64) * math.ceil(H / 64)
+    assert len(set(seen)) == len(allt) == math.ceil(W / T) * math.ceil(H / T)

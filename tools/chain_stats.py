@@ -17,13 +17,14 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "raytracing-tests_amd")]
 import torch  # noqa: E402
 
 import rt_amd as R  # noqa: E402
-from bench import TILE, tiles_for_rank  # noqa: E402
+from bench import tile_for, tiles_for_rank  # noqa: E402
 
 r, n = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (0, 1)
 lib = R.load()
 sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0)
 W, H = sc.params.width, sc.params.height
-_, mine, per_rank = tiles_for_rank(W, H, n, r)
+TILE = tile_for(n)
+_, mine, per_rank = tiles_for_rank(W, H, n, r, TILE)
 scene = lib.rt_dev_scene_iow03(R.fptr(sc.types), R.fptr(sc.records), sc.n, sc.params.spp, 0)
 dev = torch.device("cuda", 0)
 d_tiles = torch.tensor(mine, dtype=torch.int32, device=dev).reshape(-1, 2).contiguous()
