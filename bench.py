@@ -50,6 +50,9 @@ CUS = 256                  # MI355X compute units
 CLOCK_HZ = 2.4e9           # MI355X peak engine clock
 WORKLOAD = ("In-One-Weekend 03_Adding_Materials final scene (~500 random spheres + ground cuboid), "
             "1200x800, 100 spp, 50 bounces")
+# --config c4 (BASELINE configs[3]): the C3 LBVH scene tile-partitioned; not the headline line
+WORKLOAD_C4 = ("In-Next-Week 01 LBVH: 10k random moving spheres, 1920x1080, 500 spp, 50 bounces, "
+               "tile-partitioned (C4)")
 
 
 def algorithmic_flops(st: dict) -> float:
@@ -57,8 +60,11 @@ def algorithmic_flops(st: dict) -> float:
     return 40.0 * st["node_visits"] + 70.0 * st["prim_tests"] + 60.0 * st["segments"]
 
 
-def algorithmic_bytes(st: dict, pixels: int) -> float:
-    """SURVEY.md 8d contract: B_alg = 32*node_visits + 96*prim_tests (IOW records) + 16*W*H."""
+def algorithmic_bytes(st: dict, pixels: int, inw: bool = False) -> float:
+    """SURVEY.md 8d contract: B_alg = 32*node_visits + 96*prim_tests (IOW records) + 16*W*H;
+    INW: 112-B records and 20 B per pixel (colour + depth)."""
+    if inw:
+        return 32.0 * st["node_visits"] + 112.0 * st["prim_tests"] + 20.0 * pixels
     return 32.0 * st["node_visits"] + 96.0 * st["prim_tests"] + 16.0 * pixels
 
 
@@ -106,6 +112,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--occupancy", action="store_true", help="report per-phase lane occupancy (diagnostic)")
     ap.add_argument("--save-image", default="", help="rank 0 saves the assembled frame (.npy) for checking")
+    ap.add_argument("--config", default="c2", choices=("c2", "c4"),
+                    help="c2: the headline (BASELINE configs[1]); c4: the LBVH scene of configs[3]")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -135,7 +143,11 @@ def main():
         over["width"] = args.width
     if args.height:
         over["height"] = args.height
-    sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0, **over)
+    inw = args.config == "c4"
+    if inw:
+        sc = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 10_000, **over)
+    else:
+        sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0, **over)
     W, H, spp = sc.params.width, sc.params.height, sc.params.spp
     T = tile_for(world)
     allt, mine, per_rank = tiles_for_rank(W, H, world, rank, T)
@@ -145,11 +157,15 @@ def main():
         T = tile_for(sn)
         allt, mine, per_rank = tiles_for_rank(W, H, sn, sr, T)
 
-    scene = lib.rt_dev_scene_iow03(R.fptr(sc.types), R.fptr(sc.records), sc.n, spp, local)
+    if inw:
+        scene = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, sc.layout, R.fptr(sc.nodes), None, 0, spp, local)
+    else:
+        scene = lib.rt_dev_scene_iow03(R.fptr(sc.types), R.fptr(sc.records), sc.n, spp, local)
     if not scene:
         raise RuntimeError("rt_dev_scene_iow03 failed (no gfx950 device?)")
     d_tiles = torch.tensor(mine, dtype=torch.int32, device=dev).reshape(-1, 2).contiguous()
     packed = torch.zeros((per_rank, T, T, 4), dtype=torch.float32, device=dev)
+    depth = torch.zeros((per_rank, T, T), dtype=torch.float32, device=dev) if inw else None  # INW's r32f image
     counters = torch.zeros(6, dtype=torch.int64, device=dev)
     dbg = torch.zeros(16, dtype=torch.int64, device=dev)
     px_rays = torch.zeros(per_rank * T * T, dtype=torch.int32, device=dev)
@@ -168,7 +184,8 @@ def main():
             ev[i][0].record(stream)
         if mine:
             rc = lib.rt_render_tiles_async(scene, C.byref(sc.camera), C.byref(sc.params), d_tiles.data_ptr(),
-                                           len(mine), T, packed.data_ptr(), None, counters.data_ptr(),
+                                           len(mine), T, packed.data_ptr(),
+                                           depth.data_ptr() if depth is not None else None, counters.data_ptr(),
                                            stream.cuda_stream)
             if rc != 0:
                 raise RuntimeError(f"rt_render_tiles_async -> {rc}")
@@ -241,7 +258,7 @@ def main():
         # per launch of the main kernel: the frame's algorithmic flops (all of its rays; the
         # sequential leftover pass traces ~2% of them) over the main kernel's launches
         achieved = flops / (main_ms * 1e-3) / 1e12
-        balg = algorithmic_bytes(per_step, W * H / world) / launches
+        balg = algorithmic_bytes(per_step, W * H / world, inw) / launches
         traffic, valu = None, None
         prof = os.path.join(ROOT, "profiles", "pmc_iow03.json")
         if os.path.exists(prof):
@@ -275,8 +292,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded final-scene generator, SURVEY 8d seed 20250131)",
-            "config": {"workload": WORKLOAD, "width": W, "height": H, "spp": spp,
+            "data": ("synthetic (seeded C3 generator, SURVEY 8d seed 1234)" if inw else
+                     "synthetic (seeded final-scene generator, SURVEY 8d seed 20250131)"),
+            "config": {"workload": WORKLOAD_C4 if inw else WORKLOAD, "width": W, "height": H, "spp": spp,
                        "max_bounces": sc.params.max_bounces, "objects": sc.n, "tile": T,
                        "parallelism": f"tiles_rr{world}" + ("+rccl_gather" if world > 1 else "")},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
