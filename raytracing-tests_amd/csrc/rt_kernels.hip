@@ -957,7 +957,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     const float dsy = 1.0f * rcp((float)(H * grid));
     bool live = true, busy = false;
     bool solo = false;  // wave-uniform: the wave holds one unit from the sorted head
-    const uint32_t solo_n = min(min(ct.solo_n, n_waves / 2u), total);
+    const uint32_t solo_n = min(min(ct.solo_n, n_waves), total);
     bool solo_open = solo_n != 0;  // wave-uniform: the queue head may still be below solo_n
     uint32_t u = 0, urays = 0;
     int skip = 0;

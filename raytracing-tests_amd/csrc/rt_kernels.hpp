@@ -143,7 +143,7 @@ struct Cont {
     uint32_t seg_budget;  // > 0: a lane parks its unit after this many segments in the launch
     int spread;           // a wave takes at most ceil(units / waves) units at a time
     // units sorted longest first (the LPT re-execution list): while the queue head is below
-    // min(solo_n, waves / 2), an empty wave takes one unit and keeps it alone to the end, so
+    // min(solo_n, waves), an empty wave takes one unit and keeps it alone to the end, so
     // the longest samples run with the wave-cooperative closest hits instead of sharing a wave
     uint32_t solo_n;
 };

@@ -4,8 +4,9 @@
 - RT_IOW_NARROW=1: the byte-bounce stack layout (12-deep BVH stack) instead of the 9-float one;
 - RT_ROUNDS=0/6:   no tail compaction (no parking / resume launches) / six compaction rounds
   per pass (default 1 on the sample-parallel path);
-- RT_SOLO=0/10^5:  the re-run pass's longest samples without / with up to waves/2 waves of
-  their own (default 4096, i.e. waves/2 on MI355X; DESIGN.md "Solo head");
+- RT_SOLO=0/10^5:  the re-run pass's longest samples share waves / take a wave each up to the
+  resident wave count (default 4096, clamped to the 3072 resident waves on MI355X; DESIGN.md
+  "Solo head");
 - RT_IOW_SPEC=0:   the sequential per-pixel kernel instead of sample-parallel speculation;
 - RT_SPEC_ITERS=0/3/10: other numbers of resolve passes (default 1), more pixels finished by the sequential kernel (which
   takes the still-exact records; RT_SPEC_VALIDATE=0 re-runs every sample from the first bad one);
