@@ -39,6 +39,14 @@ CASES = {
     "inw04_refset": lambda: _scene(R.PRESET_INW04_REFSET, spp=16),
     "inw04_nolights": lambda: _no_lights(_scene(R.PRESET_INW04_REFSET, spp=8)),
     "inw04_cornell": lambda: _scene(R.PRESET_INW04_CORNELL, 7, 0, width=64, height=64, spp=8),
+    # edge cases: ragged frames (no tile or wave multiple), a single pixel, one bounce, and
+    # LBVHs whose root is a leaf (one object) or has two leaves
+    "iow03_final_odd": lambda: _scene(R.PRESET_IOW03_FINAL, 20250131, 0, width=67, height=5, spp=2),
+    "iow03_final_1px": lambda: _scene(R.PRESET_IOW03_FINAL, 20250131, 0, width=1, height=1, spp=3),
+    "iow03_ref3_b1": lambda: _scene(R.PRESET_IOW03_REF3, spp=2, max_bounces=1),
+    "inw01_random_one": lambda: _scene(R.PRESET_INW01_RANDOM, 5, 1, width=17, height=3, spp=4),
+    "inw01_random_two": lambda: _scene(R.PRESET_INW01_RANDOM, 5, 2, width=33, height=7, spp=4),
+    "inw04_cornell_odd": lambda: _scene(R.PRESET_INW04_CORNELL, 7, 0, width=13, height=11, spp=3, max_bounces=3),
 }
 
 GOLDEN_CASES = ["iow01_c1", "iow03_ref3", "iow03_ref3_normals", "iow03_final", "inw01_grid",
