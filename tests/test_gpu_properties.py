@@ -10,6 +10,7 @@ full configs are checked through properties that hold for any correct render:
 - C3/C4 (configs[2]/[3], INW-01 LBVH scene, 10k spheres, 1920x1080, 500 spp): the 2-rank deal
   of 16x16 tiles (the multi-GPU partition, rt_render_tiles_async) reassembles to the
   single-call frame bit for bit, colour and depth, with the same ray counts.
+- C5 (configs[4], INW-04 Cornell box, 4096x4096, 2000 spp): see test_c5_full_size_properties.
 """
 import ctypes as C
 
@@ -91,3 +92,24 @@ def test_c4_two_rank_partition_full_size(gpu):
     assert _same(img, full), compare(img, full)
     assert _same(dimg, full_depth)
     assert seg == sf["segments"]
+
+
+def test_c5_full_size_properties(gpu):
+    """C5 (configs[4], INW-04 Cornell box, 4096x4096, 2000 spp): the full frame renders with
+    alpha 1, the depth image holds only the two values INW writes (0 on a hit, 32000 on a miss,
+    01_BVH...glsl depth store), every pixel-sample casts at least one ray and the lights are
+    queried; repeat renders (at 64 spp) are bit-identical with identical counters."""
+    W, H, spp = 4096, 4096, 2000
+    sc = R.make_scene(R.PRESET_INW04_CORNELL, 7, 0, width=W, height=H, spp=spp)
+    img, depth, st = R.render(sc)
+    assert (img[..., 3] == 1.0).all()
+    assert np.isin(depth, (0.0, 32000.0)).all()
+    assert st["segments"] >= W * H * spp
+    assert st["shadow_queries"] > 0
+
+    p = R.RtParams.from_buffer_copy(sc.params)
+    p.spp = 64
+    a, da, sa = R.render(sc, p)
+    b, db, sb = R.render(sc, p)
+    assert _same(a, b) and _same(da, db)
+    assert sa == {**sb, "ms": sa["ms"]}
