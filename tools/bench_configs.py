@@ -40,7 +40,13 @@ def run(name, preset, seed, n_hint, spp=None, **over):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--full", action="store_true", help="C3 and C5 at BASELINE's full spp only")
     a = ap.parse_args()
+    if a.full:
+        for o in (run("C3 INW-01 LBVH 10k moving spheres (full)", R.PRESET_INW01_RANDOM, 1234, 10_000, spp=500),
+                  run("C5 INW-04 Cornell (full)", R.PRESET_INW04_CORNELL, 7, 0, spp=2000)):
+            print(json.dumps(o), flush=True)
+        return
     q = a.quick
     out = []
     d = R.iow01_defaults()
