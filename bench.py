@@ -8,9 +8,10 @@ every pixel, every sample, every bounce of the reference's IOW-03 render loop.
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-Multi-GPU: the frame is cut into 64x64 tiles dealt round-robin to the ranks (one process per
-GPU); each rank renders its tiles into a packed buffer and the tiles are gathered to rank 0
-with one RCCL gather over xGMI, where the image is assembled.  Total work is fixed, so the
+Multi-GPU: the frame is cut into tiles dealt round-robin to the ranks (one process per GPU):
+16x16 tiles across ranks, 64x64 on one GPU (RT_BENCH_TILE overrides both).  Each rank renders
+its tiles into a packed buffer and the tiles are gathered to rank 0 with one RCCL gather over
+xGMI, where the image is assembled.  Total work is fixed, so the
 scaling mode is "strong".
 
 Metric: Mrays/s = W*H*spp*mean_bounces / t = (rays cast, counted by the kernels) / t, summed

@@ -280,6 +280,10 @@ int rt_debug_spec_dump(rt_dev_scene *s, uint32_t *rays_out, size_t cap, uint32_t
 /* Main render kernel of the scene's last render and how many times it was launched (the
  * bench's per-launch roofline figures divide by this).  Returns the count; writes the name. */
 int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap);
+/* Sample chunks of the scene's last render: the sample-parallel paths split the samples into
+ * chunks whose records fit the device's free memory (INW: RT_SPEC_MAX_GB), and the per-pixel
+ * paths split them by chunk_plan.  1 = one pass over all samples. */
+int rt_debug_chunks(rt_dev_scene *s);
 /* Kernel timing (diagnostics / bench): with rt_debug_time_kernels(1), every launch of the main
  * sample-parallel IOW-03 kernel (rt_debug_launches' name) is bracketed by HIP events on its
  * stream; rt_debug_kernel_time returns the summed durations and the launch count of the

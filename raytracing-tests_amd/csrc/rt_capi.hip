@@ -137,6 +137,7 @@ struct rt_dev_scene {
     // launches of the render's main kernel in the last render (rt_debug_launches)
     int last_launches = 0;
     const char *last_kernel = "";
+    int last_chunks = 0;  // sample chunks of the last render (rt_debug_chunks)
     // sample-parallel pipelines: one stream per pixel group, each with its own queue counter,
     // continuation buffers and sort scratch (rt_render_* calls on one scene must not overlap)
     struct GroupLane {
@@ -460,6 +461,7 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const uint32_t units = rtk::units_of(f);
     s->last_kernel = s->kind == 3 ? (rtk::iow_narrow(f) ? "k_iow03n" : "k_iow03") : (s->layout == 4 ? "k_inw<true>" : "k_inw<false>");
     s->last_launches = int(plan.size()) * (1 + std::min(14, std::max(0, env_int("RT_ROUNDS", 6))));
+    s->last_chunks = int(plan.size());
     if (plan.size() > 1) {
         int rc = ensure_workspace(s, units);
         if (rc != RT_OK) return rc;
@@ -637,6 +639,11 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // the K costliest indices for every pixel (sample-major, so the long samples start first);
     // the pixels are then re-sorted by the rays of those samples and the remaining indices run
     // pixel-major (so each heavy pixel's frontier reaches its long samples early).
+    // Budgeted tail rounds (RT_SPEC_TAIL_ROUNDS, RT_SPEC_TAIL_BUDGET segments each; DESIGN.md
+    // "Budgeted tail"): the frontier advances between them, so mispredicted samples re-run while
+    // the long ones still run instead of in a re-run pass after them.
+    const int tail_budgeted =
+        ckpt > 0 ? std::max(0, std::min(kCountSlots - 16 - ckpt - rounds, env_int("RT_SPEC_TAIL_ROUNDS", 60))) : 0;
     auto ckpt_pass = [&](const Lane &q, const rtk::SpecRecs &RG, uint32_t n_fresh) {
         const uint32_t slots = uint32_t(s->blocks_cap) * rtk::kBlock, cap_cont = 2 * slots;
         struct Rnd { int mode; uint32_t lo, hi; };
@@ -694,8 +701,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         // mispredicted re-runs while the long samples are still running; the last round runs to
         // completion
         const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap_s * rtk::kBlock / 8)));
-        const int tb = std::max(0, std::min(kCountSlots - 16 - ckpt - rounds, env_int("RT_SPEC_TAIL_ROUNDS", 0)));
-        const uint32_t budget = uint32_t(std::max(1, env_int("RT_SPEC_TAIL_BUDGET", 4096)));
+        const int tb = tail_budgeted;
+        const uint32_t budget = uint32_t(std::max(1, env_int("RT_SPEC_TAIL_BUDGET", 3072)));
         const int n_tail = tb + rounds;
         const bool spread = spread_last;
         for (int t = 0; t <= n_tail && e == hipSuccess; t++) {
@@ -724,7 +731,9 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         }
     };
     s->last_kernel = lds ? "k_iow03sL" : "k_iow03s";
-    s->last_launches = (1 + rounds) * (1 + groups * ((S > 1 ? 1 : 0) + iters)) + (ckpt > 0 ? groups * ckpt : 0);
+    s->last_launches = (1 + rounds) * (1 + groups * ((S > 1 ? 1 : 0) + iters)) +
+                       (ckpt > 0 ? groups * (ckpt + tail_budgeted) : 0);
+    s->last_chunks = 1;
     // (1) on the caller's stream: sample 0 of every pixel (exact), the guesses for the other
     // samples, and the pixel order (heaviest sample 0 first)
     const Lane L0{st, s->counter.as<unsigned>(), s->cont, s->cont_count.as<unsigned>()};
@@ -748,13 +757,15 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         return RT_OK;
     }
     if (S > 1) {
-        // Entries sample 0 left unwritten: guess 0 (as sample 0 saw them) for samples below
-        // RT_SPEC_PRIOR_FROM (2), the scene's most common RI from there on.  The prior misses
-        // far less often (the re-run pass re-traces ~1.5% of the rays instead of ~20%); the
-        // dependent chains it forms are cheap for the validating sequential pass.
+        // Sample 1 starts from sample 0's final stack (exact: its written entries, 0 elsewhere).
+        // From RT_SPEC_PRIOR_FROM (2) on every entry is guessed as the scene's most common RI
+        // (RT_SPEC_PRIOR_S0=1: keep sample 0's values where it wrote them, the round-1 rule).
+        // The prior misses far less often (the re-run pass re-traces ~1% of the rays instead of
+        // ~20% with zeros); the dependent chains it forms are cheap for the validating pass.
         const uint32_t prior_from = uint32_t(std::max(1, env_int("RT_SPEC_PRIOR_FROM", 2)));
         if (e == hipSuccess)
-            e = rtk::launch_iow03_prep(f, R, s->ws_cost.as<unsigned>(), s->ri_prior, prior_from, st);
+            e = rtk::launch_iow03_prep(f, R, s->ws_cost.as<unsigned>(), s->ri_prior, prior_from,
+                                         env_int("RT_SPEC_PRIOR_S0", 0), st);
         if (e == hipSuccess)
             e = rtk::sort_units_by_cost(s->ws_cost.as<unsigned>(), s->ws_keys.as<unsigned>(), s->ws_iota.as<unsigned>(),
                                         s->ws_order.as<unsigned>(), P, s->ws_temp.p, s->ws_temp_bytes, st);
@@ -852,6 +863,7 @@ int launch_scene_inw_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st, int ns
     hipError_t e = hipSuccess;
     s->last_kernel = s->layout == 4 ? "k_inw_s<true>" : "k_inw_s<false>";
     s->last_launches = (1 + rounds) * ((f.spp + ns - 1) / ns);
+    s->last_chunks = (f.spp + ns - 1) / ns;
     for (int s0 = 0; s0 < f.spp && e == hipSuccess; s0 += ns) {
         const int k = std::min(ns, f.spp - s0);
         for (int r = 0; r <= rounds && e == hipSuccess; r++) {
@@ -1096,6 +1108,11 @@ int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {
         name_out[name_cap - 1] = 0;
     }
     return s->last_launches;
+}
+
+int rt_debug_chunks(rt_dev_scene *s) {
+    if (!s) return RT_E_ARG;
+    return s->last_chunks;
 }
 
 int rt_debug_time_kernels(int on) {

@@ -215,7 +215,7 @@ hipError_t launch_iow03_sample_order(const Frame &f, const SpecRecs &R, const fl
 hipError_t launch_iow03_pixel_key(const Frame &f, const SpecRecs &R, const float4 *cont, const unsigned *count,
                                   int max_lanes, unsigned *key, hipStream_t s);
 hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,
-                             hipStream_t s);
+                             int keep_s0, hipStream_t s);
 // replay each pixel's samples: re-queue wrong assumptions; final: write clean pixels, hand
 // the rest (with their resume state in `state`) to the sequential kernel via R.fb_list
 hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pass, float4 *state, hipStream_t s);

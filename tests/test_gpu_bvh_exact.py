@@ -12,6 +12,10 @@
   takes the still-exact records; RT_SPEC_VALIDATE=0 re-runs every sample from the first bad one);
 - RT_SPEC_PRIOR_FROM: from which sample on the scene's RI prior is guessed for entries sample 0
   left unwritten (default 2; 10^6 = never, with the former 10 re-run passes);
+- RT_SPEC_TAIL_ROUNDS=0/3: no budgeted tail rounds (the round-1 default) / three, with
+  RT_SPEC_TAIL_BUDGET segments per unit and round (default 60 rounds of 3072);
+- RT_SPEC_PRIOR_S0=1: the round-1 guess (entries sample 0 wrote keep its values from
+  RT_SPEC_PRIOR_FROM on; default 0 guesses the prior for every entry);
 - RT_SPEC_GROUPS=2/7: pixel groups on separate streams;
 - RT_IOW_ASYNC=1: asynchronous windows (per-wave frontiers) instead of global resolve passes;
 - RT_SPEC_FIX=1: mid-pass correction of parked samples (patch / restart with the exact state);
@@ -59,7 +63,8 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS", "RT_IOW_SPEC", "RT_SPEC_ITERS",
               "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_SPEC_GROUPS", "RT_IOW_ASYNC", "RT_SPEC_FIX",
               "RT_SPEC_VALIDATE", "RT_SPEC_PRIOR_FROM", "RT_COOP", "RT_IOW_LDS",
-              "RT_SPEC_ROUNDS", "RT_SOLO", "RT_SPEC_HEAVY"):
+              "RT_SPEC_ROUNDS", "RT_SOLO", "RT_SPEC_HEAVY", "RT_SPEC_PRIOR_S0",
+              "RT_SPEC_TAIL_ROUNDS", "RT_SPEC_TAIL_BUDGET"):
         env.pop(k, None)
     env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out, preset=scene[0], seed=scene[1], n_hint=scene[2])
@@ -98,6 +103,11 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     ({"RT_SOLO": "0"}, 600, 400, 12),
     ({"RT_SOLO": "100000", "RT_SPEC_ITERS": "2"}, 300, 200, 16),
     ({"RT_SPEC_HEAVY": "0"}, 300, 200, 16),
+    ({"RT_SPEC_PRIOR_S0": "1"}, 600, 400, 12),
+    ({"RT_SPEC_PRIOR_S0": "1", "RT_SPEC_ROUNDS": "0"}, 300, 200, 16),
+    ({"RT_SPEC_TAIL_ROUNDS": "0"}, 600, 400, 12),
+    ({"RT_SPEC_TAIL_ROUNDS": "3", "RT_SPEC_TAIL_BUDGET": "64"}, 300, 200, 16),
+    ({"RT_SPEC_TAIL_ROUNDS": "40", "RT_SPEC_TAIL_BUDGET": "16", "RT_SPEC_ROUNDS": "3"}, 300, 200, 16),
 ])
 def test_strategies_bit_identical(tmp_path, gpu, over, w, h, spp):
     a, sa = _render(tmp_path, {}, w, h, spp)
