@@ -1173,7 +1173,7 @@ __global__ __launch_bounds__(kBlock) void k_iow03_prep(Frame f, SpecRecs R, unsi
     // From prior_from on every entry is guessed as the prior unless keep_s0: sample 0 starts from
     // the all-zero stack no later sample sees (a stale 0 makes target_RI 0 and forces TIR,
     // 03...glsl:316-327), so the values it leaves are a worse guess of the steady state than the
-    // scene's most common RI (tools/fork_stats.py: mispredicted rays 2.6% -> 0.8% on C2).
+    // scene's most common RI (tests/analysis/fork_stats.py: mispredicted rays 2.6% -> 0.8% on C2).
     const bool k0 = keep_s0 != 0;
     const float4 e1 = make_float4((k0 && (wm & 2u)) ? fn.x : prior, (k0 && (wm & 4u)) ? fn.y : prior,
                                   (k0 && (wm & 8u)) ? fn.z : prior, 0.0f);

@@ -13,10 +13,10 @@
  * For sampled pixels of a scene this prints, per sample: segments on the exact path, segments
  * over all branches (prefix shared), branches, and the longest branch.
  *
- *   gcc -O2 -fopenmp -ffp-contract=off -o /tmp/fork_stats tools/fork_stats.c -lm
- *   (driven by tools/fork_stats.py)
+ * Lives under tests/ because it builds on the CPU oracle (test infrastructure); it is an offline
+ * study, not a test.  Driven by tests/analysis/fork_stats.py, which compiles it to /tmp.
  */
-#include "../oracle/rt_oracle.c"
+#include "../../oracle/rt_oracle.c"
 
 #define MAXV 8
 typedef struct {

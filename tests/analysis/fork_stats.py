@@ -1,7 +1,9 @@
 """Offline analysis: the cost of evaluating IOW-03 samples for every value of the stale RI entries
 they read (fork on read, tools/fork_stats.c) on random pixels of the bench frame (C2).
 
-  python tools/fork_stats.py [npix] [seed] [extra px,py ...]
+  python tests/analysis/fork_stats.py [npix] [seed] [extra px,py ...]
+
+Offline study on the CPU oracle (test infrastructure, hence under tests/); not collected by pytest.
 """
 import ctypes as C
 import json
@@ -11,13 +13,13 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "raytracing-tests_amd")]
 import rt_amd as R  # noqa: E402
 
 SO = "/tmp/libfork_stats.so"
 subprocess.run(["gcc", "-O2", "-fopenmp", "-ffp-contract=off", "-fPIC", "-shared", "-o", SO,
-                os.path.join(ROOT, "tools", "fork_stats.c"), "-lm"], check=True)
+                os.path.join(ROOT, "tests", "analysis", "fork_stats.c"), "-lm"], check=True)
 lib = C.CDLL(SO)
 npix = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
