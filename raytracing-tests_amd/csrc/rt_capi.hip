@@ -133,6 +133,9 @@ struct rt_dev_scene {
     DevBuf sp_pstate;  // asynchronous windows: per-pixel frontier state
     DevBuf sp_front;   // checkpoint rounds: per-pixel frontier (uint4)
     DevBuf sp_sorder, sp_fcost;  // heavy-first enumeration: sample indices by cost, their costs
+    DevBuf sp_exact;             // RT_SPEC_ORACLE diagnostics: exact incoming state per sample
+    size_t sp_exact_n = 0;
+    bool sp_exact_valid = false;
     size_t sp_temp_bytes = 0;
     // launches of the render's main kernel in the last render (rt_debug_launches)
     int last_launches = 0;
@@ -246,7 +249,13 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
         }
         int depth = 0, depth4 = 0;
         const std::vector<float> bin = rtamd::sah_build(boxes.data(), n, &depth);
-        const std::vector<float> wide = rtamd::bvh4_collapse(bin, &depth4);
+        std::vector<float> wide = rtamd::bvh4_collapse(bin, &depth4);
+        // the kernels read the child links (float 24..27 of a node) as int bits
+        for (size_t w = 0; w < wide.size() / 32; w++)
+            for (int k = 0; k < 4; k++) {
+                const int link = int(wide[w * 32 + 24 + size_t(k)]);
+                std::memcpy(&wide[w * 32 + 24 + size_t(k)], &link, sizeof(link));
+            }
         // links travel as int16 on the traversal stack: wide node ids < n, object ids < n
         if (n < 16384) {
             HIP_OK(s->nodes.upload(wide.data(), wide.size() * sizeof(float)));
@@ -573,7 +582,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     if ((rc = ensure_cont(s)) != RT_OK) return rc;
     if ((rc = ensure_lanes(s, groups, rtk::sort_pairs_temp_bytes(gmax * S, 24))) != RT_OK) return rc;
     unsigned *sc = s->sp_counts.as<unsigned>();  // group g: [32g] list count, [32g+16] fallback count
-    const rtk::SpecRecs R{s->sp_col.as<float4>(), s->sp_fin.as<float4>(), s->sp_ctr.as<uint4>(),
+    rtk::SpecRecs R{s->sp_col.as<float4>(), s->sp_fin.as<float4>(), s->sp_ctr.as<uint4>(),
                           s->sp_assume.as<float4>(), P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(),
                           sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), ++s->epoch,
                           s->sp_front.as<uint4>(), s->sp_sorder.as<uint32_t>(),
@@ -581,6 +590,19 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                           S > 2 && groups == 1 ? uint32_t(std::min(int(S) - 2, std::max(0, env_int("RT_SPEC_HEAVY",
                                                                                                   int(S - 1) / 20))))
                                                : 0u};
+    if (env_int("RT_SPEC_ORACLE", 0) != 0) {  // diagnostics only (see SpecRecs::exact)
+        const size_t n = size_t(P) * S;
+        if (s->sp_exact_n != n) {
+            s->sp_exact.~DevBuf();
+            new (&s->sp_exact) DevBuf();
+            HIP_OK(s->sp_exact.alloc(n * sizeof(float4)));
+            s->sp_exact_n = n;
+            s->sp_exact_valid = false;
+        }
+        R.exact = s->sp_exact.as<float4>();
+        R.exact_mode = 1 | (s->sp_exact_valid ? 2 : 0);
+        s->sp_exact_valid = true;
+    }
     rtk::IowScene scene{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
                         s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link,
                                  s->obox.as<float4>(), s->n_wide};

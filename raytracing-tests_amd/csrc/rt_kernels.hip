@@ -164,6 +164,33 @@ __device__ __forceinline__ float cull_t(float lx, float ly, float lz, float hx, 
     const float tx = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
     return (te <= tx && tx >= -1e-3f && te <= lim) ? te : kMiss;
 }
+// The four children of a 4-wide node at once.  The node is SoA over the children (lx = the
+// four children's low x planes, ...), so (plane - o) * (1/d) runs on child pairs with packed
+// fp32 arithmetic (v_pk_add_f32 / v_pk_mul_f32: two lanes' worth per instruction); min / max
+// stay scalar.  Same operations and rounding per plane as cull_t.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 pk(float a, float b) { return pf2{a, b}; }
+__device__ __forceinline__ void cull4(const float4 lx, const float4 ly, const float4 lz, const float4 hx,
+                                      const float4 hy, const float4 hz, f3 o, f3 id, float lim, float &t0,
+                                      float &t1, float &t2, float &t3) {
+    const pf2 ox = pk(o.x, o.x), oy = pk(o.y, o.y), oz = pk(o.z, o.z);
+    const pf2 ix = pk(id.x, id.x), iy = pk(id.y, id.y), iz = pk(id.z, id.z);
+    const pf2 ax01 = (pk(lx.x, lx.y) - ox) * ix, bx01 = (pk(hx.x, hx.y) - ox) * ix;
+    const pf2 ay01 = (pk(ly.x, ly.y) - oy) * iy, by01 = (pk(hy.x, hy.y) - oy) * iy;
+    const pf2 az01 = (pk(lz.x, lz.y) - oz) * iz, bz01 = (pk(hz.x, hz.y) - oz) * iz;
+    const pf2 ax23 = (pk(lx.z, lx.w) - ox) * ix, bx23 = (pk(hx.z, hx.w) - ox) * ix;
+    const pf2 ay23 = (pk(ly.z, ly.w) - oy) * iy, by23 = (pk(hy.z, hy.w) - oy) * iy;
+    const pf2 az23 = (pk(lz.z, lz.w) - oz) * iz, bz23 = (pk(hz.z, hz.w) - oz) * iz;
+    auto one = [&](float x0, float x1, float y0, float y1, float z0, float z1) {
+        const float te = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+        const float tx = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+        return (te <= tx && tx >= -1e-3f && te <= lim) ? te : kMiss;
+    };
+    t0 = one(ax01.x, bx01.x, ay01.x, by01.x, az01.x, bz01.x);
+    t1 = one(ax01.y, bx01.y, ay01.y, by01.y, az01.y, bz01.y);
+    t2 = one(ax23.x, bx23.x, ay23.x, by23.x, az23.x, bz23.x);
+    t3 = one(ax23.y, bx23.y, ay23.y, by23.y, az23.y, bz23.y);
+}
 __device__ __forceinline__ void cswap(float &ta, int &ka, float &tb, int &kb) {
     const bool sw = tb < ta;
     const float t = sw ? tb : ta;
@@ -287,6 +314,7 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
         DBG_T0(F_, t_trav);
         int sp = 0, pend = -1, cur = S.root_link;
         bool walking = true, ovf = false;  // ovf: a child was dropped by a full stack
+        float lim = min_t * 1.0001f + 1e-3f;  // culling limit, follows min_t
         for (;;) {
             DBG_TALLY(F_, c, kDbgTrav, walking);
             if (walking) {
@@ -294,14 +322,12 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
                 if (cur > 0) {
                     const float4 *nd = nodes + NS * (cur - 1);
                     const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
-                    const float4 lk = nd[6];
+                    const float4 lk = nd[6];  // child links as int bits (set_iow_bvh)
                     c.nodes += 4;
-                    const float lim = min_t * 1.0001f + 1e-3f;
-                    float t0 = cull_t(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, go, id, lim);
-                    float t1 = cull_t(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, go, id, lim);
-                    float t2 = cull_t(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, go, id, lim);
-                    float t3 = cull_t(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, go, id, lim);
-                    int k0 = (int)lk.x, k1 = (int)lk.y, k2 = (int)lk.z, k3 = (int)lk.w;
+                    float t0, t1, t2, t3;
+                    cull4(lx, ly, lz, hx, hy, hz, go, id, lim, t0, t1, t2, t3);
+                    int k0 = __float_as_int(lk.x), k1 = __float_as_int(lk.y), k2 = __float_as_int(lk.z),
+                        k3 = __float_as_int(lk.w);
                     // sort (t, link) ascending; misses carry t = +inf
                     cswap(t0, k0, t1, k1); cswap(t2, k2, t3, k3);
                     cswap(t0, k0, t2, k2); cswap(t1, k1, t3, k3);
@@ -328,7 +354,7 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
             if (__all(!walking || pend >= 0) || __popcll(__ballot(pend >= 0)) >= F_.leaf_batch) {
                 DBG_TALLY(F_, c, kDbgLeaf, pend >= 0);
                 DBG_T0(F_, t_leaf);
-                if (pend >= 0) { test(pend); pend = -1; }
+                if (pend >= 0) { test(pend); pend = -1; lim = min_t * 1.0001f + 1e-3f; }
                 DBG_CYC(F_, c, kDbgCycLeaf, t_leaf);
                 if (__all(!walking)) break;
             }
@@ -1178,6 +1204,8 @@ __global__ __launch_bounds__(kBlock) void k_iow03_prep(Frame f, SpecRecs R, unsi
     const float4 e1 = make_float4((k0 && (wm & 2u)) ? fn.x : prior, (k0 && (wm & 4u)) ? fn.y : prior,
                                   (k0 && (wm & 8u)) ? fn.z : prior, 0.0f);
     for (uint32_t s = 1; s < R.S; s++) R.assume[(size_t)s * R.P + pu] = s >= prior_from ? e1 : e0;
+    if (R.exact && (R.exact_mode & 2))
+        for (uint32_t s = 1; s < R.S; s++) R.assume[(size_t)s * R.P + pu] = R.exact[(size_t)s * R.P + pu];
     if (R.front)  // sample 0 is exact: the frontier starts at sample 1 with its final entries
         R.front[pu] = make_uint4(1u, __float_as_uint(e0.x), __float_as_uint(e0.y), __float_as_uint(e0.z));
     key[pu] = R.ctr[pu].x;
@@ -1280,6 +1308,8 @@ __global__ __launch_bounds__(kBlock) void k_iow03_resolve(Frame f, SpecRecs R, i
         const float4 cl = R.col[u];
         const uint32_t fl = __float_as_uint(cl.w), rm = fl & 15u, wm = (fl >> 4) & 15u;
         const float4 a = R.assume[u];
+        if (final_pass && R.exact && (R.exact_mode & 1) && first_bad < 0)
+            R.exact[u] = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
         const bool bad = ((rm & 2u) && __float_as_uint(a.x) != E1) || ((rm & 4u) && __float_as_uint(a.y) != E2) ||
                          ((rm & 8u) && __float_as_uint(a.z) != E3);
         if (bad) {

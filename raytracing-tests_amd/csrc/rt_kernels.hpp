@@ -114,6 +114,11 @@ struct SpecRecs {
     // expensive first; the first n_heavy of them run for every pixel before the rest
     const uint32_t *sorder;
     uint32_t probe_stride, n_heavy;
+    // diagnostics (RT_SPEC_ORACLE=1): the final resolve stores every sample's exact incoming
+    // RI of entries 1..3 (exact_mode bit 0) and the next render's guesses copy them (bit 1), so
+    // a frame runs with no misprediction -- the bound any better guess could reach
+    float4 *exact = nullptr;
+    int exact_mode = 0;
 };
 enum { kSpecFirst = 0, kSpecRest = 1, kSpecList = 2 };
 
