@@ -9,7 +9,8 @@ every pixel, every sample, every bounce of the reference's IOW-03 render loop.
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Multi-GPU: the frame is cut into tiles dealt round-robin to the ranks (one process per GPU):
-16x16 tiles across ranks, 64x64 on one GPU (RT_BENCH_TILE overrides both).  Each rank renders
+16x16 tiles across ranks, in a hashed order (deal_order), 64x64 on one GPU (RT_BENCH_TILE
+overrides both).  Each rank renders
 its tiles into a packed buffer and the tiles are gathered to rank 0 with one RCCL gather over
 xGMI, where the image is assembled.  Total work is fixed, so the
 scaling mode is "strong".
@@ -69,18 +70,34 @@ def algorithmic_bytes(st: dict, pixels: int, inw: bool = False) -> float:
     return 32.0 * st["node_visits"] + 96.0 * st["prim_tests"] + 16.0 * pixels
 
 
+def deal_order(nx: int, ny: int, world: int):
+    """The order tiles are dealt in: row-major on one GPU; across ranks, row-major tiles permuted
+    by a multiplicative hash of their index.  A plain round-robin over rows gives rank r the
+    tile columns r, r+N, ... whenever the row length is a multiple of N (1920 px / 16 = 120
+    tiles), so a heavy vertical region (a glass sphere) lands on a few ranks."""
+    tiles = [(tx, ty) for ty in range(ny) for tx in range(nx)]
+    if world == 1:
+        return tiles
+    perm = sorted(range(len(tiles)), key=lambda i: ((i * 2654435761) & 0xFFFFFFFF, i))
+    return [tiles[i] for i in perm]
+
+
 def tiles_for_rank(W: int, H: int, world: int, rank: int, tile: int = TILE):
+    """(deal order of all tiles, this rank's tiles = order[rank::world], tiles per rank)."""
     nx, ny = math.ceil(W / tile), math.ceil(H / tile)
-    allt = [(tx, ty) for ty in range(ny) for tx in range(nx)]
-    return allt, allt[rank::world], math.ceil(len(allt) / world)
+    order = deal_order(nx, ny, world)
+    return order, order[rank::world], math.ceil(len(order) / world)
 
 
-def assemble_frame(src, n_tiles: int, nx: int, ny: int):
+def assemble_frame(src, order, nx: int, ny: int):
     """src: [world, per_rank, T, T, 4] packed tiles as gathered on rank 0, where tile t of rank r
-    is allt[r + world*t].  Returns the [ny*T, nx*T, 4] frame (crop to W x H)."""
+    is order[r + world*t].  Returns the [ny*T, nx*T, 4] frame (crop to W x H)."""
     T = src.shape[2]
-    order = src.permute(1, 0, 2, 3, 4).reshape(-1, T, T, 4)[:n_tiles]
-    return order.view(ny, nx, T, T, 4).permute(0, 2, 1, 3, 4).reshape(ny * T, nx * T, 4)
+    flat = src.permute(1, 0, 2, 3, 4).reshape(-1, T, T, 4)[:len(order)]
+    idx = torch.tensor([ty * nx + tx for tx, ty in order], dtype=torch.long, device=src.device)
+    grid = torch.empty((nx * ny, T, T, 4), dtype=src.dtype, device=src.device)
+    grid[idx] = flat
+    return grid.view(ny, nx, T, T, 4).permute(0, 2, 1, 3, 4).reshape(ny * T, nx * T, 4)
 
 
 def cpu_baseline(sc, threads: int, px: int) -> dict:
@@ -202,7 +219,7 @@ def main():
                     g_.copy_(h_)
         if rank == 0 and not shard:  # assemble the frame: tile t of rank r is allt[r + world*t]
             src = torch.stack(gathered, 0) if world > 1 else packed.unsqueeze(0)
-            image.copy_(assemble_frame(src, len(allt), nx, ny))
+            image.copy_(assemble_frame(src, allt, nx, ny))
 
     def barrier():
         if world > 1:

@@ -1,6 +1,7 @@
 """Multi-GPU partition + exchange, rehearsed on the CPU with gloo (world size 2 and 3).
 
-bench.py deals tiles round-robin to ranks (64x64 on one GPU, 16x16 across ranks), each rank packs its tiles, one gather brings
+bench.py deals tiles round-robin to ranks (64x64 on one GPU, 16x16 across ranks in a hashed
+order), each rank packs its tiles, one gather brings
 them to rank 0, and rank 0 assembles the frame.  Here every rank "renders" a
 deterministic per-pixel pattern into its packed tiles; the assembled frame must equal the
 pattern everywhere, and the tile lists must cover every tile exactly once.
@@ -45,7 +46,7 @@ def _worker(rank, world, port, W, H, T, q):
         dist.gather(packed, gathered, dst=0)
         if rank == 0:
             nx, ny = math.ceil(W / T), math.ceil(H / T)
-            img = bench.assemble_frame(torch.stack(gathered, 0), len(allt), nx, ny)[:H, :W]
+            img = bench.assemble_frame(torch.stack(gathered, 0), allt, nx, ny)[:H, :W]
             q.put(bool(torch.equal(img, ref)))
     finally:
         dist.destroy_process_group()
@@ -78,3 +79,13 @@ def test_tiles_cover_frame_once(world):
         seen += mine
     assert sorted(seen) == sorted(allt)
     assert len(set(seen)) == len(allt) == math.ceil(W / T) * math.ceil(H / T)
+
+
+def test_deal_order_spreads_columns():
+    """With 120 tiles per row (1920 px / 16) a row-major round-robin gives each of 8 ranks whole
+    tile columns; the hashed deal order gives every rank tiles from every column band."""
+    W, H, T, world = 1920, 1080, 16, 8
+    for r in range(world):
+        _, mine, _ = bench.tiles_for_rank(W, H, world, r, T)
+        cols = {tx for tx, _ in mine}
+        assert len(cols) > 100, (r, len(cols))
