@@ -277,6 +277,10 @@ int rt_debug_spec_list_stale(rt_dev_scene *s, uint64_t *out);
  * units) and dims = {P, S, list count, sequential-leftover count}. */
 int rt_debug_spec_dump(rt_dev_scene *s, uint32_t *rays_out, size_t cap, uint32_t *list_out, uint32_t list_cap,
                        uint32_t *dims);
+/* With RT_DEBUG_TIMES=1 set before the render: per (pixel unit, sample) record of the last
+ * sample-parallel IOW-03 render, start_out[s * P + pu] = launch of the sample's last start
+ * (bits 0-15) and its start count (bits 16-31), end_out = launch it finished in (synchronises). */
+int rt_debug_spec_times(rt_dev_scene *s, uint32_t *start_out, uint32_t *end_out, size_t cap);
 /* Main render kernel of the scene's last render and how many times it was launched (the
  * bench's per-launch roofline figures divide by this).  Returns the count; writes the name. */
 int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap);

@@ -133,6 +133,8 @@ struct rt_dev_scene {
     DevBuf sp_pstate;  // asynchronous windows: per-pixel frontier state
     DevBuf sp_front;   // checkpoint rounds: per-pixel frontier (uint4)
     DevBuf sp_sorder, sp_fcost;  // heavy-first enumeration: sample indices by cost, their costs
+    DevBuf sp_dbg_t;             // RT_DEBUG_TIMES diagnostics: per unit start / end launch
+    uint32_t launch_seq = 0;
     DevBuf sp_exact;             // RT_SPEC_ORACLE diagnostics: exact incoming state per sample
     size_t sp_exact_n = 0;
     bool sp_exact_valid = false;
@@ -413,7 +415,7 @@ bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
         s->sp_counts.alloc(64 * 64) != hipSuccess || s->sp_keys.alloc(n * 4) != hipSuccess ||
         s->sp_keys2.alloc(n * 4) != hipSuccess || s->sp_list2.alloc(n * 4) != hipSuccess ||
         s->sp_pstate.alloc(size_t(P) * 3 * sizeof(uint4)) != hipSuccess ||
-        s->sp_front.alloc(size_t(P) * sizeof(uint4)) != hipSuccess ||
+        s->sp_front.alloc(size_t(P) * 2 * sizeof(uint4)) != hipSuccess ||
         s->sp_sorder.alloc(size_t(S) * sizeof(uint32_t)) != hipSuccess ||
         s->sp_fcost.alloc(size_t(S) * sizeof(unsigned long long)) != hipSuccess ||
         s->sp_temp.alloc(s->sp_temp_bytes = rtk::sort_pairs_temp_bytes(n, 24)) != hipSuccess) {
@@ -565,7 +567,9 @@ hipError_t spec_launch(rt_dev_scene *s, const rtk::Frame &f, const rtk::IowScene
         hipError_t e = hipEventRecord(ev->first, st);
         if (e != hipSuccess) return e;
     }
-    hipError_t e = rtk::launch_iow03_spec(f, sc, R, mode, ct, n, counter, cap, st);
+    rtk::Cont c2 = ct;
+    c2.launch_id = s->launch_seq++;
+    hipError_t e = rtk::launch_iow03_spec(f, sc, R, mode, c2, n, counter, cap, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->second, st);
     return e;
 }
@@ -590,6 +594,21 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                           S > 2 && groups == 1 ? uint32_t(std::min(int(S) - 2, std::max(0, env_int("RT_SPEC_HEAVY",
                                                                                                   int(S - 1) / 20))))
                                                : 0u};
+    s->launch_seq = 0;
+    if (env_int("RT_DEBUG_TIMES", 0) != 0) {  // diagnostics only (rt_debug_spec_times)
+        const size_t n = size_t(P) * S * 2 * sizeof(uint32_t);
+        if (s->sp_dbg_t.bytes < n) {
+            s->sp_dbg_t.~DevBuf();
+            new (&s->sp_dbg_t) DevBuf();
+            HIP_OK(s->sp_dbg_t.alloc(n));
+        }
+        HIP_OK(hipMemsetAsync(s->sp_dbg_t.p, 0, n, st));
+        R.dbg_start = s->sp_dbg_t.as<uint32_t>();
+        R.dbg_end = R.dbg_start + size_t(P) * S;
+    }
+    R.front2 = s->sp_front.as<uint4>() + P;  // the anchored scan's secondary frontier
+    R.scan_max = uint32_t(std::max(0, env_int("RT_SPEC_SCAN", 128)));
+    if (R.scan_max == 0) R.front2 = nullptr;
     if (env_int("RT_SPEC_ORACLE", 0) != 0) {  // diagnostics only (see SpecRecs::exact)
         const size_t n = size_t(P) * S;
         if (s->sp_exact_n != n) {
@@ -664,6 +683,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // Budgeted tail rounds (RT_SPEC_TAIL_ROUNDS, RT_SPEC_TAIL_BUDGET segments each; DESIGN.md
     // "Budgeted tail"): the frontier advances between them, so mispredicted samples re-run while
     // the long ones still run instead of in a re-run pass after them.
+    // exact restarts go on down their pixel's chain of mispredicted samples (RT_SPEC_CHAIN)
+    const int chain = env_int("RT_SPEC_CHAIN", 1) != 0 ? 1 : 0;
     const int tail_budgeted =
         ckpt > 0 ? std::max(0, std::min(kCountSlots - 16 - ckpt - rounds, env_int("RT_SPEC_TAIL_ROUNDS", 60))) : 0;
     auto ckpt_pass = [&](const Lane &q, const rtk::SpecRecs &RG, uint32_t n_fresh) {
@@ -693,6 +714,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             ct.out = q.cont[r & 1].as<float4>();
             ct.out_count = q.cnt + 16 * r;
             ct.mixed = 1;
+            ct.chain = chain;
             ct.park_below = 65;  // park every busy lane once the queue drains
             ct.fresh_mode = plan[size_t(r)].mode;
             ct.fresh_lo = plan[size_t(r)].lo;
@@ -730,6 +752,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         for (int t = 0; t <= n_tail && e == hipSuccess; t++) {
             const int r = ckpt + t;
             rtk::Cont ct{};
+            ct.chain = chain;
             ct.in = q.cont[b].as<float4>();
             ct.in_count = q.cnt + 16 * (r - 1);
             if (t < n_tail) {
@@ -1120,6 +1143,16 @@ int rt_debug_spec_dump(rt_dev_scene *s, uint32_t *rays_out, size_t cap, uint32_t
     const uint32_t nl = std::min(cnt[0], list_cap);
     if (list_out && nl) HIP_OK(hipMemcpy(list_out, s->sp_list.p, size_t(nl) * 4, hipMemcpyDeviceToHost));
     dims[0] = P; dims[1] = S; dims[2] = cnt[0]; dims[3] = cnt[16];
+    return RT_OK;
+}
+
+int rt_debug_spec_times(rt_dev_scene *s, uint32_t *start_out, uint32_t *end_out, size_t cap) {
+    if (!s || !start_out || !end_out || !s->spec_cap || !s->spec_units || !s->sp_dbg_t.p) return RT_E_ARG;
+    const size_t n = size_t(s->spec_units) * (s->spec_cap / s->spec_units);
+    if (n > cap || s->sp_dbg_t.bytes < 2 * n * sizeof(uint32_t)) return RT_E_ARG;
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(start_out, s->sp_dbg_t.p, n * 4, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(end_out, static_cast<char *>(s->sp_dbg_t.p) + n * 4, n * 4, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

@@ -991,12 +991,15 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
     const unsigned started_tag = (1u << 9) | ((R.epoch & 0xffffu) << 16);  // heavy-first: taken, unfinished
     uint32_t useg = 0;  // segments of the current unit in this launch (ct.seg_budget)
+    // exact: the unit was (re)started with its exact incoming state (a frontier or fixf restart),
+    // so the state after it is exact too and the lane may go on down its pixel's chain
+    bool exact = false;
     // the lane's state at a segment boundary -> a continuation slot (13 float4)
     auto park = [&](float4 *p) {
         p[0] = make_float4(ubits(u), ibits(skip), ibits(K.size), ubits(K.wmask | (K.rmask << 4)));
         p[1] = make_float4(sample.x, sample.y, sample.z, ubits(urays));
         p[2] = make_float4(ubits(c.seg), ubits(c.nodes), ubits(c.prims), ubits(c.drops));
-        p[12] = make_float4(ubits(c.nans), 0.0f, 0.0f, 0.0f);  // .y: restart flag (k_iow03_fix)
+        p[12] = make_float4(ubits(c.nans), 0.0f, exact ? 1.0f : 0.0f, 0.0f);  // .y: restart flag (k_iow03_fix), .z: exact
         float *fl = reinterpret_cast<float *>(p + 3);
         for (int k = 0; k < kFl; k++) fl[k] = K.base[k * kBlock];
         if constexpr (NARROW)
@@ -1005,6 +1008,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     // start unit u (sample s of pixel pu) with assumed stack RI a.xyz in entries 1..3
     auto begin = [&](uint32_t u_, float4 a) {
         u = u_;
+        if (R.dbg_start) R.dbg_start[u] = (ct.launch_id & 0xffffu) | ((R.dbg_start[u] >> 16) + 1u) << 16;
         const uint32_t pu = u % R.P;
         const int s = (int)(u / R.P);
         const UnitPix px = unit_pixel(f, pu);
@@ -1052,6 +1056,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
             else if (q < nin && ct.in[(size_t)q * kContSlots + 12].y != 0.0f) {  // doomed while parked: restart exact
                 u = __float_as_uint(ct.in[(size_t)q * kContSlots].x);
                 begin(u, R.assume[u]);
+                exact = ct.chain != 0;
             } else if (q < nin) {  // resume a parked lane
                 const float4 *p = ct.in + (size_t)q * kContSlots;
                 const float4 m = p[0], a = p[1], b = p[2];
@@ -1060,6 +1065,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 sample = f3{a.x, a.y, a.z}; urays = __float_as_uint(a.w);
                 c.seg = __float_as_uint(b.x); c.nodes = __float_as_uint(b.y); c.prims = __float_as_uint(b.z);
                 c.drops = __float_as_uint(b.w); c.nans = __float_as_uint(p[12].x);
+                exact = p[12].z != 0.0f;
                 const float *fl = reinterpret_cast<const float *>(p + 3);
                 for (int k = 0; k < kFl; k++) K.base[k * kBlock] = fl[k];
                 if constexpr (NARROW)
@@ -1087,6 +1093,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 if (fresh && unit_pixel(f, u % R.P).in_image) {
                     if (ct.fresh_mode != 0) R.col[u].w = ubits(started_tag);
                     begin(u, mode == kSpecFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : R.assume[u]);
+                    exact = false;
                 }
             }
         }
@@ -1113,10 +1120,57 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
             }
         }
         if (busy && K.size == 0) {  // sample done: record it
-            R.col[u] = make_float4(sample.x, sample.y, sample.z, ubits(K.rmask | (K.wmask << 4) | done_tag));
+            R.col[u] = make_float4(sample.x, sample.y, sample.z,
+                                   ubits(K.rmask | (K.wmask << 4) | done_tag | ((ct.launch_id & 63u) << 10)));
             R.fin[u] = make_float4(K.at(1, 7), K.at(2, 7), K.at(3, 7), ubits(c.prims));
             R.ctr[u] = make_uint4(c.seg, c.drops, c.nans, c.nodes);
+            if (R.dbg_end) R.dbg_end[u] = ct.launch_id;
             busy = false;
+            if (exact) {
+                // Chain following: the stack this exact sample left is the exact incoming state of
+                // the next sample.  Walk the pixel's following finished samples while their
+                // assumptions hold on the entries they read; re-run the first one that does not,
+                // here and now, with the exact state.  A pixel whose samples all mispredict (each
+                // reads the entry its predecessor wrote) then runs down its chain on one lane,
+                // not one sample per frontier round.  Stops at an unfinished sample (running or
+                // queued elsewhere), which the frontier handles.
+                // Other lanes of this launch may write these records, so only records finished in
+                // an earlier launch (stable since that kernel boundary) are read, with
+                // device-coherent loads; a record is claimed for a re-run by a compare-and-swap of
+                // its flags, and a read whose flags changed meanwhile stops the walk.
+                const uint32_t pu = u % R.P;
+                uint32_t E1 = __float_as_uint(K.at(1, 7)), E2 = __float_as_uint(K.at(2, 7)),
+                         E3 = __float_as_uint(K.at(3, 7));
+                auto ld = [](const float *p) {
+                    return __hip_atomic_load(reinterpret_cast<const unsigned *>(p), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                };
+                for (uint32_t t = u / R.P + 1u; t < R.S; t++) {
+                    const uint32_t v = t * R.P + pu;
+                    unsigned *flp = reinterpret_cast<unsigned *>(&R.col[v].w);
+                    const unsigned fl = ld(&R.col[v].w);
+                    if ((fl & 0xffff0100u) != done_tag || ((fl >> 10) & 63u) == (ct.launch_id & 63u)) break;
+                    const unsigned rm = fl & 15u, wm = (fl >> 4) & 15u;
+                    const unsigned a1 = ld(&R.assume[v].x), a2 = ld(&R.assume[v].y), a3 = ld(&R.assume[v].z);
+                    const unsigned f1 = ld(&R.fin[v].x), f2 = ld(&R.fin[v].y), f3v = ld(&R.fin[v].z);
+                    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+                    if (ld(&R.col[v].w) != fl) break;
+                    if (((rm & 2u) && a1 != E1) || ((rm & 4u) && a2 != E2) || ((rm & 8u) && a3 != E3)) {
+                        unsigned expect = fl;
+                        if (!__hip_atomic_compare_exchange_strong(flp, &expect, started_tag, __ATOMIC_ACQ_REL,
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                            break;
+                        const float4 e = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
+                        R.assume[v] = e;
+                        begin(v, e);
+                        break;
+                    }
+                    if (wm & 2u) E1 = f1;
+                    if (wm & 4u) E2 = f2;
+                    if (wm & 8u) E3 = f3v;
+                }
+                exact = busy;
+            }
         }
     }
     if (c.wdbg && (threadIdx.x & 63) == 0)
@@ -1208,6 +1262,7 @@ __global__ __launch_bounds__(kBlock) void k_iow03_prep(Frame f, SpecRecs R, unsi
         for (uint32_t s = 1; s < R.S; s++) R.assume[(size_t)s * R.P + pu] = R.exact[(size_t)s * R.P + pu];
     if (R.front)  // sample 0 is exact: the frontier starts at sample 1 with its final entries
         R.front[pu] = make_uint4(1u, __float_as_uint(e0.x), __float_as_uint(e0.y), __float_as_uint(e0.z));
+    if (R.front2) R.front2[pu] = make_uint4(0xffffffffu, 0u, 0u, 0u);
     key[pu] = R.ctr[pu].x;
 }
 
@@ -1229,7 +1284,18 @@ __global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, 
     uint4 st = R.front[pu];
     if (st.x >= R.S) return;
     const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
+    // queue sample u for an exact re-run with incoming state E (its record is marked unfinished)
+    auto requeue = [&](size_t u, uint32_t e1, uint32_t e2, uint32_t e3) {
+        const uint32_t slot = atomicAdd(count, 1u);
+        if (slot >= cap) { atomicSub(count, 1u); return; }  // full: leave it to the resolve after the pass
+        R.assume[u] = make_float4(__uint_as_float(e1), __uint_as_float(e2), __uint_as_float(e3), 0.0f);
+        R.col[u].w = __uint_as_float((1u << 9) | ((R.epoch & 0xffffu) << 16));  // queued: unfinished
+        float4 *p = cont + (size_t)slot * kContSlots;
+        p[0] = make_float4(__uint_as_float((uint32_t)u), 0.0f, 0.0f, 0.0f);
+        p[12] = make_float4(0.0f, 1.0f, 0.0f, 0.0f);  // restart with the (now exact) assumption
+    };
     uint32_t s = st.x;
+    bool queued = false;
     for (; s < R.S; s++) {
         const size_t u = (size_t)s * R.P + pu;
         const unsigned fl = __float_as_uint(R.col[u].w);
@@ -1238,15 +1304,8 @@ __global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, 
         const unsigned rm = fl & 15u, wm = (fl >> 4) & 15u;
         if (((rm & 2u) && __float_as_uint(a.x) != st.y) || ((rm & 4u) && __float_as_uint(a.y) != st.z) ||
             ((rm & 8u) && __float_as_uint(a.z) != st.w)) {
-            const uint32_t slot = atomicAdd(count, 1u);
-            if (slot >= cap) atomicSub(count, 1u);  // full: leave it to the resolve after the pass
-            else {
-                R.assume[u] = make_float4(__uint_as_float(st.y), __uint_as_float(st.z), __uint_as_float(st.w), 0.0f);
-                R.col[u].w = __uint_as_float((1u << 9) | ((R.epoch & 0xffffu) << 16));  // queued: unfinished
-                float4 *p = cont + (size_t)slot * kContSlots;
-                p[0] = make_float4(__uint_as_float((uint32_t)u), 0.0f, 0.0f, 0.0f);
-                p[12] = make_float4(0.0f, 1.0f, 0.0f, 0.0f);  // restart with the (now exact) assumption
-            }
+            requeue(u, st.y, st.z, st.w);
+            queued = true;
             break;
         }
         const float4 fn = R.fin[u];
@@ -1256,6 +1315,50 @@ __global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, 
     }
     st.x = s;
     R.front[pu] = st;
+    // Anchored scan past the blocked sample s.  A finished sample that read no entry it had not
+    // written (rmask 0) is exact whatever came before it, and so are the entries it wrote; a
+    // finished sample whose reads are all of known entries is exact if its assumption matches
+    // them.  Knowledge of entries 1..3 is tracked from s + 1 on (none known at first); once all
+    // three are known, a mispredicted finished sample is re-queued at once with the exact state,
+    // and the first unfinished one is handed to k_iow03_fixf (front2).  The scan goes on past
+    // unfinished and mispredicted samples (knowledge restarts at the next anchor) up to
+    // scan_max samples past the frontier.  So a misprediction
+    // behind a long running sample is repaired without waiting for that sample (anchors --
+    // samples with rmask 0 that write all three entries -- are 18% of the samples of the bench
+    // scene, tests/analysis/fork_stats.py).
+    if (!R.front2) return;
+    uint4 f2 = make_uint4(0xffffffffu, 0u, 0u, 0u);
+    if (!queued && s < R.S) {
+        unsigned known = 0;
+        uint32_t E[4] = {0u, 0u, 0u, 0u};
+        const uint32_t k_end = min(R.S, s + 1u + R.scan_max);
+        for (uint32_t k = s + 1u; k < k_end; k++) {
+            const size_t u = (size_t)k * R.P + pu;
+            const unsigned fl = __float_as_uint(R.col[u].w);
+            if ((fl & 0xffff0100u) != done_tag) {  // unfinished: fixf may patch the first one
+                if (known == 14u && f2.x == 0xffffffffu) f2 = make_uint4(k, E[1], E[2], E[3]);
+                known = 0;  // its outputs are unknown; later anchors restore knowledge
+                continue;
+            }
+            const unsigned rm = fl & 14u, wm = (fl >> 4) & 14u;
+            if (rm & ~known) { known &= ~wm; continue; }  // read an unknown entry: its writes are unknown
+            const float4 a = R.assume[u];
+            const bool bad = ((rm & 2u) && __float_as_uint(a.x) != E[1]) ||
+                             ((rm & 4u) && __float_as_uint(a.y) != E[2]) ||
+                             ((rm & 8u) && __float_as_uint(a.z) != E[3]);
+            if (bad) {  // mispredicted: re-run it now if the whole state is known
+                if (known == 14u) requeue(u, E[1], E[2], E[3]);
+                known = 0;
+                continue;
+            }
+            const float4 fn = R.fin[u];
+            if (wm & 2u) E[1] = __float_as_uint(fn.x);
+            if (wm & 4u) E[2] = __float_as_uint(fn.y);
+            if (wm & 8u) E[3] = __float_as_uint(fn.z);
+            known |= wm;
+        }
+    }
+    R.front2[pu] = f2;
 }
 // Parked samples at their pixel's frontier: the exact incoming state E is known.  As in
 // k_iow03_fix: entries the sample neither read nor wrote get E; if an entry it read differs
@@ -1267,8 +1370,12 @@ __global__ __launch_bounds__(kBlock) void k_iow03_fixf(Frame f, SpecRecs R, floa
     if (p[12].y != 0.0f) return;  // a restart already
     const uint32_t u = __float_as_uint(p[0].x);
     const uint32_t pu = u % R.P, s = u / R.P;
-    const uint4 st = R.front[pu];
-    if (st.x != s) return;
+    uint4 st = R.front[pu];
+    if (st.x != s) {  // not at the frontier: past it, its exact state may come from the anchored scan
+        if (!R.front2) return;
+        st = R.front2[pu];
+        if (st.x != s) return;
+    }
     const unsigned E[3] = {st.y, st.z, st.w};
     const unsigned masks = __float_as_uint(p[0].w), wm = masks & 15u, rm = masks >> 4;
     float4 a = R.assume[u];

@@ -119,6 +119,14 @@ struct SpecRecs {
     // a frame runs with no misprediction -- the bound any better guess could reach
     float4 *exact = nullptr;
     int exact_mode = 0;
+    // checkpoint rounds: per pixel unit, the first unfinished sample past the main frontier whose
+    // exact incoming state the anchored scan of k_iow03_frontier found, and that state (x =
+    // 0xffffffff: none); k_iow03_fixf patches or restarts it like a sample at the frontier
+    uint4 *front2 = nullptr;
+    uint32_t scan_max = 0;  // samples the anchored scan may look past the main frontier (0 = off)
+    // diagnostics (RT_DEBUG_TIMES=1): per unit, the launch of its last start (bits 0-15) and its
+    // start count (bits 16-31), and the launch it finished in (rt_debug_spec_times)
+    uint32_t *dbg_start = nullptr, *dbg_end = nullptr;
 };
 enum { kSpecFirst = 0, kSpecRest = 1, kSpecList = 2 };
 
@@ -151,6 +159,8 @@ struct Cont {
     // min(solo_n, waves), an empty wave takes one unit and keeps it alone to the end, so
     // the longest samples run with the wave-cooperative closest hits instead of sharing a wave
     uint32_t solo_n;
+    uint32_t launch_id;  // sequence number of the launch in the frame (diagnostics)
+    int chain;           // exact restarts follow their pixel's chain of mispredicted samples
 };
 
 hipError_t launch_iow01(const Frame &f, hipStream_t s);

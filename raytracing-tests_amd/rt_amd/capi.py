@@ -131,6 +131,7 @@ SIGNATURES = {
     "rt_debug_spec_hist": (C.c_int, [C.c_void_p, C.c_void_p]),
     "rt_debug_launches": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
     "rt_debug_chunks": (C.c_int, [C.c_void_p]),
+    "rt_debug_spec_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
     "rt_debug_time_kernels": (C.c_int, [C.c_int]),
     "rt_debug_kernel_time": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "rt_debug_spec_pixels": (C.c_int, [C.c_void_p, _U32P, C.c_uint32]),

@@ -14,6 +14,10 @@
   left unwritten (default 2; 10^6 = never, with the former 10 re-run passes);
 - RT_SPEC_TAIL_ROUNDS=0/3: no budgeted tail rounds (the round-1 default) / three, with
   RT_SPEC_TAIL_BUDGET segments per unit and round (default 60 rounds of 3072);
+- RT_SPEC_SCAN=0/4: no anchored scan past the frontier (default 64 samples; DESIGN.md
+  "Anchored scan") / a short one;
+- RT_SPEC_CHAIN=0: exact restarts stop after their own sample (default: they go on down the
+  pixel's chain of mispredicted samples);
 - RT_SPEC_PRIOR_S0=1: the round-1 guess (entries sample 0 wrote keep its values from
   RT_SPEC_PRIOR_FROM on; default 0 guesses the prior for every entry);
 - RT_SPEC_GROUPS=2/7: pixel groups on separate streams;
@@ -64,7 +68,8 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
               "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_SPEC_GROUPS", "RT_IOW_ASYNC", "RT_SPEC_FIX",
               "RT_SPEC_VALIDATE", "RT_SPEC_PRIOR_FROM", "RT_COOP", "RT_IOW_LDS",
               "RT_SPEC_ROUNDS", "RT_SOLO", "RT_SPEC_HEAVY", "RT_SPEC_PRIOR_S0",
-              "RT_SPEC_TAIL_ROUNDS", "RT_SPEC_TAIL_BUDGET"):
+              "RT_SPEC_TAIL_ROUNDS", "RT_SPEC_TAIL_BUDGET", "RT_SPEC_SCAN",
+              "RT_SPEC_CHAIN"):
         env.pop(k, None)
     env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out, preset=scene[0], seed=scene[1], n_hint=scene[2])
@@ -106,6 +111,11 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     ({"RT_SPEC_PRIOR_S0": "1"}, 600, 400, 12),
     ({"RT_SPEC_PRIOR_S0": "1", "RT_SPEC_ROUNDS": "0"}, 300, 200, 16),
     ({"RT_SPEC_TAIL_ROUNDS": "0"}, 600, 400, 12),
+    ({"RT_SPEC_SCAN": "0"}, 600, 400, 12),
+    ({"RT_SPEC_CHAIN": "0"}, 600, 400, 12),
+    ({"RT_SPEC_CHAIN": "0", "RT_SPEC_SCAN": "0"}, 300, 200, 24),
+    ({"RT_SPEC_SCAN": "4", "RT_SPEC_TAIL_BUDGET": "32"}, 300, 200, 24),
+    ({"RT_SPEC_SCAN": "1000", "RT_SPEC_TAIL_BUDGET": "16", "RT_SPEC_ROUNDS": "6"}, 200, 100, 40),
     ({"RT_SPEC_TAIL_ROUNDS": "3", "RT_SPEC_TAIL_BUDGET": "64"}, 300, 200, 16),
     ({"RT_SPEC_TAIL_ROUNDS": "40", "RT_SPEC_TAIL_BUDGET": "16", "RT_SPEC_ROUNDS": "3"}, 300, 200, 16),
 ])

@@ -1,5 +1,6 @@
 """Diagnostic: the heaviest samples of one rank's share of an N-way tile partition and the chains
-they form inside their pixels.  python tools/chain_stats.py [r N]   (default 0 1 = whole frame)
+they form inside their pixels.  python tools/chain_stats.py [r N [W H spp]]   (default 0 1 = whole
+bench frame; W H spp: another resolution / sample count of the same scene)
 
 Renders the share once (as bench.py does), then reads rt_debug_spec_dump: the rays of every
 (pixel, sample) record (their last execution), the re-execution list after the pass, and the
@@ -21,7 +22,8 @@ from bench import tile_for, tiles_for_rank  # noqa: E402
 
 r, n = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (0, 1)
 lib = R.load()
-sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0)
+over = dict(zip(("width", "height", "spp"), (int(v) for v in sys.argv[3:6])))
+sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0, **over)
 W, H = sc.params.width, sc.params.height
 TILE = tile_for(n)
 _, mine, per_rank = tiles_for_rank(W, H, n, r, TILE)
