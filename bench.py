@@ -89,15 +89,39 @@ def tiles_for_rank(W: int, H: int, world: int, rank: int, tile: int = TILE):
     return order, order[rank::world], math.ceil(len(order) / world)
 
 
+def lpt_deal(costs, nx: int, ny: int, world: int):
+    """Tile lists per rank by longest-processing-time-first: tiles in decreasing measured cost
+    (ties: row-major index), each to the rank with the least cost so far (ties: lowest rank).
+    costs[ty * nx + tx] = rays the tile took in an earlier frame of the same view."""
+    import heapq
+    order = sorted(range(nx * ny), key=lambda i: (-float(costs[i]), i))
+    heap = [(0.0, r) for r in range(world)]
+    lists = [[] for _ in range(world)]
+    for i in order:
+        load, r = heapq.heappop(heap)
+        lists[r].append((i % nx, i // nx))
+        heapq.heappush(heap, (load + float(costs[i]), r))
+    return lists
+
+
+def assemble_lists(src, lists, nx: int, ny: int):
+    """src: [world, per_rank, T, T, 4] packed tiles as gathered on rank 0, where tile t of rank r
+    is lists[r][t].  Returns the [ny*T, nx*T, 4] frame (crop to W x H)."""
+    T = src.shape[2]
+    sel = [(r, t) for r, lst in enumerate(lists) for t in range(len(lst))]
+    rr = torch.tensor([a for a, _ in sel], dtype=torch.long, device=src.device)
+    tt = torch.tensor([b for _, b in sel], dtype=torch.long, device=src.device)
+    idx = torch.tensor([ty * nx + tx for lst in lists for tx, ty in lst], dtype=torch.long, device=src.device)
+    grid = torch.empty((nx * ny, T, T, 4), dtype=src.dtype, device=src.device)
+    grid[idx] = src[rr, tt]
+    return grid.view(ny, nx, T, T, 4).permute(0, 2, 1, 3, 4).reshape(ny * T, nx * T, 4)
+
+
 def assemble_frame(src, order, nx: int, ny: int):
     """src: [world, per_rank, T, T, 4] packed tiles as gathered on rank 0, where tile t of rank r
     is order[r + world*t].  Returns the [ny*T, nx*T, 4] frame (crop to W x H)."""
-    T = src.shape[2]
-    flat = src.permute(1, 0, 2, 3, 4).reshape(-1, T, T, 4)[:len(order)]
-    idx = torch.tensor([ty * nx + tx for tx, ty in order], dtype=torch.long, device=src.device)
-    grid = torch.empty((nx * ny, T, T, 4), dtype=src.dtype, device=src.device)
-    grid[idx] = flat
-    return grid.view(ny, nx, T, T, 4).permute(0, 2, 1, 3, 4).reshape(ny * T, nx * T, 4)
+    world = src.shape[0]
+    return assemble_lists(src, [order[r::world] for r in range(world)], nx, ny)
 
 
 def cpu_baseline(sc, threads: int, px: int) -> dict:
@@ -128,6 +152,9 @@ def main():
     ap.add_argument("--cpu-px", type=int, default=16, help="CPU baseline sample block size")
     ap.add_argument("--cpu-threads", type=int, default=16, help="host cores for the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--balance", action="store_true",
+                    help="multi-rank: deal the timed frames' tiles by LPT over the warm-up frame's tile costs "
+                         "(measured neutral on the 8-way frames: their time is set by long samples, not by rays)")
     ap.add_argument("--occupancy", action="store_true", help="report per-phase lane occupancy (diagnostic)")
     ap.add_argument("--save-image", default="", help="rank 0 saves the assembled frame (.npy) for checking")
     ap.add_argument("--config", default="c2", choices=("c2", "c4"),
@@ -168,12 +195,14 @@ def main():
         sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0, **over)
     W, H, spp = sc.params.width, sc.params.height, sc.params.spp
     T = tile_for(world)
-    allt, mine, per_rank = tiles_for_rank(W, H, world, rank, T)
+    nparts, part = world, rank  # partition size and this process's part
     shard = os.environ.get("RT_BENCH_SHARD", "")  # diagnostic "r/N": one process renders rank r's tiles of N
     if shard and world == 1:
-        sr, sn = (int(v) for v in shard.split("/"))
-        T = tile_for(sn)
-        allt, mine, per_rank = tiles_for_rank(W, H, sn, sr, T)
+        part, nparts = (int(v) for v in shard.split("/"))
+        T = tile_for(nparts)
+    nx, ny = math.ceil(W / T), math.ceil(H / T)
+    allt = deal_order(nx, ny, nparts)
+    lists = [allt[r::nparts] for r in range(nparts)]  # the hashed deal (first frame)
 
     if inw:
         scene = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, sc.layout, R.fptr(sc.nodes), None, 0, spp, local)
@@ -181,22 +210,30 @@ def main():
         scene = lib.rt_dev_scene_iow03(R.fptr(sc.types), R.fptr(sc.records), sc.n, spp, local)
     if not scene:
         raise RuntimeError("rt_dev_scene_iow03 failed (no gfx950 device?)")
-    d_tiles = torch.tensor(mine, dtype=torch.int32, device=dev).reshape(-1, 2).contiguous()
-    packed = torch.zeros((per_rank, T, T, 4), dtype=torch.float32, device=dev)
-    depth = torch.zeros((per_rank, T, T), dtype=torch.float32, device=dev) if inw else None  # INW's r32f image
     counters = torch.zeros(6, dtype=torch.int64, device=dev)
     dbg = torch.zeros(16, dtype=torch.int64, device=dev)
-    px_rays = torch.zeros(per_rank * T * T, dtype=torch.int32, device=dev)
+    buf = {}
+
+    def use_tiles(my_tiles, per_rank):
+        """(Re)allocate this rank's tile list and packed buffers (outside the timed region)."""
+        buf["mine"] = my_tiles
+        buf["d_tiles"] = torch.tensor(my_tiles, dtype=torch.int32, device=dev).reshape(-1, 2).contiguous()
+        buf["packed"] = torch.zeros((per_rank, T, T, 4), dtype=torch.float32, device=dev)
+        buf["depth"] = torch.zeros((per_rank, T, T), dtype=torch.float32, device=dev) if inw else None  # r32f image
+        buf["px_rays"] = torch.zeros(max(1, len(my_tiles)) * T * T, dtype=torch.int32, device=dev)
+        buf["gathered"] = [torch.empty_like(buf["packed"]) for _ in range(world)] if (world > 1 and rank == 0) else None
+
+    per_rank = max(len(v) for v in lists)
+    use_tiles(lists[part], per_rank)
     lib.rt_debug_time_kernels(1)
     if args.occupancy:
         lib.rt_debug_counters(dbg.data_ptr())
-        lib.rt_debug_pixel_rays(px_rays.data_ptr())
-    gathered = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
-    nx, ny = math.ceil(W / T), math.ceil(H / T)
     image = torch.empty((ny * T, nx * T, 4), dtype=torch.float32, device=dev) if rank == 0 else None
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     def step(i=None):
+        mine, d_tiles, packed, depth = buf["mine"], buf["d_tiles"], buf["packed"], buf["depth"]
+        gathered = buf["gathered"]
         stream = torch.cuda.current_stream()
         if i is not None:
             ev[i][0].record(stream)
@@ -217,9 +254,9 @@ def main():
             if rank == 0:
                 for g_, h_ in zip(gathered, hg):
                     g_.copy_(h_)
-        if rank == 0 and not shard:  # assemble the frame: tile t of rank r is allt[r + world*t]
+        if rank == 0 and not shard:  # assemble the frame: tile t of rank r is lists[r][t]
             src = torch.stack(gathered, 0) if world > 1 else packed.unsqueeze(0)
-            image.copy_(assemble_frame(src, allt, nx, ny))
+            image.copy_(assemble_lists(src, lists, nx, ny))
 
     def barrier():
         if world > 1:
@@ -229,9 +266,51 @@ def main():
                 dist.barrier(device_ids=[local])
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    def tile_costs():
+        """Rays per tile over the whole frame from the last rendered frame's per-pixel counts."""
+        mine = buf["mine"]
+        g = torch.zeros(nx * ny, dtype=torch.float64, device=dev)
+        if mine:
+            per = buf["px_rays"][:len(mine) * T * T].view(len(mine), T * T).sum(1).double()
+            idx = torch.tensor([ty * nx + tx for tx, ty in mine], dtype=torch.long, device=dev)
+            g[idx] = per
+        if world > 1:
+            if host_coll:
+                g = g.cpu()
+            dist.all_reduce(g)
+        return g.cpu().numpy()
+
+    # Load balance (multi-rank partitions, --balance; off by default): the warm-up
+    # frames record rays per pixel; the timed frames deal tiles by LPT over those per-tile costs
+    # (the view is static, so a frame's costs predict the next one's).  A shard-diagnostic
+    # process renders every tile in its warm-up to get them (cached in RT_BENCH_COSTS).
+    balance = nparts > 1 and args.balance and args.warmup > 0
+    costs = None
+    cache = os.environ.get("RT_BENCH_COSTS", "")
+    if balance and shard and cache and os.path.exists(cache):
+        costs = np.load(cache)
+    if balance and costs is None and shard:
+        use_tiles(allt, len(allt))
+    if balance and costs is None:
+        lib.rt_debug_pixel_rays(buf["px_rays"].data_ptr())
+    for w in range(args.warmup):
+        if balance and costs is None and w == args.warmup - 1:
+            buf["px_rays"].zero_()
         step()
     barrier()
+    if balance:
+        if costs is None:
+            costs = tile_costs()
+            if shard and cache:
+                np.save(cache, costs)
+        lib.rt_debug_pixel_rays(None)
+        lists = lpt_deal(costs, nx, ny, nparts)
+        per_rank = max(len(v) for v in lists)
+        use_tiles(lists[part], per_rank)
+        step()  # one frame on the final partition (first use of its buffers)
+        barrier()
+    if args.occupancy:
+        lib.rt_debug_pixel_rays(buf["px_rays"].data_ptr())
     counters.zero_()
     barrier()
     t0 = time.perf_counter()
@@ -337,6 +416,7 @@ def main():
             out["lane_occupancy"] = {name: round(d[2 * i + 1] / max(d[2 * i], 1) / 64, 4)
                                      for i, name in enumerate(("outer", "bvh_walk", "leaf_tests", "segments"))}
             out["wave_iterations"] = {name: d[2 * i] for i, name in enumerate(("outer", "bvh_walk", "leaf_tests", "segments"))}
+            px_rays = buf["px_rays"]
             pr = px_rays[px_rays > 0].double()
             q = torch.quantile(pr.float().cpu(), torch.tensor([0.5, 0.9, 0.99, 0.999])).tolist()
             out["pixel_rays"] = {"mean": round(float(pr.mean()), 1), "p50": q[0], "p90": q[1], "p99": q[2],

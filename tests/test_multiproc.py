@@ -89,3 +89,25 @@ def test_deal_order_spreads_columns():
         _, mine, _ = bench.tiles_for_rank(W, H, world, r, T)
         cols = {tx for tx, _ in mine}
         assert len(cols) > 100, (r, len(cols))
+
+
+def test_lpt_deal_balances_and_assembles():
+    """The LPT deal over measured tile costs covers every tile once, keeps the heaviest rank
+    within one tile's cost of the mean, and assemble_lists puts uneven per-rank lists back."""
+    W, H, T, world = 200, 130, 16, 3
+    nx, ny = math.ceil(W / T), math.ceil(H / T)
+    g = torch.Generator().manual_seed(5)
+    costs = (torch.rand(nx * ny, generator=g) ** 4 * 1000).tolist()
+    lists = bench.lpt_deal(costs, nx, ny, world)
+    flat = sorted(t for lst in lists for t in lst)
+    assert flat == sorted((tx, ty) for ty in range(ny) for tx in range(nx))
+    loads = [sum(costs[ty * nx + tx] for tx, ty in lst) for lst in lists]
+    assert max(loads) - sum(loads) / world <= max(costs)
+    ref = _pattern(W, H)
+    per = max(len(v) for v in lists)
+    src = torch.zeros((world, per, T, T, 4))
+    for r, lst in enumerate(lists):
+        for k, (tx, ty) in enumerate(lst):
+            blk = ref[ty * T:ty * T + T, tx * T:tx * T + T]
+            src[r, k, :blk.shape[0], :blk.shape[1]] = blk
+    assert torch.equal(bench.assemble_lists(src, lists, nx, ny)[:H, :W], ref)

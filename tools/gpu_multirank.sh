@@ -2,7 +2,7 @@
 # the assembled frames must be bit-identical
 set -o pipefail
 mkdir -p gpurun_out
-A="--steps 1 --warmup 0 --no-cpu-baseline --spp 8"
+A="--steps 1 --warmup 1 --no-cpu-baseline --spp 8 --balance"  # the timed frame uses the LPT deal
 timeout -k 10 300 python bench.py $A --save-image gpurun_out/mr_1.npy > gpurun_out/mr_1.json 2> gpurun_out/mr.err || exit 1
 RT_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 $A --save-image gpurun_out/mr_2.npy > gpurun_out/mr_2.json 2>> gpurun_out/mr.err || exit 1
 RT_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 3 $A --save-image gpurun_out/mr_3.npy > gpurun_out/mr_3.json 2>> gpurun_out/mr.err || exit 1

@@ -6,7 +6,7 @@ mkdir -p $O
 A="--width 1920 --height 1080 --spp 500 --steps 1 --warmup 1 --no-cpu-baseline"
 timeout -k 10 300 python bench.py $A > $O/n1.json 2> $O/n1.err || exit 1
 for r in 0 1 2 3 4 5 6 7; do
-  RT_BENCH_SHARD=$r/8 timeout -k 10 200 python bench.py $A > $O/b8_$r.json 2> $O/b8_$r.err || exit 1
+  RT_BENCH_COSTS=$O/costs_ns8.npy RT_BENCH_SHARD=$r/8 timeout -k 10 200 python bench.py $A > $O/b8_$r.json 2> $O/b8_$r.err || exit 1
 done
 python3 - <<'PY'
 import json
