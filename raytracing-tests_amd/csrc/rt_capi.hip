@@ -119,6 +119,8 @@ struct rt_dev_scene {
     DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
     DevBuf obox;  // IOW-03: per-object culling boxes (2 float4 each) for wave-cooperative queries
     DevBuf tex, tex_info;  // INW-04 material textures (float4 texels, (first, w, h, 0) per texture)
+    DevBuf wnodes, wrank, wleaf;  // INW wide walk: culling BVH, depth-first ranks, LBVH leaf nodes
+    uint32_t dfs_high = 0;
     uint32_t n_tex = 0;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
     uint32_t ws_units = 0;
@@ -280,6 +282,89 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
 
 int upload_textures(rt_dev_scene *s, const rt_texture *tex, int n_tex);
 
+// INW wide walk (DESIGN.md "INW wide walk").  The reference finds the closest hit by a
+// depth-first walk of its LBVH (01_BVH...glsl:431-473); the result is the nearest hit, ties to
+// the object the walk meets first, among the objects whose LBVH leaf box the ray crosses.  The
+// kernels find the same object with an ordered walk of a 4-wide culling BVH over the leaf boxes
+// (inflated to stay conservative), the reference's exact test on the leaf box, and a (t, rank)
+// rule with each object's rank in the reference's depth-first order.  That equivalence needs
+// the reference walk to drop no push on its shared 40-float stack: dfs_high is the walk's
+// stack high-water mark, and the kernels use the wide walk only while size + dfs_high <= 40.
+void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
+    if (!s->dfs_high) return;
+    sc.wnodes = s->wnodes.as<float4>();
+    sc.wroot = 1;
+    sc.rank = s->wrank.as<uint32_t>();
+    sc.leafnode = s->wleaf.as<uint32_t>();
+    sc.dfs_high = s->dfs_high;
+}
+
+int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
+    s->dfs_high = 0;
+    const char *off = std::getenv("RT_INW_FAST");
+    if (n < 2 || (off && off[0] == '0')) return RT_OK;
+    const uint32_t nn = 2 * n - 1;
+    std::vector<uint32_t> leaf(n, 0xffffffffu), rank(size_t(2) * n, 0);
+    for (uint32_t i = 0; i < nn; i++) {
+        const float left = nodes[size_t(i) * 8 + 6];
+        if (!(left > 0.1f)) {
+            const float g = -left;
+            if (!(g >= 0.0f) || g >= float(n)) return RT_OK;  // not a well-formed LBVH: exact walk only
+            leaf[uint32_t(g)] = i;
+        }
+    }
+    for (uint32_t g = 0; g < n; g++)
+        if (leaf[g] == 0xffffffffu) return RT_OK;
+    // depth-first order of the leaves and the stack high-water mark, both child orders
+    // (01_BVH...glsl:456-460: push(invert ? right : left), push(invert ? left : right))
+    uint32_t high = 0;
+    for (int inv = 0; inv < 2; inv++) {
+        std::vector<uint32_t> st{0};
+        uint32_t r = 0;
+        high = std::max<uint32_t>(high, 1);
+        while (!st.empty()) {
+            const uint32_t i = st.back();
+            st.pop_back();
+            const float left = nodes[size_t(i) * 8 + 6];
+            if (left > 0.1f) {
+                const uint32_t l = uint32_t(left), rr = l + 1;
+                if (rr >= nn) return RT_OK;
+                st.push_back(inv ? rr : l);
+                st.push_back(inv ? l : rr);
+                high = std::max<uint32_t>(high, uint32_t(st.size()));
+            } else {
+                rank[size_t(inv) * n + uint32_t(-left)] = r++;
+            }
+        }
+        if (r != n) return RT_OK;
+    }
+    // culling boxes: the leaf boxes, inflated as the IOW culling BVH's
+    std::vector<float> boxes(size_t(n) * 6);
+    for (uint32_t g = 0; g < n; g++) {
+        const float *b = nodes + size_t(leaf[g]) * 8;  // bbmin xyz, bbmax xyz
+        float big = 0.0f;
+        for (int k = 0; k < 6; k++) big = std::fmax(big, std::fabs(b[k]));
+        for (int k = 0; k < 3; k++) {
+            const float e = (b[3 + k] - b[k]) * 1e-3f + 1e-3f + big * 1e-5f;
+            boxes[size_t(g) * 6 + k] = b[k] - e;
+            boxes[size_t(g) * 6 + 3 + k] = b[3 + k] + e;
+        }
+    }
+    int depth = 0, depth4 = 0;
+    const std::vector<float> bin = rtamd::sah_build(boxes.data(), n, &depth);
+    std::vector<float> wide = rtamd::bvh4_collapse(bin, &depth4);
+    for (size_t w = 0; w < wide.size() / 32; w++)  // child links as int bits
+        for (int k = 0; k < 4; k++) {
+            const int link = int(wide[w * 32 + 24 + size_t(k)]);
+            std::memcpy(&wide[w * 32 + 24 + size_t(k)], &link, sizeof(link));
+        }
+    HIP_OK(s->wnodes.upload(wide.data(), wide.size() * sizeof(float)));
+    HIP_OK(s->wrank.upload(rank.data(), rank.size() * sizeof(uint32_t)));
+    HIP_OK(s->wleaf.upload(leaf.data(), leaf.size() * sizeof(uint32_t)));
+    s->dfs_high = high;
+    return RT_OK;
+}
+
 int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const float *nodes,
              const float *lights, uint32_t n_lights, const rt_texture *tex, int n_tex, int spp) {
     if (int rc = upload_textures(s, layout == 4 ? tex : nullptr, layout == 4 ? n_tex : 0); rc != RT_OK) return rc;
@@ -312,6 +397,7 @@ int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const f
     HIP_OK(s->hot.upload(hot.data(), hot.size() * sizeof(float)));
     HIP_OK(s->cold.upload(cold.data(), cold.size() * sizeof(float)));
     HIP_OK(s->nodes.upload(nodes, size_t(2 * n - 1) * 8 * sizeof(float)));
+    if (int rc = make_inw_wide(s, nodes, n); rc != RT_OK) return rc;
     if (s->n_lights) HIP_OK(s->lights.upload(lights, size_t(s->n_lights) * 7 * sizeof(float)));
     else HIP_OK(s->lights.alloc(16));
     set_residency(s);
@@ -532,6 +618,7 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                 rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
                                  s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>(),
                                  s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
+    set_wide(s, sc);
                 e = rtk::launch_inw(f, sc, ch, ct, n_units, s->counter.as<unsigned>(), s->blocks_cap, st);
             }
         }
@@ -903,6 +990,7 @@ int launch_scene_inw_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st, int ns
     rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
                      s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>(),
                      s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
+    set_wide(s, sc);
     const int cap = s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 7 : 6);
     const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
     hipError_t e = hipSuccess;

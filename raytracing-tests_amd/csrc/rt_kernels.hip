@@ -1596,6 +1596,190 @@ __device__ float inw_surrounding_ri(const InwScene &S, FStack &K, f3 hp, float r
     return acc;
 }
 
+// ---------------------------------------------------------------- INW wide walk
+// The reference's closest hit (01_BVH...glsl:431-473) is the nearest hit among the objects whose
+// LBVH leaf box its depth-first walk reaches, ties to the one it reaches first.  With finite ray
+// reciprocals the walk reaches every leaf whose own box test passes (an ancestor box holds the
+// leaf box, and the slab intervals are monotone in the planes), as long as its 40-float stack
+// drops no push -- guaranteed while size + dfs_high <= 40.  Under those conditions the ordered
+// walk of the 4-wide culling BVH below, the reference's test of the leaf box with the initial
+// limit, the exact object test and the (t, depth-first rank) rule pick the same object with the
+// same t; its normal and extra data are then computed as the reference computes them.  The
+// walk's stack lives in the free part of the shared stack above K.size.  Node and primitive
+// counters count this walk's own work.  ok = false: the conditions do not hold (or the walk's
+// stack overflowed) and the caller runs the reference walk.
+template <bool WANT_NORMAL>
+__device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
+                                   f3 &normal, float &extra, float init_geom, Ctr &c, bool &ok) {
+    const f3 id = f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};  // the reference's reciprocals (test_aabb)
+    ok = S.wnodes != nullptr && K.size + S.dfs_high <= (uint32_t)kFStack && __builtin_isfinite(id.x) &&
+         __builtin_isfinite(id.y) && __builtin_isfinite(id.z) && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
+    if (!__any(ok)) return init_geom;
+    const float tlim0 = tlim;
+    float bt = tlim0;
+    int bg = -1;
+    uint32_t br = 0xffffffffu;
+    const uint32_t *rank = S.rank + (invert ? S.n : 0u);
+    const f3 fid = f3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
+    const int base = (int)K.size, cap = kFStack - 3 - base;  // 3 spare slots for branch-free pushes
+    int sp = 0, pend = -1, cur = S.wroot;
+    bool walking = ok, ovf = false;
+    float lim = bt * 1.0001f + 1e-3f;
+    auto leaf = [&](int g) {
+        c.prims++;
+        const uint32_t ln = S.leafnode[g];
+        const float4 n0 = S.nodes[2 * ln], n1 = S.nodes[2 * ln + 1];
+        if (!test_aabb(n0, n1, o, id, tlim0)) return;
+        const Xf x = load_xf(S, g);
+        f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+        f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+        float t = -1.0f;
+        if (x.type == 1) t = t_ellipsoid(to, td, x.is);
+        else if (x.type == 2) t = t_cuboid(to, td, x.scale);
+        if (t > 0.0f && t < tlim0) {
+            const uint32_t r = rank[g];
+            if (t < bt || (t == bt && r < br)) { bt = t; bg = g; br = r; lim = bt * 1.0001f + 1e-3f; }
+        }
+    };
+    for (;;) {
+        if (walking) {
+            bool pop;
+            if (cur > 0) {
+                const float4 *nd = S.wnodes + 8 * (cur - 1);
+                const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], lk = nd[6];
+                c.nodes += 4;
+                float t0, t1, t2, t3;
+                cull4(lx, ly, lz, hx, hy, hz, o, fid, lim, t0, t1, t2, t3);
+                int k0 = __float_as_int(lk.x), k1 = __float_as_int(lk.y), k2 = __float_as_int(lk.z),
+                    k3 = __float_as_int(lk.w);
+                cswap(t0, k0, t1, k1); cswap(t2, k2, t3, k3);
+                cswap(t0, k0, t2, k2); cswap(t1, k1, t3, k3);
+                cswap(t1, k1, t2, k2);
+                int p = sp;  // branch-free pushes, farthest first (a miss is overwritten before a pop)
+                K.at((uint32_t)(base + p)) = __int_as_float(k3); p += t3 != kMiss;
+                K.at((uint32_t)(base + p)) = __int_as_float(k2); p += t2 != kMiss;
+                K.at((uint32_t)(base + p)) = __int_as_float(k1); p += t1 != kMiss;
+                if (p > cap) { ovf = true; p = cap; }
+                sp = p;
+                cur = k0;
+                pop = t0 == kMiss;
+            } else {
+                pop = pend < 0;  // a leaf waits while the lane still holds one
+                if (pop) pend = -cur;
+            }
+            if (pop) {
+                if (sp == 0) walking = false;
+                else cur = __float_as_int(K.at((uint32_t)(base + (--sp))));
+            }
+            if (ovf) walking = false;
+        }
+        if (__all(!walking || pend >= 0)) {
+            if (pend >= 0) { leaf(pend); pend = -1; }
+            if (__all(!walking)) break;
+        }
+    }
+    if (ovf) ok = false;
+    if (!ok) return init_geom;
+    if (bg < 0) return init_geom;
+    tlim = bt;
+    if (WANT_NORMAL) {
+        const Xf x = load_xf(S, bg);
+        f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+        f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+        f3 h = to + td * bt, nl;
+        if (x.type == 1) nl = normalize(f3{h.x * x.is2.x, h.y * x.is2.y, h.z * x.is2.z});
+        else if (x.type == 2) nl = cuboid_normal(h, x.scale);
+        else nl = f3{0, 0, 0};
+        normal = mul(x.R, nl);
+        extra = x.extra;
+    }
+    return (float)bg;
+}
+
+// The surrounding-RI walk (01_BVH...glsl:486-502) sums the RI of every object holding the point,
+// in its depth-first order (right child first).  Same conditions as above: the objects are those
+// whose leaf box holds the point (inclusive, as the reference compares) and whose inside test
+// passes, found by a walk of the culling BVH and summed in rank order.  ok = false: fall back.
+constexpr int kRiMax = 8;
+__device__ float inw_surrounding_ri_wide(const InwScene &S, FStack &K, f3 hp, float ratio, Ctr &c, bool &ok) {
+    ok = S.wnodes != nullptr && K.size + S.dfs_high <= (uint32_t)kFStack;
+    if (!__any(ok)) return 1.0f;
+    const int base = (int)K.size, cap = kFStack - 4 - base;
+    uint32_t rk[kRiMax];
+    float rv[kRiMax];
+    int nin = 0;
+    int sp = 0, cur = S.wroot;
+    bool walking = ok;
+    while (walking) {
+        if (cur > 0) {
+            const float4 *nd = S.wnodes + 8 * (cur - 1);
+            const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], lk = nd[6];
+            c.nodes += 4;
+            const bool i0 = hp.x >= lx.x && hp.x <= hx.x && hp.y >= ly.x && hp.y <= hy.x && hp.z >= lz.x && hp.z <= hz.x;
+            const bool i1 = hp.x >= lx.y && hp.x <= hx.y && hp.y >= ly.y && hp.y <= hy.y && hp.z >= lz.y && hp.z <= hz.y;
+            const bool i2 = hp.x >= lx.z && hp.x <= hx.z && hp.y >= ly.z && hp.y <= hy.z && hp.z >= lz.z && hp.z <= hz.z;
+            const bool i3 = hp.x >= lx.w && hp.x <= hx.w && hp.y >= ly.w && hp.y <= hy.w && hp.z >= lz.w && hp.z <= hz.w;
+            int p = sp;
+            K.at((uint32_t)(base + p)) = lk.x; p += i0;
+            K.at((uint32_t)(base + p)) = lk.y; p += i1;
+            K.at((uint32_t)(base + p)) = lk.z; p += i2;
+            K.at((uint32_t)(base + p)) = lk.w; p += i3;
+            if (p > cap) { ok = false; break; }
+            sp = p;
+        } else {
+            const int g = -cur;
+            c.prims++;
+            const uint32_t ln = S.leafnode[g];
+            const float4 n0 = S.nodes[2 * ln], n1 = S.nodes[2 * ln + 1];
+            if (hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z) {
+                const Xf x = load_xf(S, g);
+                f3 v = (hp - x.pos) + x.delta * (1.0f - ratio);
+                v = tmul(x.R, v);
+                v.x *= x.is.x; v.y *= x.is.y; v.z *= x.is.z;
+                bool inside;
+                if (x.type == 1) inside = dot(v, v) <= 1.0f;
+                else if (x.type == 2) inside = fabsf(v.x) <= 0.5f && fabsf(v.y) <= 0.5f && fabsf(v.z) <= 0.5f;
+                else inside = false;
+                if (inside) {
+                    if (nin == kRiMax) { ok = false; break; }
+                    rk[nin] = S.rank[g];
+                    rv[nin] = x.ri_acc;
+                    nin++;
+                }
+            }
+        }
+        if (sp == 0) walking = false;
+        else cur = __float_as_int(K.at((uint32_t)(base + (--sp))));
+    }
+    if (!ok) return 1.0f;
+    // sum in the reference's order (insertion sort by rank; a handful of objects at most)
+    for (int i = 1; i < nin; i++)
+        for (int j = i; j > 0 && rk[j] < rk[j - 1]; j--) {
+            const uint32_t tr = rk[j]; rk[j] = rk[j - 1]; rk[j - 1] = tr;
+            const float tv = rv[j]; rv[j] = rv[j - 1]; rv[j - 1] = tv;
+        }
+    float acc = 0.0f;
+    for (int i = 0; i < nin; i++) acc += rv[i];
+    if (acc > 1.0f) acc *= rcp((float)nin);
+    else acc = 1.0f;
+    return acc;
+}
+
+template <bool WANT_NORMAL>
+__device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
+                                             float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c) {
+    bool ok = false;
+    const float g = inw_traverse_wide<WANT_NORMAL>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c, ok);
+    if (ok) return g;
+    return inw_traverse<WANT_NORMAL>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
+}
+__device__ __forceinline__ float inw_ri(const InwScene &S, FStack &K, f3 hp, float ratio, Ctr &c) {
+    bool ok = false;
+    const float r = inw_surrounding_ri_wide(S, K, hp, ratio, c, ok);
+    if (ok) return r;
+    return inw_surrounding_ri(S, K, hp, ratio, c);
+}
+
 __device__ __forceinline__ bool is_lit_geom(const InwScene &S, uint32_t in) {  // 04...glsl:468-474
     bool r = false;
     for (uint32_t i = 0; i < S.n_lights && !r; i++) r = in == __float_as_uint(S.lights[i * 7 + 6]);
@@ -1704,7 +1888,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         const float tlim0 = mf0 ? K.at(4) : kMaxT;
         float tlim = tlim0, extra = 0.0f;
         f3 normal = f3{0, 0, 0};
-        float fg = inw_traverse<true>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
+        float fg = inw_closest<true>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
         const f3 hitpoint = co + cd * tlim;
         if (!(tlim < tlim0)) {
             if (mf0 && (int)(K.at(5) + 0.1f) < F.n_focus) {  // next focal lens, 01_BVH...glsl:506-528
@@ -1740,7 +1924,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
                 m_color = mulv(m_color, inw_tex_color(S, ti - 1u, tmul(R, hitpoint - mk(h0.x, h0.y, h0.z))));
             }
         }
-        const float surr = inw_surrounding_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
+        const float surr = inw_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
         if (mf0) K.size = 0;  // 01_BVH...glsl:544-549: the lens record goes after a primary hit
         if (LIGHTS) {  // 04...glsl:604-665
             uint32_t is_lit = S.n_lights > 0 ? 0u : (uint32_t)is_lit_geom(S, f2u(fg + 0.1f));
@@ -1753,7 +1937,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
                     f3 sd = normalize((bmin + (bmax - bmin) * ratio) - so);
                     c.shadow++;
                     f3 dummy_n; float dummy_e;
-                    float sg = inw_traverse<false>(S, K, so, sd, ratio, invert, sl, dummy_n, dummy_e, -1.0f, c);
+                    float sg = inw_closest<false>(S, K, so, sd, ratio, invert, sl, dummy_n, dummy_e, -1.0f, c);
                     is_lit += (uint32_t)is_lit_geom(S, f2u(sg + 0.1f));
                 }
                 const uint32_t nl = S.n_lights > 1 ? S.n_lights : 1u;

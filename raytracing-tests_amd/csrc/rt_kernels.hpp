@@ -68,6 +68,15 @@ struct InwScene {
     const float4 *tex;
     const int4 *tex_info;
     uint32_t n_tex;
+    // Wide walk (DESIGN.md "INW wide walk"; null wnodes = off): a 4-wide culling BVH over the
+    // LBVH leaf boxes, each object's rank in the reference's depth-first order for either child
+    // order (rank[g] with invert false, rank[n + g] with invert true), its LBVH leaf node, and the
+    // depth-first stack high-water mark (pushes can only drop when size + dfs_high > 40)
+    const float4 *wnodes = nullptr;
+    int wroot = 0;
+    const uint32_t *rank = nullptr;
+    const uint32_t *leafnode = nullptr;
+    uint32_t dfs_high = 0;
 };
 
 // One launch of a chunked render: samples [s_begin, s_end) of every pixel unit.  A pixel's

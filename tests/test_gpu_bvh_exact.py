@@ -28,7 +28,8 @@
 - RT_IOW_LDS=0: the BVH read from global memory instead of staged in LDS (768-lane blocks);
 - RT_COOP=0/64: no wave-cooperative closest hits / every closest hit wave-cooperative (default:
   waves with at most 4 tracing lanes);
-- INW: RT_INW_SPEC=0 (per-pixel sequential samples) and RT_SPEC_MAX_GB tiny (sample chunks).
+- INW: RT_INW_SPEC=0 (per-pixel sequential samples), RT_SPEC_MAX_GB tiny (sample chunks) and
+  RT_INW_FAST=0 (the reference's LBVH walk instead of the wide walk; images and ray counts equal).
 Each must give a bit-identical image of the final scene with identical ray counts.  The
 renders run in subprocesses because the switches are read by the library at scene build /
 launch time."""
@@ -69,7 +70,7 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
               "RT_SPEC_VALIDATE", "RT_SPEC_PRIOR_FROM", "RT_COOP", "RT_IOW_LDS",
               "RT_SPEC_ROUNDS", "RT_SOLO", "RT_SPEC_HEAVY", "RT_SPEC_PRIOR_S0",
               "RT_SPEC_TAIL_ROUNDS", "RT_SPEC_TAIL_BUDGET", "RT_SPEC_SCAN",
-              "RT_SPEC_CHAIN"):
+              "RT_SPEC_CHAIN", "RT_INW_FAST"):
         env.pop(k, None)
     env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out, preset=scene[0], seed=scene[1], n_hint=scene[2])
@@ -135,10 +136,16 @@ def test_strategies_bit_identical(tmp_path, gpu, over, w, h, spp):
     ({"RT_INW_SPEC": "0"}, INW1, 192, 108, 24),
     ({"RT_SPEC_MAX_GB": "0.005"}, INW1, 192, 108, 24),   # forces several sample chunks
     ({"RT_INW_SPEC": "0"}, INW4, 128, 128, 16),
+    ({"RT_INW_FAST": "0"}, INW1, 480, 270, 16),          # the reference's LBVH walk
+    ({"RT_INW_FAST": "0"}, INW4, 256, 256, 12),
+    ({"RT_INW_FAST": "0", "RT_INW_SPEC": "0"}, INW1, 192, 108, 24),
 ])
 def test_inw_strategies_bit_identical(tmp_path, gpu, over, scene, w, h, spp):
     a, sa = _render(tmp_path, {}, w, h, spp, scene)
     b, sb = _render(tmp_path, over, w, h, spp, scene)
     same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
     assert same.all(), np.argwhere(~same.all(axis=2))[:10].tolist()
-    assert sa == {**sb, "ms": sa["ms"]}
+    # the wide walk's node and primitive counts depend on which rays share a wave (postponed
+    # leaves are tested together), so only the ray-level counters must agree
+    for k in ("segments", "shadow_queries", "stack_drops", "nan_drops"):
+        assert sa[k] == sb[k], k

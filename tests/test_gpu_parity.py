@@ -38,9 +38,13 @@ def test_iow01_c1_matches_oracle(gpu):
     assert gst["segments"] == ost["segments"] == 400 * 225
 
 
+@pytest.mark.parametrize("wide", ["1", "0"])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_render_matches_oracle(gpu, name):
+def test_render_matches_oracle(gpu, name, wide, monkeypatch):
+    monkeypatch.setenv("RT_INW_FAST", wide)  # read by the library when it builds the device scene
     sc = CASES[name]()
+    if sc.stage == R.RT_STAGE_IOW03 and wide == "0":
+        pytest.skip("RT_INW_FAST only switches the INW walk")
     g, gd, gst = R.render(sc)
     o, od, ost = O.render(sc)
     c = _check(name, g, o)
@@ -48,9 +52,13 @@ def test_render_matches_oracle(gpu, name):
         _check(name + ":depth", gd, od)
     print(name, "gpu", {k: gst[k] for k in COUNTERS}, "ms %.2f" % gst["ms"])
     print(name, "cpu", {k: ost[k] for k in COUNTERS}, "ms %.2f" % ost["ms"])
-    # IOW-03 walks a culling BVH instead of the reference's linear object loop, so its node /
-    # primitive counts are its own; every ray-level counter must still match exactly.
-    exact = COUNTERS if sc.stage != R.RT_STAGE_IOW03 else ("segments", "shadow_queries", "stack_drops", "nan_drops")
+    # IOW-03 walks a culling BVH instead of the reference's linear object loop, and INW's wide
+    # walk (RT_INW_FAST, default on) a 4-wide culling BVH instead of the reference's LBVH walk, so
+    # their node / primitive counts are their own; every ray-level counter must still match
+    # exactly.  With RT_INW_FAST=0 the INW kernels walk the LBVH as the reference does, and the
+    # node and primitive counts match too.
+    own = sc.stage == R.RT_STAGE_IOW03 or wide == "1"
+    exact = ("segments", "shadow_queries", "stack_drops", "nan_drops") if own else COUNTERS
     for k in exact:
         assert gst[k] == ost[k], (k, gst[k], ost[k])
     assert c["exact_frac"] == 1.0, c

@@ -29,16 +29,22 @@ def test_iow00_matches_oracle(gpu, wh):
     _exact("iow00", R.render_iow00(p), O.render_iow00(p))
 
 
+@pytest.mark.parametrize("wide", ["1", "0"])
 @pytest.mark.parametrize("name", sorted(S.IOW02_CASES) + sorted(S.MF_CASES))
-def test_stage_matches_oracle(gpu, name):
+def test_stage_matches_oracle(gpu, name, wide, monkeypatch):
+    if name in S.IOW02_CASES and wide == "0":
+        pytest.skip("RT_INW_FAST only switches the INW walk")
+    monkeypatch.setenv("RT_INW_FAST", wide)  # the MULTIFOCUS cases run the INW kernels
     g, gd, gst = S.render_gpu(name)
     o, od, ost = S.render_oracle(name)
     _exact(name, g, o)
     if gd is not None:
         _exact(name + ":depth", gd, od)
     print(name, "gpu", {k: gst[k] for k in COUNTERS}, "cpu", {k: ost[k] for k in COUNTERS})
+    own = name in S.MF_CASES and wide == "1"  # the wide walk counts its own nodes and primitives
     for k in COUNTERS:
-        assert gst[k] == ost[k], (k, gst[k], ost[k])
+        if not (own and k in ("node_visits", "prim_tests")):
+            assert gst[k] == ost[k], (k, gst[k], ost[k])
 
 
 @pytest.mark.parametrize("name", S.GOLDEN_STAGE_CASES)
