@@ -98,7 +98,7 @@ def test_c5_full_size_properties(gpu):
     """C5 (configs[4], INW-04 Cornell box, 4096x4096, 2000 spp): the full frame renders with
     alpha 1, the depth image holds only the two values INW writes (0 on a hit, 32000 on a miss,
     01_BVH...glsl depth store), every pixel-sample casts at least one ray and the lights are
-    queried; repeat renders (at 64 spp) are bit-identical with identical counters."""
+    queried; repeat renders (at 64 spp) are bit-identical with identical ray counters."""
     W, H, spp = 4096, 4096, 2000
     sc = R.make_scene(R.PRESET_INW04_CORNELL, 7, 0, width=W, height=H, spp=spp)
     img, depth, st = R.render(sc)
@@ -112,4 +112,6 @@ def test_c5_full_size_properties(gpu):
     a, da, sa = R.render(sc, p)
     b, db, sb = R.render(sc, p)
     assert _same(a, b) and _same(da, db)
-    assert sa == {**sb, "ms": sa["ms"]}
+    # the wide walk's node / primitive counts depend on which rays share a wave; rays must agree
+    for k in ("segments", "shadow_queries", "stack_drops", "nan_drops"):
+        assert sa[k] == sb[k], k
