@@ -116,6 +116,12 @@ struct rt_dev_scene {
     int root_link = 0;   // IOW-03 culling BVH: leftData of the root
     uint32_t n_wide = 0; // IOW-03 culling BVH: 4-wide nodes
     float ri_prior = 1.0f;  // IOW-03: most common refractive index (sample-parallel guess)
+    // IOW-03 alternative runs: the values a stale ray-stack RI can hold (0 for a never-written
+    // entry, 1 for the camera ray, every material RI; 03...glsl:285-356), up to 8, else none
+    float alt_vals[8] = {};
+    int n_alt_vals = 0;
+    DevBuf sp_alt, sp_alt_hash, sp_alt_count;
+    uint32_t alt_cap = 0;
     int n_focus = 0;        // INW-01 MULTIFOCUS lens chain (0 = the reference's single focus)
     float focus[9] = {};
     DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
@@ -230,6 +236,16 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
             while (k < ri.size() && ri[k] == ri[i]) k++;
             if (k - i > best) { best = k - i; s->ri_prior = ri[i]; }
             i = k;
+        }
+        std::vector<float> vals{0.0f, 1.0f};
+        vals.insert(vals.end(), ri.begin(), ri.end());
+        std::sort(vals.begin(), vals.end());
+        vals.erase(std::unique(vals.begin(), vals.end(), [](float a, float b) {
+            return std::memcmp(&a, &b, sizeof(a)) == 0; }), vals.end());
+        s->n_alt_vals = 0;
+        if (vals.size() <= 8) {
+            for (size_t v = 0; v < vals.size(); v++) s->alt_vals[v] = vals[v];
+            s->n_alt_vals = int(vals.size());
         }
     }
     HIP_OK(s->hot.upload(hot.data(), hot.size() * sizeof(float)));
@@ -695,6 +711,30 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         R.dbg_start = s->sp_dbg_t.as<uint32_t>();
         R.dbg_end = R.dbg_start + size_t(P) * S;
     }
+    const bool alt_on = env_int("RT_SPEC_ALT", 1) != 0 && s->n_alt_vals > 1 && S > 1;
+    if (alt_on) {  // alternative runs (DESIGN.md "Alternative runs")
+        const uint32_t cap = uint32_t(std::max(1024, env_int("RT_SPEC_ALT_CAP", 1 << 17)));
+        if (s->alt_cap != cap) {
+            for (DevBuf *b : {&s->sp_alt, &s->sp_alt_hash, &s->sp_alt_count}) { b->~DevBuf(); new (b) DevBuf(); }
+            HIP_OK(s->sp_alt.alloc(size_t(cap) * sizeof(rtk::AltRec)));
+            HIP_OK(s->sp_alt_hash.alloc(size_t(cap) * 2 * sizeof(uint2)));
+            HIP_OK(s->sp_alt_count.alloc(64));
+            s->alt_cap = cap;
+        }
+        HIP_OK(hipMemsetAsync(s->sp_alt_hash.p, 0, size_t(cap) * 2 * sizeof(uint2), st));
+        HIP_OK(hipMemsetAsync(s->sp_alt_count.p, 0, 64, st));
+        R.alt = s->sp_alt.as<rtk::AltRec>();
+        R.alt_hash = s->sp_alt_hash.as<uint2>();
+        R.alt_count = s->sp_alt_count.as<unsigned>();
+        R.alt_cap = cap;
+        R.alt_hcap = cap * 2;
+        R.alt_min_seg = uint32_t(std::max(1, env_int("RT_SPEC_ALT_SEG", 16384)));
+        for (int v = 0; v < 8; v++) R.alt_vals[v] = s->alt_vals[v];
+        R.n_alt_vals = s->n_alt_vals;
+    }
+    // alternatives are spawned after the checkpoint rounds and, with RT_SPEC_ALT_EVERY = k > 0,
+    // after every k-th budgeted tail round too (measured: once is best on the bench frame)
+    const int alt_every = std::max(0, env_int("RT_SPEC_ALT_EVERY", 0));
     R.front2 = s->sp_front.as<uint4>() + P;  // the anchored scan's secondary frontier
     R.scan_max = uint32_t(std::max(0, env_int("RT_SPEC_SCAN", 128)));
     if (R.scan_max == 0) R.front2 = nullptr;
@@ -815,6 +855,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                                                  q.counter, cap_s, q.st);
             if (e == hipSuccess) e = rtk::launch_iow03_frontier(f, RG, ct.out, ct.out_count, cap_cont, q.st);
             if (e == hipSuccess) e = rtk::launch_iow03_fixf(f, RG, ct.out, ct.out_count, int(cap_cont), q.st);
+            if (e == hipSuccess && RG.alt && r == ckpt - 1)
+                e = rtk::launch_iow03_altspawn(f, RG, ct.out, ct.out_count, cap_cont, q.st);
             if (e == hipSuccess && r == 0 && r_heavy_end > 0)
                 e = rtk::launch_iow03_sample_order(f, RG, ct.out, ct.out_count, int(cap_cont),
                                                    s->sp_fcost.as<unsigned long long>(), s->sp_sorder.as<uint32_t>(),
@@ -860,6 +902,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             if (e == hipSuccess && t < tb) {
                 e = rtk::launch_iow03_frontier(f, RG, ct.out, ct.out_count, cap_cont, q.st);
                 if (e == hipSuccess) e = rtk::launch_iow03_fixf(f, RG, ct.out, ct.out_count, int(cap_cont), q.st);
+                if (e == hipSuccess && RG.alt && alt_every > 0 && t % alt_every == alt_every - 1)
+                    e = rtk::launch_iow03_altspawn(f, RG, ct.out, ct.out_count, cap_cont, q.st);
             }
             b ^= 1;
         }

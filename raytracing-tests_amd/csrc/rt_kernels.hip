@@ -942,6 +942,45 @@ void k_iow03n(Frame f, IowScene S, Chunk ch, Cont ct, unsigned *counter, int s_s
 // those entries (zeros in the first pass, else what the last resolve computed) and records
 // which entries it read before writing (rmask) and which it wrote (wmask); the resolve replays
 // the pixel in sample order and re-queues exactly the samples whose assumption was wrong.
+// ---------------------------------------------------------------- alternative runs
+// The slots (first, count) of unit u's alternative runs; count 0: none.  Open addressing over
+// alt_hcap entries, key u + 1.
+__device__ __forceinline__ uint2 alt_find(const SpecRecs &R, uint32_t u) {
+    if (!R.alt_hash) return make_uint2(0u, 0u);
+    uint32_t h = (u * 2654435761u) % R.alt_hcap;
+    for (uint32_t i = 0; i < R.alt_hcap; i++) {
+        const uint2 e = R.alt_hash[h];
+        if (e.x == 0u) break;
+        if (e.x == u + 1u) return make_uint2(e.y & 0xffffffu, e.y >> 24);
+        h = h + 1u == R.alt_hcap ? 0u : h + 1u;
+    }
+    return make_uint2(0u, 0u);
+}
+// A finished alternative run of u (finished in a launch other than `launch`, whose records are
+// stable) whose assumption holds on the entries it read under the exact state E: copied into
+// u's records, which then read as a finished exact execution (flags tagged with `tag_launch`).
+// Returns its slot + 1, or 0.
+__device__ uint32_t alt_adopt(const SpecRecs &R, uint32_t u, uint32_t E1, uint32_t E2, uint32_t E3, uint32_t launch,
+                              uint32_t tag_launch) {
+    const uint2 fk = alt_find(R, u);
+    for (uint32_t i = 0; i < fk.y; i++) {
+        const AltRec &A = R.alt[fk.x + i];
+        const uint32_t st = __hip_atomic_load(&A.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (st == 0u || st == launch + 1u) continue;
+        const unsigned fl = __float_as_uint(A.col.w), rm = fl & 15u;
+        if (((rm & 2u) && __float_as_uint(A.assume.x) != E1) || ((rm & 4u) && __float_as_uint(A.assume.y) != E2) ||
+            ((rm & 8u) && __float_as_uint(A.assume.z) != E3))
+            continue;
+        R.assume[u] = A.assume;
+        R.fin[u] = A.fin;
+        R.ctr[u] = A.ctr;
+        R.col[u] = make_float4(A.col.x, A.col.y, A.col.z,
+                               __uint_as_float((fl & ~(63u << 10)) | ((tag_launch & 63u) << 10)));
+        return fk.x + i + 1u;
+    }
+    return 0u;
+}
+
 template <bool NARROW, int SUB, bool LN>
 __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, const SpecRecs &R, int mode,
                                             const Cont &ct, unsigned *counter) {
@@ -994,12 +1033,14 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     // exact: the unit was (re)started with its exact incoming state (a frontier or fixf restart),
     // so the state after it is exact too and the lane may go on down its pixel's chain
     bool exact = false;
+    uint32_t alt_slot = 0;  // an alternative run: its slot + 1 (its record goes to R.alt)
     // the lane's state at a segment boundary -> a continuation slot (13 float4)
     auto park = [&](float4 *p) {
         p[0] = make_float4(ubits(u), ibits(skip), ibits(K.size), ubits(K.wmask | (K.rmask << 4)));
         p[1] = make_float4(sample.x, sample.y, sample.z, ubits(urays));
         p[2] = make_float4(ubits(c.seg), ubits(c.nodes), ubits(c.prims), ubits(c.drops));
-        p[12] = make_float4(ubits(c.nans), 0.0f, exact ? 1.0f : 0.0f, 0.0f);  // .y: restart flag (k_iow03_fix), .z: exact
+        // .y: restart flag (k_iow03_fix), .z: exact, .w: alternative slot + 1 (bits)
+        p[12] = make_float4(ubits(c.nans), 0.0f, exact ? 1.0f : 0.0f, ubits(alt_slot));
         float *fl = reinterpret_cast<float *>(p + 3);
         for (int k = 0; k < kFl; k++) fl[k] = K.base[k * kBlock];
         if constexpr (NARROW)
@@ -1053,10 +1094,17 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         if (solo_open && __ballot(want && q < solo_n) != 0) solo = true;
         if (want) {
             if (q >= total) live = false;
-            else if (q < nin && ct.in[(size_t)q * kContSlots + 12].y != 0.0f) {  // doomed while parked: restart exact
+            else if (q < nin && ct.in[(size_t)q * kContSlots + 12].y == 3.0f) {  // an alternative run
+                const uint32_t slot = __float_as_uint(ct.in[(size_t)q * kContSlots + 12].z);
+                u = __float_as_uint(ct.in[(size_t)q * kContSlots].x);
+                begin(u, R.alt[slot].assume);
+                exact = false;
+                alt_slot = slot + 1u;
+            } else if (q < nin && ct.in[(size_t)q * kContSlots + 12].y != 0.0f) {  // doomed while parked: restart exact
                 u = __float_as_uint(ct.in[(size_t)q * kContSlots].x);
                 begin(u, R.assume[u]);
                 exact = ct.chain != 0;
+                alt_slot = 0;
             } else if (q < nin) {  // resume a parked lane
                 const float4 *p = ct.in + (size_t)q * kContSlots;
                 const float4 m = p[0], a = p[1], b = p[2];
@@ -1066,6 +1114,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 c.seg = __float_as_uint(b.x); c.nodes = __float_as_uint(b.y); c.prims = __float_as_uint(b.z);
                 c.drops = __float_as_uint(b.w); c.nans = __float_as_uint(p[12].x);
                 exact = p[12].z != 0.0f;
+                alt_slot = __float_as_uint(p[12].w);
                 const float *fl = reinterpret_cast<const float *>(p + 3);
                 for (int k = 0; k < kFl; k++) K.base[k * kBlock] = fl[k];
                 if constexpr (NARROW)
@@ -1094,6 +1143,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                     if (ct.fresh_mode != 0) R.col[u].w = ubits(started_tag);
                     begin(u, mode == kSpecFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : R.assume[u]);
                     exact = false;
+                    alt_slot = 0;
                 }
             }
         }
@@ -1118,6 +1168,16 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 const uint32_t slot = park_slot(ct.out_count, over);
                 if (over) { park(ct.out + (size_t)slot * kContSlots); busy = false; }
             }
+        }
+        if (busy && K.size == 0 && alt_slot) {  // an alternative run done: its own record
+            AltRec &A = R.alt[alt_slot - 1u];
+            A.col = make_float4(sample.x, sample.y, sample.z, ubits(K.rmask | (K.wmask << 4) | done_tag));
+            A.fin = make_float4(K.at(1, 7), K.at(2, 7), K.at(3, 7), ubits(c.prims));
+            A.ctr = make_uint4(c.seg, c.drops, c.nans, c.nodes);
+            __threadfence();
+            __hip_atomic_store(&A.state, ct.launch_id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            busy = false;
+            alt_slot = 0;
         }
         if (busy && K.size == 0) {  // sample done: record it
             R.col[u] = make_float4(sample.x, sample.y, sample.z,
@@ -1160,6 +1220,15 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                         if (!__hip_atomic_compare_exchange_strong(flp, &expect, started_tag, __ATOMIC_ACQ_REL,
                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                             break;
+                        const uint32_t got = alt_adopt(R, v, E1, E2, E3, ct.launch_id, ct.launch_id);
+                        if (got) {  // an alternative run already holds its exact execution
+                            const AltRec &A = R.alt[got - 1u];
+                            const unsigned awm = (__float_as_uint(A.col.w) >> 4) & 15u;
+                            if (awm & 2u) E1 = __float_as_uint(A.fin.x);
+                            if (awm & 4u) E2 = __float_as_uint(A.fin.y);
+                            if (awm & 8u) E3 = __float_as_uint(A.fin.z);
+                            continue;
+                        }
                         const float4 e = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
                         R.assume[v] = e;
                         begin(v, e);
@@ -1188,7 +1257,7 @@ __global__ __launch_bounds__(kBlock) void k_iow03_fix(Frame f, SpecRecs R, float
     if (i >= *count) return;  // no cross-lane work in this kernel
     float4 *p = cont + (size_t)i * kContSlots;
     const uint32_t u = __float_as_uint(p[0].x);
-    if (p[12].y != 0.0f) return;
+    if (p[12].y != 0.0f || __float_as_uint(p[12].w) != 0u) return;  // a restart / an alternative run
     const uint32_t pu = u % R.P, s = u / R.P;
     const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
     unsigned E1 = 0, E2 = 0, E3 = 0;
@@ -1298,20 +1367,29 @@ __global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, 
     bool queued = false;
     for (; s < R.S; s++) {
         const size_t u = (size_t)s * R.P + pu;
-        const unsigned fl = __float_as_uint(R.col[u].w);
-        if ((fl & 0xffff0100u) != done_tag) break;  // still running (or queued)
+        unsigned fl = __float_as_uint(R.col[u].w);
+        if ((fl & 0xffff0100u) != done_tag) {  // still running (or queued): an alternative may hold it
+            if (!R.alt || !alt_adopt(R, (uint32_t)u, st.y, st.z, st.w, 0xffffffffu, 0u)) break;
+            fl = __float_as_uint(R.col[u].w);
+        }
         const float4 a = R.assume[u];
         const unsigned rm = fl & 15u, wm = (fl >> 4) & 15u;
         if (((rm & 2u) && __float_as_uint(a.x) != st.y) || ((rm & 4u) && __float_as_uint(a.y) != st.z) ||
             ((rm & 8u) && __float_as_uint(a.z) != st.w)) {
-            requeue(u, st.y, st.z, st.w);
-            queued = true;
-            break;
+            if (R.alt && alt_adopt(R, (uint32_t)u, st.y, st.z, st.w, 0xffffffffu, 0u)) {
+                fl = __float_as_uint(R.col[u].w);  // the adopted alternative is exact: go on
+            } else {
+                requeue(u, st.y, st.z, st.w);
+                queued = true;
+                break;
+            }
         }
+        const unsigned wm2 = (fl >> 4) & 15u;
+        (void)wm;
         const float4 fn = R.fin[u];
-        if (wm & 2u) st.y = __float_as_uint(fn.x);
-        if (wm & 4u) st.z = __float_as_uint(fn.y);
-        if (wm & 8u) st.w = __float_as_uint(fn.z);
+        if (wm2 & 2u) st.y = __float_as_uint(fn.x);
+        if (wm2 & 4u) st.z = __float_as_uint(fn.y);
+        if (wm2 & 8u) st.w = __float_as_uint(fn.z);
     }
     st.x = s;
     R.front[pu] = st;
@@ -1346,20 +1424,81 @@ __global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, 
             const bool bad = ((rm & 2u) && __float_as_uint(a.x) != E[1]) ||
                              ((rm & 4u) && __float_as_uint(a.y) != E[2]) ||
                              ((rm & 8u) && __float_as_uint(a.z) != E[3]);
-            if (bad) {  // mispredicted: re-run it now if the whole state is known
-                if (known == 14u) requeue(u, E[1], E[2], E[3]);
-                known = 0;
-                continue;
+            unsigned wmx = wm;
+            if (bad) {  // mispredicted: adopt an alternative, or re-run it now if the whole state is known
+                if (known == 14u && R.alt && alt_adopt(R, (uint32_t)u, E[1], E[2], E[3], 0xffffffffu, 0u)) {
+                    wmx = (__float_as_uint(R.col[u].w) >> 4) & 14u;
+                } else {
+                    if (known == 14u) requeue(u, E[1], E[2], E[3]);
+                    known = 0;
+                    continue;
+                }
             }
             const float4 fn = R.fin[u];
-            if (wm & 2u) E[1] = __float_as_uint(fn.x);
-            if (wm & 4u) E[2] = __float_as_uint(fn.y);
-            if (wm & 8u) E[3] = __float_as_uint(fn.z);
-            known |= wm;
+            if (wmx & 2u) E[1] = __float_as_uint(fn.x);
+            if (wmx & 4u) E[2] = __float_as_uint(fn.y);
+            if (wmx & 8u) E[3] = __float_as_uint(fn.z);
+            known |= wmx;
         }
     }
     R.front2[pu] = f2;
 }
+// Alternative runs (RT_SPEC_ALT, between tail rounds): for each pixel, every finished sample
+// past the frontier that read exactly one stale entry before writing it, traced at least
+// alt_min_seg segments and has no alternatives yet gets one run per other value that entry can
+// hold (R.alt_vals), queued as restart records with flag 3.  Such a sample is where a dependent
+// chain forms: if its guess was wrong, the frontier adopts the matching alternative instead of
+// re-running a long sample once the samples before it are done.
+__global__ __launch_bounds__(kBlock) void k_iow03_altspawn(Frame f, SpecRecs R, float4 *cont, unsigned *count,
+                                                           uint32_t cap) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = R.order_n ? R.order_n : R.P;
+    if (i >= n) return;  // no cross-lane work in this kernel
+    const uint32_t pu = R.order_n ? R.order[R.order_base + i] : i;
+    if (!unit_pixel(f, pu).in_image) return;
+    const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
+    for (uint32_t s = R.front[pu].x; s < R.S; s++) {
+        const uint32_t u = s * R.P + pu;
+        const unsigned fl = __float_as_uint(R.col[u].w);
+        if ((fl & 0xffff0100u) != done_tag) continue;
+        const unsigned rm = fl & 14u;
+        if (rm == 0u || (rm & (rm - 1u)) != 0u) continue;  // exactly one stale entry read
+        if (R.ctr[u].x < R.alt_min_seg) continue;
+        if (alt_find(R, u).y != 0u) continue;
+        const int e = rm == 2u ? 0 : (rm == 4u ? 1 : 2);
+        const float4 a = R.assume[u];
+        const float ae = e == 0 ? a.x : (e == 1 ? a.y : a.z);
+        uint32_t k = 0;
+        for (int v = 0; v < R.n_alt_vals; v++) k += __float_as_uint(R.alt_vals[v]) != __float_as_uint(ae);
+        if (k == 0u) continue;
+        const uint32_t first = atomicAdd(R.alt_count, k);
+        if (first + k > R.alt_cap) { atomicSub(R.alt_count, k); return; }
+        const uint32_t slot = atomicAdd(count, k);
+        if (slot + k > cap) { atomicSub(count, k); return; }  // leaves the claimed alt slots unused
+        uint32_t j = 0;
+        for (int v = 0; v < R.n_alt_vals; v++) {
+            if (__float_as_uint(R.alt_vals[v]) == __float_as_uint(ae)) continue;
+            AltRec &A = R.alt[first + j];
+            A.u = u;
+            A.state = 0u;
+            float4 b = a;
+            if (e == 0) b.x = R.alt_vals[v]; else if (e == 1) b.y = R.alt_vals[v]; else b.z = R.alt_vals[v];
+            A.assume = b;
+            float4 *p = cont + (size_t)(slot + j) * kContSlots;
+            p[0] = make_float4(__uint_as_float(u), 0.0f, 0.0f, 0.0f);
+            p[12] = make_float4(0.0f, 3.0f, __uint_as_float(first + j), 0.0f);  // start an alternative run
+            j++;
+        }
+        // publish u -> (first, k) in the hash (open addressing, key u + 1)
+        uint32_t h = (u * 2654435761u) % R.alt_hcap;
+        for (uint32_t t = 0; t < R.alt_hcap; t++) {
+            const unsigned prev = atomicCAS(&R.alt_hash[h].x, 0u, u + 1u);
+            if (prev == 0u) { R.alt_hash[h].y = first | (k << 24); break; }
+            h = h + 1u == R.alt_hcap ? 0u : h + 1u;
+        }
+    }
+}
+
 // Parked samples at their pixel's frontier: the exact incoming state E is known.  As in
 // k_iow03_fix: entries the sample neither read nor wrote get E; if an entry it read differs
 // from E it restarts with E.  Either way its assumption becomes exact.
@@ -1367,7 +1506,7 @@ __global__ __launch_bounds__(kBlock) void k_iow03_fixf(Frame f, SpecRecs R, floa
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= *count) return;  // no cross-lane work in this kernel
     float4 *p = cont + (size_t)i * kContSlots;
-    if (p[12].y != 0.0f) return;  // a restart already
+    if (p[12].y != 0.0f || __float_as_uint(p[12].w) != 0u) return;  // a restart already / an alternative run
     const uint32_t u = __float_as_uint(p[0].x);
     const uint32_t pu = u % R.P, s = u / R.P;
     uint4 st = R.front[pu];
@@ -1412,13 +1551,19 @@ __global__ __launch_bounds__(kBlock) void k_iow03_resolve(Frame f, SpecRecs R, i
     uint32_t s = 0;
     for (; work && s < R.S; s++) {
         const size_t u = (size_t)s * R.P + pu;
-        const float4 cl = R.col[u];
-        const uint32_t fl = __float_as_uint(cl.w), rm = fl & 15u, wm = (fl >> 4) & 15u;
-        const float4 a = R.assume[u];
+        float4 cl = R.col[u];
+        uint32_t fl = __float_as_uint(cl.w), rm = fl & 15u, wm = (fl >> 4) & 15u;
+        float4 a = R.assume[u];
         if (final_pass && R.exact && (R.exact_mode & 1) && first_bad < 0)
             R.exact[u] = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
-        const bool bad = ((rm & 2u) && __float_as_uint(a.x) != E1) || ((rm & 4u) && __float_as_uint(a.y) != E2) ||
-                         ((rm & 8u) && __float_as_uint(a.z) != E3);
+        bool bad = ((rm & 2u) && __float_as_uint(a.x) != E1) || ((rm & 4u) && __float_as_uint(a.y) != E2) ||
+                   ((rm & 8u) && __float_as_uint(a.z) != E3);
+        if (bad && first_bad < 0 && R.alt && alt_adopt(R, (uint32_t)u, E1, E2, E3, 0xffffffffu, 0u)) {
+            cl = R.col[u];  // an alternative run under the exact state: adopted
+            fl = __float_as_uint(cl.w); rm = fl & 15u; wm = (fl >> 4) & 15u;
+            a = R.assume[u];
+            bad = false;
+        }
         if (bad) {
             if (first_bad < 0) first_bad = (int)s;
             if (final_pass) break;  // the sequential kernel takes over from here
@@ -2659,6 +2804,13 @@ hipError_t launch_iow03_frontier(const Frame &f, const SpecRecs &R, float4 *cont
                                  hipStream_t s) {
     const uint32_t n = R.order_n ? R.order_n : R.P;
     hipLaunchKernelGGL(k_iow03_frontier, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, f, R, cont, count, cap);
+    return hipGetLastError();
+}
+hipError_t launch_iow03_altspawn(const Frame &f, const SpecRecs &R, float4 *cont, unsigned *count, uint32_t cap,
+                                 hipStream_t s) {
+    const uint32_t n = R.order_n ? R.order_n : R.P;
+    const unsigned blocks = (n + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_iow03_altspawn, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, cont, count, cap);
     return hipGetLastError();
 }
 hipError_t launch_iow03_fixf(const Frame &f, const SpecRecs &R, float4 *cont, const unsigned *count, int max_lanes,

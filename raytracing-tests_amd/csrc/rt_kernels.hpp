@@ -104,6 +104,13 @@ struct Chunk {
 // of entries 1..3 that earlier samples of the pixel left behind) and records what it read and
 // wrote; a resolve pass replays the pixel's samples in order and re-queues every sample whose
 // assumption was wrong.  Records are SoA over u.
+struct AltRec {  // an alternative run of a speculative sample (RT_SPEC_ALT, DESIGN.md "Alternative runs")
+    uint32_t u;      // unit (s * P + pu)
+    uint32_t state;  // 0 queued / running, else 1 + the launch it finished in
+    uint32_t pad0, pad1;
+    float4 assume, col, fin;
+    uint4 ctr;
+};
 struct SpecRecs {
     float4 *col;       // rgb of the sample, flags (bits: rmask 0-3, wmask 4-7)
     float4 *fin;       // RI of entries 1..3 after the sample, prim tests (bits)
@@ -136,6 +143,15 @@ struct SpecRecs {
     // diagnostics (RT_DEBUG_TIMES=1): per unit, the launch of its last start (bits 0-15) and its
     // start count (bits 16-31), and the launch it finished in (rt_debug_spec_times)
     uint32_t *dbg_start = nullptr, *dbg_end = nullptr;
+    // alternative runs: records, a hash u -> (first slot, count) with key u + 1 (0 = empty), the
+    // slot counter, the values a stale entry can hold, and the segment count that makes a
+    // sample long enough to get alternatives
+    AltRec *alt = nullptr;
+    uint2 *alt_hash = nullptr;
+    unsigned *alt_count = nullptr;
+    uint32_t alt_cap = 0, alt_hcap = 0, alt_min_seg = 0;
+    float alt_vals[8] = {};
+    int n_alt_vals = 0;
 };
 enum { kSpecFirst = 0, kSpecRest = 1, kSpecList = 2 };
 
@@ -238,6 +254,8 @@ hipError_t launch_iow03_sample_order(const Frame &f, const SpecRecs &R, const fl
                                      int max_lanes, unsigned long long *fcost, uint32_t *sorder, hipStream_t s);
 hipError_t launch_iow03_pixel_key(const Frame &f, const SpecRecs &R, const float4 *cont, const unsigned *count,
                                   int max_lanes, unsigned *key, hipStream_t s);
+hipError_t launch_iow03_altspawn(const Frame &f, const SpecRecs &R, float4 *cont, unsigned *count, uint32_t cap,
+                                 hipStream_t s);
 hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,
                              int keep_s0, hipStream_t s);
 // replay each pixel's samples: re-queue wrong assumptions; final: write clean pixels, hand

@@ -18,6 +18,8 @@
   "Anchored scan") / a short one;
 - RT_SPEC_CHAIN=0: exact restarts stop after their own sample (default: they go on down the
   pixel's chain of mispredicted samples);
+- RT_SPEC_ALT=0 / RT_SPEC_ALT_SEG small: no alternative runs / alternatives for almost every
+  sample that read a stale entry (default 4096 segments), so adoption runs often;
 - RT_SPEC_PRIOR_S0=1: the round-1 guess (entries sample 0 wrote keep its values from
   RT_SPEC_PRIOR_FROM on; default 0 guesses the prior for every entry);
 - RT_SPEC_GROUPS=2/7: pixel groups on separate streams;
@@ -70,7 +72,7 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
               "RT_SPEC_VALIDATE", "RT_SPEC_PRIOR_FROM", "RT_COOP", "RT_IOW_LDS",
               "RT_SPEC_ROUNDS", "RT_SOLO", "RT_SPEC_HEAVY", "RT_SPEC_PRIOR_S0",
               "RT_SPEC_TAIL_ROUNDS", "RT_SPEC_TAIL_BUDGET", "RT_SPEC_SCAN",
-              "RT_SPEC_CHAIN", "RT_INW_FAST"):
+              "RT_SPEC_CHAIN", "RT_INW_FAST", "RT_SPEC_ALT", "RT_SPEC_ALT_SEG", "RT_SPEC_ALT_EVERY"):
         env.pop(k, None)
     env.update(over)
     code = SCRIPT.format(root=ROOT, w=w, h=h, spp=spp, out=out, preset=scene[0], seed=scene[1], n_hint=scene[2])
@@ -114,6 +116,10 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     ({"RT_SPEC_TAIL_ROUNDS": "0"}, 600, 400, 12),
     ({"RT_SPEC_SCAN": "0"}, 600, 400, 12),
     ({"RT_SPEC_CHAIN": "0"}, 600, 400, 12),
+    ({"RT_SPEC_ALT": "0"}, 600, 400, 12),
+    ({"RT_SPEC_ALT_SEG": "8", "RT_SPEC_ALT_EVERY": "1", "RT_SPEC_TAIL_BUDGET": "64"}, 300, 200, 24),
+    ({"RT_SPEC_ALT_SEG": "1", "RT_SPEC_ALT_EVERY": "2", "RT_SPEC_TAIL_BUDGET": "16", "RT_SPEC_ROUNDS": "4",
+      "RT_SPEC_PRIOR_S0": "1"}, 200, 100, 40),
     ({"RT_SPEC_CHAIN": "0", "RT_SPEC_SCAN": "0"}, 300, 200, 24),
     ({"RT_SPEC_SCAN": "4", "RT_SPEC_TAIL_BUDGET": "32"}, 300, 200, 24),
     ({"RT_SPEC_SCAN": "1000", "RT_SPEC_TAIL_BUDGET": "16", "RT_SPEC_ROUNDS": "6"}, 200, 100, 40),
