@@ -127,7 +127,7 @@ struct rt_dev_scene {
     DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
     DevBuf obox;  // IOW-03: per-object culling boxes (2 float4 each) for wave-cooperative queries
     DevBuf tex, tex_info;  // INW-04 material textures (float4 texels, (first, w, h, 0) per texture)
-    DevBuf wnodes, wrank, wleaf;  // INW wide walk: culling BVH, depth-first ranks, LBVH leaf nodes
+    DevBuf wnodes, wrank, wleaf;  // INW wide walk: culling BVH, depth-first ranks, LBVH leaf boxes
     uint32_t dfs_high = 0;
     uint32_t n_tex = 0;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
@@ -313,7 +313,7 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     sc.wnodes = s->wnodes.as<float4>();
     sc.wroot = 1;
     sc.rank = s->wrank.as<uint32_t>();
-    sc.leafnode = s->wleaf.as<uint32_t>();
+    sc.leafbox = s->wleaf.as<float4>();
     sc.dfs_high = s->dfs_high;
 }
 
@@ -378,7 +378,9 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
         }
     HIP_OK(s->wnodes.upload(wide.data(), wide.size() * sizeof(float)));
     HIP_OK(s->wrank.upload(rank.data(), rank.size() * sizeof(uint32_t)));
-    HIP_OK(s->wleaf.upload(leaf.data(), leaf.size() * sizeof(uint32_t)));
+    std::vector<float> lbox(size_t(n) * 8);  // each object's LBVH leaf node, indexed by object
+    for (uint32_t g = 0; g < n; g++) std::memcpy(&lbox[size_t(g) * 8], nodes + size_t(leaf[g]) * 8, 8 * sizeof(float));
+    HIP_OK(s->wleaf.upload(lbox.data(), lbox.size() * sizeof(float)));
     s->dfs_high = high;
     return RT_OK;
 }

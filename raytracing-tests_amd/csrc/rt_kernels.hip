@@ -1772,10 +1772,9 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
     float lim = bt * 1.0001f + 1e-3f;
     auto leaf = [&](int g) {
         c.prims++;
-        const uint32_t ln = S.leafnode[g];
-        const float4 n0 = S.nodes[2 * ln], n1 = S.nodes[2 * ln + 1];
+        const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
+        const Xf x = load_xf(S, g);  // loaded with the box, before its test: one memory latency
         if (!test_aabb(n0, n1, o, id, tlim0)) return;
-        const Xf x = load_xf(S, g);
         f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
         f3 to = tmul(x.R, ov), td = tmul(x.R, d);
         float t = -1.0f;
@@ -1874,10 +1873,9 @@ __device__ float inw_surrounding_ri_wide(const InwScene &S, FStack &K, f3 hp, fl
         } else {
             const int g = -cur;
             c.prims++;
-            const uint32_t ln = S.leafnode[g];
-            const float4 n0 = S.nodes[2 * ln], n1 = S.nodes[2 * ln + 1];
+            const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
+            const Xf x = load_xf(S, g);  // loaded with the box, before its test
             if (hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z) {
-                const Xf x = load_xf(S, g);
                 f3 v = (hp - x.pos) + x.delta * (1.0f - ratio);
                 v = tmul(x.R, v);
                 v.x *= x.is.x; v.y *= x.is.y; v.z *= x.is.z;

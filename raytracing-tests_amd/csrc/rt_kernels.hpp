@@ -75,7 +75,7 @@ struct InwScene {
     const float4 *wnodes = nullptr;
     int wroot = 0;
     const uint32_t *rank = nullptr;
-    const uint32_t *leafnode = nullptr;
+    const float4 *leafbox = nullptr;  // per object: its LBVH leaf node (2 float4: the reference's leaf box)
     uint32_t dfs_high = 0;
 };
 
