@@ -229,15 +229,15 @@ __device__ __forceinline__ void iow_test(const IowScene &S, int j, f3 go, f3 gd,
 
 // Hit attributes of the winner `best` at min_t (LaunchRay's tail, 03...glsl:221-255): the
 // closest hit's normal and attributes are evaluated once after the search.
-// cold = the winner's cold record (colour3, material3, scatter2) when min_t < max_t
-__device__ __forceinline__ RayRet iow_eval_c(const IowScene &S, f3 go, f3 gd, float min_t, int best, float max_t,
-                                             float contrib, float4 c0, float4 c1) {
+// cold = the winner's cold record (colour3, material3, scatter2) when min_t < max_t;
+// td_id / nd_id = iow_id_dirs(gd), already computed by the search
+__device__ __forceinline__ RayRet iow_eval_c(const IowScene &S, f3 go, f3 gd, f3 td_id, f3 nd_id, float min_t, int best,
+                                             float max_t, float contrib, float4 c0, float4 c1) {
     RayRet r;
     if (min_t < max_t) {
         const float *hb = S.hot + (size_t)best * kIowHot;
         const IowObj ob = iow_obj(hb);
-        f3 td_id, nd_id, best_to, best_td, best_nd;
-        iow_id_dirs(gd, td_id, nd_id);
+        f3 best_to, best_td, best_nd;
         iow_local(hb, ob, go, gd, td_id, nd_id, best_to, best_td, best_nd);
         f3 h = best_to + best_nd * min_t;
         f3 n = ob.type == 2 ? f3{h.x * ob.is.x * ob.scale.x, h.y * ob.is.y * ob.scale.y, h.z * ob.is.z * ob.scale.z}
@@ -256,10 +256,20 @@ __device__ __forceinline__ RayRet iow_eval_c(const IowScene &S, f3 go, f3 gd, fl
             f3 mr = n_ * (s * k) + nn * k;
             refl = sel(dot(refl, n_) > dot(mr, n_), refl, mr);
         }
-        m3 inv = inverse(ob.M);
         r.point = go + gd * min_t;
-        r.normal = normalize(mul(inv, n));
-        r.reflected = normalize(mul(inv, refl));
+        if (hb[19] != 0.0f) {
+            // M is glm::mat3(1) (iow_local): inverse(M) is the constant the same formula gives
+            // for the identity, folded at compile time (IEEE folding keeps its signed zeros and
+            // the 0*x products of mul), so the bits are those of the general branch
+            const m3 I = m3{f3{1.0f, 0.0f, 0.0f}, f3{0.0f, 1.0f, 0.0f}, f3{0.0f, 0.0f, 1.0f}};
+            const m3 inv = inverse(I);
+            r.normal = normalize(mul(inv, n));
+            r.reflected = normalize(mul(inv, refl));
+        } else {
+            const m3 inv = inverse(ob.M);
+            r.normal = normalize(mul(inv, n));
+            r.reflected = normalize(mul(inv, refl));
+        }
         r.color = r.color * contrib;
     } else {
         r.point = f3{0, 0, 0}; r.normal = f3{0, 0, 0};
@@ -268,14 +278,14 @@ __device__ __forceinline__ RayRet iow_eval_c(const IowScene &S, f3 go, f3 gd, fl
     }
     return r;
 }
-__device__ __forceinline__ RayRet iow_eval(const IowScene &S, f3 go, f3 gd, float min_t, int best, float max_t,
-                                           float contrib) {
+__device__ __forceinline__ RayRet iow_eval(const IowScene &S, f3 go, f3 gd, f3 td_id, f3 nd_id, float min_t, int best,
+                                           float max_t, float contrib) {
     float4 c0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), c1 = c0;
     if (min_t < max_t) {
         const float4 *cold = reinterpret_cast<const float4 *>(S.cold + (size_t)best * kIowCold);
         c0 = cold[0]; c1 = cold[1];
     }
-    return iow_eval_c(S, go, gd, min_t, best, max_t, contrib, c0, c1);
+    return iow_eval_c(S, go, gd, td_id, nd_id, min_t, best, max_t, contrib, c0, c1);
 }
 
 // LaunchRay 03...glsl:196-256.  The reference loops over every object and keeps the first
@@ -366,7 +376,7 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
     } else {
         for (uint32_t j = 0; j < S.n; j++) test((int)j);  // also the path for zero / NaN directions
     }
-    RayRet r = iow_eval(S, go, gd, min_t, best, max_t, contrib);
+    RayRet r = iow_eval(S, go, gd, td_id, nd_id, min_t, best, max_t, contrib);
     DBG_CYC(F_, c, kDbgCycRay, t_ray);
     return r;
 }
@@ -647,7 +657,10 @@ __device__ __forceinline__ void iow_seg_step(const IowScene &S, const Frame &F, 
     DBG_T0(F, t_sh);
     if (seg) {
         c.seg++; c.nodes += my_box; c.prims += my_prim;
-        const RayRet data = iow_eval_c(S, in.co, in.cd, my_t, my_j, 32000.0f, in.contribution, my_c0, my_c1);
+        f3 td_id, nd_id;
+        iow_id_dirs(in.cd, td_id, nd_id);
+        const RayRet data =
+            iow_eval_c(S, in.co, in.cd, td_id, nd_id, my_t, my_j, 32000.0f, in.contribution, my_c0, my_c1);
         iow_seg_shade(S, F, K, skip, sample, sidx, c, in, data);
     }
     DBG_CYC(F, c, kDbgCycSpare1, t_sh);

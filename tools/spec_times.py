@@ -57,5 +57,16 @@ out = {"share": f"{r}/{n}", "P": P, "S": S, "launches": nk.value, "relist": nl, 
 late = np.nonzero(t1 >= t1.max() - 3)[0]
 out["finished_last"] = [{"pu": int(i % P), "s": int(i // P), "rays": int(rays[i]), "start": int(t0[i] & 0xffff),
                          "starts": int(t0[i] >> 16), "end": int(t1[i])} for i in late[np.argsort(-rays[late].astype(np.int64))][:15]]
+# units in flight per launch (started at or before it, finished at or after it), and how many
+# of them are long (> 10k rays)
+st_l, en_l = (t0 & 0xffff).astype(np.int64), t1.astype(np.int64)
+ok = (t1 > 0) | (st_l > 0)
+alive, heavy = [], []
+for L in range(int(t1.max()) + 1):
+    a = ok & (st_l <= L) & (en_l >= L)
+    alive.append(int(a.sum()))
+    heavy.append(int((a & (rays > 10000)).sum()))
+out["alive_per_launch"] = alive
+out["alive_long_per_launch"] = heavy
 print(json.dumps(out))
 lib.rt_dev_scene_free(scene)
