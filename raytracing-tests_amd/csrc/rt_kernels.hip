@@ -252,7 +252,7 @@ __device__ __forceinline__ RayRet iow_eval_c(const IowScene &S, f3 go, f3 gd, f3
             f3 nir = normalize(cross(n_, best_td));
             f3 nn = normalize(cross(nir, n_));
             float s = r.scat1;
-            float k = 1.0f / __builtin_sqrtf(1.0f + s * s);
+            float k = rcp_sqrt_domain(__builtin_sqrtf(1.0f + s * s));
             f3 mr = n_ * (s * k) + nn * k;
             refl = sel(dot(refl, n_) > dot(mr, n_), refl, mr);
         }
@@ -1675,7 +1675,7 @@ __device__ float inw_traverse(const InwScene &S, FStack &K, f3 o, f3 d, float ra
                               float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c) {
     float final_geom = init_geom;
     const uint32_t I = K.size;
-    const f3 id = f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};
     K.push(0.0f, c);
     for (;;) {
         float geom = -1.0f;
@@ -1769,7 +1769,7 @@ __device__ float inw_surrounding_ri(const InwScene &S, FStack &K, f3 hp, float r
 template <bool WANT_NORMAL>
 __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
                                    f3 &normal, float &extra, float init_geom, Ctr &c, bool &ok) {
-    const f3 id = f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};  // the reference's reciprocals (test_aabb)
+    const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};  // the reference's reciprocals (test_aabb)
     ok = S.wnodes != nullptr && K.size + S.dfs_high <= (uint32_t)kFStack && __builtin_isfinite(id.x) &&
          __builtin_isfinite(id.y) && __builtin_isfinite(id.z) && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
     if (!__any(ok)) return init_geom;
@@ -1971,7 +1971,7 @@ __device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame 
         const float first_limit = F.focus_list[0] * 0.5f;
         const f3 nd = normalize((cd * first_limit + rr * ox) + ru * oy);
         const f3 rn = normalize((-rr) * ox - ru * oy);
-        const float mult = 1.0f / dot(cd, nd);
+        const float mult = rcp(dot(cd, nd));
         K.push(rn.x, c); K.push(rn.y, c); K.push(rn.z, c);
         K.push(mult, c); K.push(first_limit, c); K.push(0.0f, c);
         K.push_ray(co, nd, 1.0f, 0.0f, c);
@@ -2868,4 +2868,24 @@ hipError_t launch_inw(const Frame &f, const InwScene &sc, const Chunk &ch, const
     return hipGetLastError();
 }
 
+}  // namespace rtk
+
+namespace rtk {
+// rcp_sqrt_domain(sqrt(x)) against the compiler's correctly rounded 1.0f / sqrt(x) over every
+// bit pattern x (NaN == NaN)
+__global__ __launch_bounds__(kBlock) void k_check_rcp(unsigned long long *bad, unsigned *first) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < (1ull << 32); i += stride) {
+        const float b = __builtin_sqrtf(__uint_as_float((uint32_t)i));
+        const float x = rcp_sqrt_domain(b), y = 1.0f / b;
+        if (__float_as_uint(x) != __float_as_uint(y) && !(x != x && y != y)) {
+            atomicAdd(bad, 1ull);
+            atomicMin(first, (uint32_t)i);
+        }
+    }
+}
+hipError_t launch_check_rcp(unsigned long long *bad, unsigned *first, hipStream_t s) {
+    hipLaunchKernelGGL(k_check_rcp, dim3(4096), dim3(kBlock), 0, s, bad, first);
+    return hipGetLastError();
+}
 }  // namespace rtk

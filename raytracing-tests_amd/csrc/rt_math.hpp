@@ -25,8 +25,21 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
 __device__ __forceinline__ float rcp(float b) { return 1.0f / b; }
+// RN(1/s) for s = RN(sqrt(x)) of a float x, i.e. s in [2^-75, 2^64] or 0, +inf, NaN.  The
+// compiler's correctly rounded 1.0f / s is div_scale x2, rcp, five fma, div_fmas and div_fixup;
+// the div_scale steps only rescale operands whose reciprocal could leave the normal range (not
+// the case on this domain), where div_fmas is a plain fma.  This is the same arithmetic without
+// them; rt_debug_check_rcp compares it with 1.0f / sqrt(x) for all 2^32 x on the device
+// (tests/test_gpu_fastmath.py).  Outside the domain (denormal or huge s) it is not exact.
+__device__ __forceinline__ float rcp_sqrt_domain(float s) {
+    const float r0 = __builtin_amdgcn_rcpf(s);
+    const float r = __builtin_fmaf(__builtin_fmaf(-s, r0, 1.0f), r0, r0);
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-s, r, 1.0f), r, r);
+    const float q2 = __builtin_fmaf(__builtin_fmaf(-s, q1, 1.0f), r, q1);
+    return __builtin_amdgcn_div_fixupf(q2, s, 1.0f);
+}
 __device__ __forceinline__ float len(f3 v) { return __builtin_sqrtf(dot(v, v)); }
-__device__ __forceinline__ f3 normalize(f3 v) { return v * (1.0f / __builtin_sqrtf(dot(v, v))); }
+__device__ __forceinline__ f3 normalize(f3 v) { return v * rcp_sqrt_domain(__builtin_sqrtf(dot(v, v))); }
 __device__ __forceinline__ float get(f3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
 
 // column-major 3x3 (GLSL mat3 / glm::mat3), c0..c2 columns
@@ -93,7 +106,7 @@ __device__ __forceinline__ float t_ellipsoid(f3 o, f3 d, f3 is) {
     float det = hb * hb - a * c;
     float t = -1.0f;
     if (det > 0.0f) {
-        float ia = 1.0f / a, sq = __builtin_sqrtf(det);
+        float ia = rcp(a), sq = __builtin_sqrtf(det);
         float t0 = (-hb - sq) * ia, t1 = (-hb + sq) * ia;
         t = (t0 > t1 || t0 < 0.0f) ? t1 : t0;
     }
@@ -101,14 +114,14 @@ __device__ __forceinline__ float t_ellipsoid(f3 o, f3 d, f3 is) {
 }
 __device__ __forceinline__ float t_cuboid(f3 o, f3 d, f3 s) {
     f3 bmin = (-s) * 0.5f, bmax = s * 0.5f;
-    float id = 1.0f / d.x;
+    float id = rcp(d.x);
     float t1 = (bmin.x - o.x) * id, t2 = (bmax.x - o.x) * id;
     float tmin = fminf(t1, t2), tmax = fmaxf(t1, t2);
-    id = 1.0f / d.y;
+    id = rcp(d.y);
     t1 = (bmin.y - o.y) * id; t2 = (bmax.y - o.y) * id;
     tmin = fmaxf(tmin, fminf(fminf(t1, t2), tmax));
     tmax = fminf(tmax, fmaxf(fmaxf(t1, t2), tmin));
-    id = 1.0f / d.z;
+    id = rcp(d.z);
     t1 = (bmin.z - o.z) * id; t2 = (bmax.z - o.z) * id;
     tmin = fmaxf(tmin, fminf(fminf(t1, t2), tmax));
     tmax = fminf(tmax, fmaxf(fmaxf(t1, t2), tmin));
