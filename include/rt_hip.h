@@ -293,11 +293,11 @@ int rt_debug_chunks(rt_dev_scene *s);
  * stream; rt_debug_kernel_time returns the summed durations and the launch count of the
  * scene's last render (waits for it). */
 int rt_debug_time_kernels(int on);
-/* Numerics self-check: the short reciprocal that normalize() uses (rt_math.hpp
- * rcp_sqrt_domain, the contract's RN(1/RN(sqrt(x)))) against the compiler's correctly rounded
- * 1.0f / sqrtf(x) for all 2^32 x.  Writes the mismatch count and the lowest mismatching x
- * (0xffffffff if none); synchronous. */
-int rt_debug_check_rcp(uint64_t *mismatches, uint32_t *first_bad);
+/* Numerics self-check of the shortened correctly rounded sequences in rt_math.hpp against the
+ * compiler's, for all 2^32 float bit patterns x: which 0 = rcp_sqrt_domain(sqrtf(x)) (the
+ * reciprocal normalize() uses) vs 1.0f / sqrtf(x); other values are RT_E_ARG.
+ * Writes the mismatch count and the lowest mismatching x (0xffffffff if none); synchronous. */
+int rt_debug_check_fastmath(int which, uint64_t *mismatches, uint32_t *first_bad);
 int rt_debug_kernel_time(rt_dev_scene *s, double *ms_total, int *launches);
 
 #ifdef __cplusplus

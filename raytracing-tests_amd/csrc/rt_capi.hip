@@ -1306,13 +1306,13 @@ int rt_debug_chunks(rt_dev_scene *s) {
     return s->last_chunks;
 }
 
-int rt_debug_check_rcp(uint64_t *mismatches, uint32_t *first_bad) {
-    if (!mismatches || !first_bad) return RT_E_ARG;
+int rt_debug_check_fastmath(int which, uint64_t *mismatches, uint32_t *first_bad) {
+    if (!mismatches || !first_bad || which != 0) return RT_E_ARG;
     DevBuf d;
     HIP_OK(d.alloc(16));
     HIP_OK(hipMemset(d.p, 0, 8));
     HIP_OK(hipMemset(static_cast<char *>(d.p) + 8, 0xff, 4));
-    HIP_OK(rtk::launch_check_rcp(d.as<unsigned long long>(), reinterpret_cast<unsigned *>(static_cast<char *>(d.p) + 8),
+    HIP_OK(rtk::launch_check_fastmath(which, d.as<unsigned long long>(), reinterpret_cast<unsigned *>(static_cast<char *>(d.p) + 8),
                                  nullptr));
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipMemcpy(mismatches, d.p, 8, hipMemcpyDeviceToHost));

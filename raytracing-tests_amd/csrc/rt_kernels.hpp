@@ -254,8 +254,9 @@ hipError_t launch_iow03_sample_order(const Frame &f, const SpecRecs &R, const fl
                                      int max_lanes, unsigned long long *fcost, uint32_t *sorder, hipStream_t s);
 hipError_t launch_iow03_pixel_key(const Frame &f, const SpecRecs &R, const float4 *cont, const unsigned *count,
                                   int max_lanes, unsigned *key, hipStream_t s);
-// rcp_sqrt_domain(sqrt(x)) (rt_math.hpp) against 1.0f / sqrt(x) for all 2^32 x: mismatch count, lowest bad x
-hipError_t launch_check_rcp(unsigned long long *bad, unsigned *first, hipStream_t s);
+// rt_math.hpp's shortened sequences against the compiler's for all 2^32 x (k_check_fastmath):
+// mismatch count, lowest bad x
+hipError_t launch_check_fastmath(int which, unsigned long long *bad, unsigned *first, hipStream_t s);
 hipError_t launch_iow03_altspawn(const Frame &f, const SpecRecs &R, float4 *cont, unsigned *count, uint32_t cap,
                                  hipStream_t s);
 hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,

@@ -29,7 +29,7 @@ __device__ __forceinline__ float rcp(float b) { return 1.0f / b; }
 // compiler's correctly rounded 1.0f / s is div_scale x2, rcp, five fma, div_fmas and div_fixup;
 // the div_scale steps only rescale operands whose reciprocal could leave the normal range (not
 // the case on this domain), where div_fmas is a plain fma.  This is the same arithmetic without
-// them; rt_debug_check_rcp compares it with 1.0f / sqrt(x) for all 2^32 x on the device
+// them; rt_debug_check_fastmath(0) compares it with 1.0f / sqrt(x) for all 2^32 x on the device
 // (tests/test_gpu_fastmath.py).  Outside the domain (denormal or huge s) it is not exact.
 __device__ __forceinline__ float rcp_sqrt_domain(float s) {
     const float r0 = __builtin_amdgcn_rcpf(s);

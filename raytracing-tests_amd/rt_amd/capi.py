@@ -133,7 +133,7 @@ SIGNATURES = {
     "rt_debug_chunks": (C.c_int, [C.c_void_p]),
     "rt_debug_spec_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
     "rt_debug_time_kernels": (C.c_int, [C.c_int]),
-    "rt_debug_check_rcp": (C.c_int, [_U64P, _U32P]),
+    "rt_debug_check_fastmath": (C.c_int, [C.c_int, _U64P, _U32P]),
     "rt_debug_kernel_time": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "rt_debug_spec_pixels": (C.c_int, [C.c_void_p, _U32P, C.c_uint32]),
     "rt_debug_spec_list_hist": (C.c_int, [C.c_void_p, _U64P]),
