@@ -405,7 +405,12 @@ def main():
                                  "traffic = PMC HBM bytes per launch from profiles/pmc_iow03.json"},
             "valu": valu,
             "hbm": {"achieved_GBps": round(balg / (main_ms / launches * 1e-3) / 1e9, 1),
-                    "peak_GBps": HBM_PEAK_GBPS, "algorithmic_bytes_per_launch": balg},
+                    "peak_GBps": HBM_PEAK_GBPS, "algorithmic_bytes_per_launch": balg,
+                    "measured_GBps": (round(traffic / (main_ms / launches * 1e-3) / 1e9, 1)
+                                      if traffic else None),
+                    "note": "achieved = SURVEY 8d algorithmic bytes (node, object and framebuffer "
+                            "reads at their nominal size), most of them served from LDS and L2, so "
+                            "it can exceed the HBM peak; measured = roofline.traffic (PMC HBM bytes)"},
             "mean_bounces": round(st["segments"] / (W * H * spp * args.steps), 3),
             "rays_per_step": int(per_step["segments"]),
             "counters_per_step": {k: int(v) for k, v in per_step.items()},

@@ -1,0 +1,7 @@
+# round-end evidence, part 1: smoke and the whole GPU suite
+set -o pipefail
+O=gpurun_out/round
+mkdir -p $O
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1 || exit 1
+tail -3 $O/gpu_tests.log
