@@ -2456,8 +2456,10 @@ __global__ __launch_bounds__(kBlock) void k_iow03_keys0(Frame f, SpecRecs R, uns
 // INW samples are independent invocations (01_BVH...glsl:601-675), so no speculation is needed:
 // each writes sqrt(colour), its depth and its counters to a record, and k_inw_fin adds the
 // records in sample order exactly as End() does.
+// 3 waves per SIMD: the kernel needs 149 (INW-01) / 159 (INW-04) VGPRs under that cap with no
+// spills; uncapped it took 169 and ran 2 waves per SIMD (LDS allows 4 blocks per CU).
 template <bool LIGHTS>
-__global__ __launch_bounds__(kBlock) void k_inw_s(Frame f, InwScene S, SpecRecs R, int s0, int ns, Cont ct,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_inw_s(Frame f, InwScene S, SpecRecs R, int s0, int ns, Cont ct,
                                                   unsigned *counter) {
     __shared__ float lds[kFStack * kBlock];
     Ctr c;
