@@ -77,6 +77,22 @@ __device__ __forceinline__ bool first_active_lane() {
         }                                                                             \
     } while (0)
 
+// Finer phase split of the wave-cooperative segment (diagnostic builds only, -DRT_DIAG_SPLIT):
+// reuses tally slots that stay zero in that mode (see tools/latency_probe.py).
+#ifdef RT_DIAG_SPLIT
+#define SPL_T0(t) const unsigned long long t = (unsigned long long)clock64()
+#define SPL_CYC(w, slot, t)                                                           \
+    do {                                                                              \
+        if (w) {                                                                      \
+            const unsigned long long d_ = (unsigned long long)clock64() - (t);        \
+            if (first_active_lane()) (w)[slot] += d_;                                 \
+        }                                                                             \
+    } while (0)
+#else
+#define SPL_T0(t) ((void)0)
+#define SPL_CYC(w, slot, t) ((void)0)
+#endif
+
 __device__ __forceinline__ void flush(const Frame &f, const Ctr &c) {
     if (c.wdbg && (threadIdx.x & 63) == 0)
         for (int i = 0; i < kDbgSlots; i++) atomicAdd(f.dbg + i, c.wdbg[i]);
@@ -414,7 +430,8 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
 // issued together: a lone ray's query costs about two memory latencies, not one per step.
 constexpr int kCoopR = 8;
 __device__ void iow_coop_search(const IowScene &S, f3 go, f3 gd, float max_t, short *wl, int cap, float &t_out,
-                                int &j_out, float4 &c0_out, float4 &c1_out, uint32_t &nbox, uint32_t &nprim) {
+                                int &j_out, float4 &c0_out, float4 &c1_out, uint32_t &nbox, uint32_t &nprim,
+                                unsigned long long *wdbg = nullptr) {
     const int lane = (int)(threadIdx.x & 63);
     float bt = max_t;
     int bj = -1;
@@ -435,6 +452,7 @@ __device__ void iow_coop_search(const IowScene &S, f3 go, f3 gd, float max_t, sh
     uint32_t j0 = 0;
     while (j0 < n) {
         uint32_t cnt = 0, jb = j0;
+        SPL_T0(t_cull);
         if (cull) {
             for (; j0 < n && cnt + 64 * kCoopR <= (uint32_t)cap; j0 += 64 * kCoopR) {
                 const float2 *ob2 = reinterpret_cast<const float2 *>(S.obox + n);
@@ -464,6 +482,8 @@ __device__ void iow_coop_search(const IowScene &S, f3 go, f3 gd, float max_t, sh
             cnt = n - j0 < (uint32_t)cap ? n - j0 : (uint32_t)cap;
             j0 += cnt;
         }
+        SPL_CYC(wdbg, kDbgTrav, t_cull);
+        SPL_T0(t_exact);
         for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
             const uint32_t k = k0 + lane;
             if (k < cnt) {
@@ -476,7 +496,9 @@ __device__ void iow_coop_search(const IowScene &S, f3 go, f3 gd, float max_t, sh
             }
         }
         nprim += cnt;
+        SPL_CYC(wdbg, kDbgTravLanes, t_exact);
     }
+    SPL_T0(t_red);
     const float tm = wave_min_all(bj >= 0 ? bt : max_t);
     unsigned long long m = __ballot(bj >= 0 && bt == tm);
     if (m == 0) return;
@@ -490,6 +512,7 @@ __device__ void iow_coop_search(const IowScene &S, f3 go, f3 gd, float max_t, sh
     j_out = jm;
     c0_out = make_float4(bcast_f(b0.x, lm), bcast_f(b0.y, lm), bcast_f(b0.z, lm), bcast_f(b0.w, lm));
     c1_out = make_float4(bcast_f(b1.x, lm), bcast_f(b1.y, lm), bcast_f(b1.z, lm), bcast_f(b1.w, lm));
+    SPL_CYC(wdbg, kDbgLeaf, t_red);
 }
 
 __device__ __forceinline__ f3 fib_dir(float4 t, float s, f3 focus) {
@@ -650,18 +673,22 @@ __device__ __forceinline__ void iow_seg_step(const IowScene &S, const Frame &F, 
         int j;
         float4 c0, c1;
         uint32_t nb, np;
-        iow_coop_search(S, go, gd, 32000.0f, wl, kCap, t, j, c0, c1, nb, np);
+        iow_coop_search(S, go, gd, 32000.0f, wl, kCap, t, j, c0, c1, nb, np, c.wdbg);
         if ((int)(threadIdx.x & 63) == L) { my_t = t; my_j = j; my_c0 = c0; my_c1 = c1; my_box = nb; my_prim = np; }
     }
     DBG_CYC(F, c, kDbgCycSpare0, t_q);
     DBG_T0(F, t_sh);
     if (seg) {
         c.seg++; c.nodes += my_box; c.prims += my_prim;
+        SPL_T0(t_ev);
         f3 td_id, nd_id;
         iow_id_dirs(in.cd, td_id, nd_id);
         const RayRet data =
             iow_eval_c(S, in.co, in.cd, td_id, nd_id, my_t, my_j, 32000.0f, in.contribution, my_c0, my_c1);
+        SPL_CYC(c.wdbg, kDbgCycRay, t_ev);
+        SPL_T0(t_sd);
         iow_seg_shade(S, F, K, skip, sample, sidx, c, in, data);
+        SPL_CYC(c.wdbg, kDbgCycTrav, t_sd);
     }
     DBG_CYC(F, c, kDbgCycSpare1, t_sh);
 }
@@ -2458,8 +2485,11 @@ __global__ __launch_bounds__(kBlock) void k_iow03_keys0(Frame f, SpecRecs R, uns
 // records in sample order exactly as End() does.
 // 3 waves per SIMD: the kernel needs 149 (INW-01) / 159 (INW-04) VGPRs under that cap with no
 // spills; uncapped it took 169 and ran 2 waves per SIMD (LDS allows 4 blocks per CU).
+#ifndef RT_INW_WAVES
+#define RT_INW_WAVES 3
+#endif
 template <bool LIGHTS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_inw_s(Frame f, InwScene S, SpecRecs R, int s0, int ns, Cont ct,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INW_WAVES))) void k_inw_s(Frame f, InwScene S, SpecRecs R, int s0, int ns, Cont ct,
                                                   unsigned *counter) {
     __shared__ float lds[kFStack * kBlock];
     Ctr c;

@@ -13,7 +13,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "librt_hip.so")
+# RT_HIP_LIB: an alternative build of the same library (diagnostic variants, tools/ only)
+LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(os.path.dirname(_HERE), "librt_hip.so")
 
 RT_OK, RT_E_ARG, RT_E_HIP, RT_E_NODEVICE, RT_E_UNSUPPORTED = 0, -1, -2, -3, -4
 
