@@ -1,19 +1,22 @@
 #!/usr/bin/env python3
-"""bench.py -- Mrays/s of the MI355X render path on BASELINE.json's headline configuration.
+"""bench.py -- Mrays/s of the MI355X render path on BASELINE.json's 1/2/4/8-GPU configuration.
 
-Workload (BASELINE.json configs[1]): In-One-Weekend 03_Adding_Materials "final scene"
-(~500 spheres + ground cuboid), 1200x800, 100 spp, 50 bounces.  One step = one full frame:
-every pixel, every sample, every bounce of the reference's IOW-03 render loop.
+Workload (default, --config c3): BASELINE.json configs[2] at N=1 and configs[3] at N>1, the
+In-Next-Week 01 LBVH scene: 10k random moving spheres (seed 1234), 1920x1080,
+500 spp, 50 bounces (In-Next-Week/base.h:148-173, 01_BoundingVolumeHierarchy/computeShaderSrc.glsl).
+One step = one full frame: every pixel, every sample, every bounce of the reference's INW-01 loop.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|ns]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-Multi-GPU: the frame is cut into tiles dealt round-robin to the ranks (one process per GPU):
+Secondary lines: --config c2 (configs[1]: In-One-Weekend 03 final scene, 1200x800, 100 spp) and
+--config ns (the north star's IOW-03 final scene at 1920x1080, 500 spp).
+
+Multi-GPU (configs[3]): the frame is cut into tiles dealt to the ranks (one process per GPU):
 16x16 tiles across ranks, in a hashed order (deal_order), 64x64 on one GPU (RT_BENCH_TILE
-overrides both).  Each rank renders
-its tiles into a packed buffer and the tiles are gathered to rank 0 with one RCCL gather over
-xGMI, where the image is assembled.  Total work is fixed, so the
-scaling mode is "strong".
+overrides both).  Each rank renders its tiles into a packed buffer and the tiles are gathered
+to rank 0 with one RCCL gather over xGMI, where the image is assembled.  Total work is fixed,
+so the scaling mode is "strong".
 
 Metric: Mrays/s = W*H*spp*mean_bounces / t = (rays cast, counted by the kernels) / t, summed
 over ranks, t = max over ranks of the timed region (barrier + synchronize on both sides).
@@ -50,11 +53,27 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (= f32 MFMA rate), MI355X_M
 HBM_PEAK_GBPS = 8000.0     # MI355X HBM3E peak, MI355X_MICROARCH.md
 CUS = 256                  # MI355X compute units
 CLOCK_HZ = 2.4e9           # MI355X peak engine clock
-WORKLOAD = ("In-One-Weekend 03_Adding_Materials final scene (~500 random spheres + ground cuboid), "
-            "1200x800, 100 spp, 50 bounces")
-# --config c4 (BASELINE configs[3]): the C3 LBVH scene tile-partitioned; not the headline line
-WORKLOAD_C4 = ("In-Next-Week 01 LBVH: 10k random moving spheres, 1920x1080, 500 spp, 50 bounces, "
-               "tile-partitioned (C4)")
+METRIC = "Mrays/s (W\u00d7H\u00d7spp\u00d7mean_bounces/t) + achieved HBM GB/s, 1/2/4/8 MI355X"  # BASELINE.json
+# --config -> (preset, seed, n_hint, overrides, workload at N=1, workload at N>1, data)
+CONFIGS = {
+    "c3": ("INW01_RANDOM", 1234, 10_000, {},
+           "In-Next-Week 01 LBVH: 10k random moving spheres, 1920x1080, 500 spp, 50 bounces, 1 MI355X "
+           "(BASELINE configs[2])",
+           "In-Next-Week 01 LBVH: 10k random moving spheres, 1920x1080, 500 spp, 50 bounces, tile-partitioned "
+           "across {n} MI355X with an RCCL gather over xGMI (BASELINE configs[3])",
+           "synthetic (seeded C3 generator, SURVEY 8d seed 1234; LBVH built by rt_lbvh_build)"),
+    "c2": ("IOW03_FINAL", 20250131, 0, {},
+           "In-One-Weekend 03_Adding_Materials final scene (~500 random spheres + ground cuboid), 1200x800, "
+           "100 spp, 50 bounces (BASELINE configs[1])",
+           "In-One-Weekend 03_Adding_Materials final scene, 1200x800, 100 spp, 50 bounces, tile-partitioned "
+           "across {n} MI355X with an RCCL gather",
+           "synthetic (seeded final-scene generator, SURVEY 8d seed 20250131)"),
+    "ns": ("IOW03_FINAL", 20250131, 0, {"width": 1920, "height": 1080, "spp": 500},
+           "In-One-Weekend 03 final scene, 1920x1080, 500 spp, 50 bounces (BASELINE north_star workload)",
+           "In-One-Weekend 03 final scene, 1920x1080, 500 spp, 50 bounces, tile-partitioned across {n} MI355X "
+           "with an RCCL gather (BASELINE north_star workload)",
+           "synthetic (seeded final-scene generator, SURVEY 8d seed 20250131)"),
+}
 
 
 def algorithmic_flops(st: dict) -> float:
@@ -124,21 +143,36 @@ def assemble_frame(src, order, nx: int, ny: int):
     return assemble_lists(src, [order[r::world] for r in range(world)], nx, ny)
 
 
-def cpu_baseline(sc, threads: int, px: int) -> dict:
-    """The CPU oracle (C restatement of the reference shader, OpenMP) on a bounded sample of the
-    same frame: the central px x px block at the full spp and bounce count."""
+def host_cores() -> int:
+    """The GPU box's host cores as `nproc` reports them (it honours the CPU affinity mask and
+    OMP_NUM_THREADS, i.e. this job's share of the host); os.cpu_count() as a fallback."""
+    import subprocess
+    try:
+        return max(1, int(subprocess.run(["nproc"], capture_output=True, text=True, check=True).stdout))
+    except Exception:  # noqa: BLE001
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(sc, threads: int, spp: int) -> dict:
+    """The CPU oracle (the C restatement of the reference shader, OpenMP schedule(dynamic, 1) over
+    pixel rows) on all `threads` host cores, on a bounded sample of the same frame: the central
+    64 x `threads` pixel block (one row per core, so every core has rows to take), at `spp`
+    samples (Mrays/s is a rate) and the full bounce count."""
     from oracle import oracle as O
     O.set_threads(threads)
     p = R.RtParams()
     C.memmove(C.addressof(p), C.addressof(sc.params), C.sizeof(p))
-    p.tile_x0, p.tile_y0 = sc.params.width // 2 - px // 2, sc.params.height // 2 - px // 2
-    p.tile_w = p.tile_h = px
+    bw, bh = 64, max(threads, 8)
+    p.spp = min(spp, sc.params.spp)
+    p.tile_x0, p.tile_y0 = sc.params.width // 2 - bw // 2, sc.params.height // 2 - bh // 2
+    p.tile_w, p.tile_h = bw, bh
     t0 = time.perf_counter()
     _, _, st = O.render(sc, p)
     dt = time.perf_counter() - t0
     return {"value": st["segments"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"central {px}x{px} pixel block of the same frame at {sc.params.spp} spp / "
-                      f"{sc.params.max_bounces} bounces ({st['segments']} rays, {dt:.1f} s, oracle/librt_oracle.so)"}
+            "sample": f"central {bw}x{bh} pixel block of the same frame at {p.spp} spp / "
+                      f"{sc.params.max_bounces} bounces, one OpenMP thread per core = nproc "
+                      f"({st['segments']} rays, {dt:.1f} s, oracle/librt_oracle.so)"}
 
 
 def main():
@@ -149,16 +183,18 @@ def main():
     ap.add_argument("--spp", type=int, default=0, help="override spp (default: the config's 100)")
     ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--height", type=int, default=0)
-    ap.add_argument("--cpu-px", type=int, default=16, help="CPU baseline sample block size")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="host cores for the CPU baseline")
+    ap.add_argument("--cpu-spp", type=int, default=0,
+                    help="CPU baseline samples per pixel (default: 128 for c3, the config's spp for c2/ns)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="host cores for the CPU baseline (default: nproc)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--balance", action="store_true",
                     help="multi-rank: deal the timed frames' tiles by LPT over the warm-up frame's tile costs "
                          "(measured neutral on the 8-way frames: their time is set by long samples, not by rays)")
     ap.add_argument("--occupancy", action="store_true", help="report per-phase lane occupancy (diagnostic)")
     ap.add_argument("--save-image", default="", help="rank 0 saves the assembled frame (.npy) for checking")
-    ap.add_argument("--config", default="c2", choices=("c2", "c4"),
-                    help="c2: the headline (BASELINE configs[1]); c4: the LBVH scene of configs[3]")
+    ap.add_argument("--config", default="c3", choices=("c3", "c4", "c2", "ns"),
+                    help="c3 (= c4): BASELINE configs[2] / configs[3], the headline; c2: configs[1]; "
+                         "ns: the north star's IOW-03 workload")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -188,11 +224,10 @@ def main():
         over["width"] = args.width
     if args.height:
         over["height"] = args.height
-    inw = args.config == "c4"
-    if inw:
-        sc = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 10_000, **over)
-    else:
-        sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0, **over)
+    cfg = "c3" if args.config == "c4" else args.config
+    preset, seed, n_hint, base_over, wl1, wln, data = CONFIGS[cfg]
+    sc = R.make_scene(getattr(R, "PRESET_" + preset), seed, n_hint, **{**base_over, **over})
+    inw = sc.stage != R.RT_STAGE_IOW03
     W, H, spp = sc.params.width, sc.params.height, sc.params.spp
     T = tile_for(world)
     nparts, part = world, rank  # partition size and this process's part
@@ -356,29 +391,34 @@ def main():
         # sequential leftover pass traces ~2% of them) over the main kernel's launches
         achieved = flops / (main_ms * 1e-3) / 1e12
         balg = algorithmic_bytes(per_step, W * H / world, inw) / launches
-        traffic, valu = None, None
-        prof = os.path.join(ROOT, "profiles", "pmc_iow03.json")
-        if os.path.exists(prof):
+        avg_s = main_ms / launches * 1e-3
+        traffic, valu, lane_issue, prof_src = None, None, None, None
+        prof = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")  # PMC passes of this config's command
+        if os.path.exists(prof) and world == 1:
             try:
                 pm = json.load(open(prof))
-                if pm.get("config") == [W, H, spp]:
-                    if pm.get("launches_per_frame") == launches and pm.get("kernel") == kname:
-                        traffic = pm.get("hbm_bytes_per_launch")
-                        # VALU issue: a wave64 VALU instruction occupies its SIMD's issue for 2
-                        # cycles (MI355X_MICROARCH.md); capacity = CUs x 4 SIMDs x clock x time
-                        insts = pm["counters"]["SQ_INSTS_VALU"] / pm["frames"]
-                        cap = CUS * 4 * CLOCK_HZ * (main_ms * 1e-3)
-                        valu = {"busy_frac": round(2.0 * insts / cap, 4),
-                                "lane_util": round(pm["valu_lane_utilisation"], 4),
-                                "insts_per_frame": insts, "clock_hz": CLOCK_HZ,
-                                "source": "profiles/pmc_iow03.json (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU)"}
-            except Exception:
-                traffic, valu = None, None
+                if (pm.get("config") == [W, H, spp] and pm.get("kernel") == kname
+                        and pm.get("launches_per_frame") == launches):
+                    prof_src = "profiles/" + os.path.basename(prof)
+                    traffic = pm.get("hbm_bytes_per_launch")
+                    # VALU issue: a wave64 VALU instruction holds its SIMD's issue for 2 cycles
+                    # (MI355X_MICROARCH.md); capacity = CUs x 4 SIMDs x clock x main-kernel time
+                    insts = pm["counters"]["SQ_INSTS_VALU"] / pm["frames"]
+                    busy = 2.0 * insts / (CUS * 4 * CLOCK_HZ * (main_ms * 1e-3))
+                    util = pm["valu_lane_utilisation"]
+                    lane_issue = busy * util
+                    valu = {"busy_frac": round(busy, 4), "lane_util": round(util, 4),
+                            "lane_issue_frac": round(lane_issue, 4), "insts_per_frame": insts,
+                            "clock_hz": CLOCK_HZ,
+                            "source": prof_src + " (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU)"}
+            except Exception:  # noqa: BLE001
+                traffic, valu, lane_issue, prof_src = None, None, None, None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(sc, args.cpu_threads, args.cpu_px)
+            cores = args.cpu_threads or host_cores()
+            cpu = cpu_baseline(sc, cores, args.cpu_spp or (128 if cfg == "c3" else sc.params.spp))
         out = {
-            "metric": "Mrays/s (W*H*spp*mean_bounces/t)",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -389,28 +429,34 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": ("synthetic (seeded C3 generator, SURVEY 8d seed 1234)" if inw else
-                     "synthetic (seeded final-scene generator, SURVEY 8d seed 20250131)"),
-            "config": {"workload": WORKLOAD_C4 if inw else WORKLOAD, "width": W, "height": H, "spp": spp,
-                       "max_bounces": sc.params.max_bounces, "objects": sc.n, "tile": T,
+            "data": data,
+            "config": {"workload": wl1 if world == 1 else wln.format(n=world), "width": W, "height": H,
+                       "spp": spp, "max_bounces": sc.params.max_bounces, "objects": sc.n, "tile": T,
                        "parallelism": f"tiles_rr{world}" + ("+rccl_gather" if world > 1 else "")},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                         "traffic": traffic, "kernel": kname, "launches_per_frame": launches,
+                         "traffic": traffic, "lane_issue_frac": round(lane_issue, 4) if lane_issue else None,
+                         "kernel": kname, "launches_per_frame": launches,
                          "avg_launch_ms": round(main_ms / launches, 3),
                          "main_kernel_ms_per_frame": round(main_ms, 3),
                          "render_ms_per_frame": round(kernel_ms, 3),
                          "flops_per_launch": flops / launches,
-                         "note": "VALU fp32 kernel (no MFMA on this path); peak = FP32 vector peak; "
-                                 "traffic = PMC HBM bytes per launch from profiles/pmc_iow03.json"},
+                         "source": prof_src,
+                         "note": "fp32 VALU kernel (no MFMA on this path); peak = FP32 vector peak; "
+                                 "achieved = SURVEY 8d F_alg per launch / average launch time (HIP events "
+                                 "on the launch stream); F_alg counts this build's own node visits and object "
+                                 "tests (4-wide culling walk), so it shrinks as the walk improves; "
+                                 "lane_issue_frac = VALU busy x lane utilisation (PMC); traffic = PMC HBM "
+                                 "bytes per launch"},
             "valu": valu,
-            "hbm": {"achieved_GBps": round(balg / (main_ms / launches * 1e-3) / 1e9, 1),
-                    "peak_GBps": HBM_PEAK_GBPS, "algorithmic_bytes_per_launch": balg,
-                    "measured_GBps": (round(traffic / (main_ms / launches * 1e-3) / 1e9, 1)
-                                      if traffic else None),
-                    "note": "achieved = SURVEY 8d algorithmic bytes (node, object and framebuffer "
-                            "reads at their nominal size), most of them served from LDS and L2, so "
-                            "it can exceed the HBM peak; measured = roofline.traffic (PMC HBM bytes)"},
+            "hbm": {"measured_GBps": round(traffic / avg_s / 1e9, 2) if traffic else None,
+                    "measured_frac": round(traffic / avg_s / 1e9 / HBM_PEAK_GBPS, 5) if traffic else None,
+                    "peak_GBps": HBM_PEAK_GBPS, "bytes_per_launch": traffic,
+                    "note": "PMC: 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section)"},
+            "onchip": {"alg_GBps": round(balg / avg_s / 1e9, 1), "alg_bytes_per_launch": balg,
+                       "note": "SURVEY 8d algorithmic bytes (node, object and framebuffer reads at their "
+                               "nominal size) per launch / average launch time; served from LDS, L1 and L2, "
+                               "so not an HBM rate"},
             "mean_bounces": round(st["segments"] / (W * H * spp * args.steps), 3),
             "rays_per_step": int(per_step["segments"]),
             "counters_per_step": {k: int(v) for k, v in per_step.items()},

@@ -143,7 +143,9 @@ struct rt_dev_scene {
     DevBuf sp_pstate;  // asynchronous windows: per-pixel frontier state
     DevBuf sp_front;   // checkpoint rounds: per-pixel frontier (uint4)
     DevBuf sp_sorder, sp_fcost;  // heavy-first enumeration: sample indices by cost, their costs
+    DevBuf inw_ring;             // k_inw_o: the waves' fold rings (kInwRingBytesPerBlock per block)
     DevBuf sp_dbg_t;             // RT_DEBUG_TIMES diagnostics: per unit start / end launch
+    size_t sp_dbg_n = 0;         // units (P * S) of the render that last wrote sp_dbg_t
     uint32_t launch_seq = 0;
     DevBuf sp_exact;             // RT_SPEC_ORACLE diagnostics: exact incoming state per sample
     size_t sp_exact_n = 0;
@@ -559,6 +561,7 @@ int ensure_inw_spec(rt_dev_scene *s, uint32_t P, int spp) {
 }
 
 int launch_scene_inw_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st, int ns);
+int launch_scene_inw_ordered(rt_dev_scene *s, rtk::Frame &f, hipStream_t st);
 
 // Enqueue a whole render (all chunks) on `st`.  The first call for a given frame size
 // allocates the chunk workspace; later calls allocate nothing.
@@ -570,6 +573,7 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     if (s->kind == 3 && env_int("RT_IOW_SPEC", 1) != 0 && !rtk::iow_narrow(f) && s->s_stop > 0 &&
         ensure_spec(s, rtk::units_of(f), uint32_t(s->s_stop)))
         return launch_scene_spec(s, f, st);
+    if (s->kind != 3 && env_int("RT_INW_ORDER", 1) != 0) return launch_scene_inw_ordered(s, f, st);
     if (s->kind != 3 && env_int("RT_INW_SPEC", 1) != 0) {
         const int ns = ensure_inw_spec(s, rtk::units_of(f), f.spp);
         if (ns > 0) return launch_scene_inw_spec(s, f, st, ns);
@@ -712,10 +716,12 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         HIP_OK(hipMemsetAsync(s->sp_dbg_t.p, 0, n, st));
         R.dbg_start = s->sp_dbg_t.as<uint32_t>();
         R.dbg_end = R.dbg_start + size_t(P) * S;
+        s->sp_dbg_n = size_t(P) * S;
     }
     const bool alt_on = env_int("RT_SPEC_ALT", 1) != 0 && s->n_alt_vals > 1 && S > 1;
     if (alt_on) {  // alternative runs (DESIGN.md "Alternative runs")
-        const uint32_t cap = uint32_t(std::max(1024, env_int("RT_SPEC_ALT_CAP", 1 << 17)));
+        // slots pack as first | count << 24 in the hash (alt_find): the cap stays below 2^24
+        const uint32_t cap = uint32_t(std::min(1 << 24, std::max(1024, env_int("RT_SPEC_ALT_CAP", 1 << 17))));
         if (s->alt_cap != cap) {
             for (DevBuf *b : {&s->sp_alt, &s->sp_alt_hash, &s->sp_alt_count}) { b->~DevBuf(); new (b) DevBuf(); }
             HIP_OK(s->sp_alt.alloc(size_t(cap) * sizeof(rtk::AltRec)));
@@ -1020,6 +1026,49 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     return RT_OK;
 }
 
+// INW, wave-ordered (k_inw_o): one persistent launch per frame, the per-pixel End() sums folded
+// on chip in sample order (DESIGN.md "k_inw_o").  The launch is bracketed by HIP events on its
+// stream when kernel timing is on (rt_debug_kernel_time).
+int launch_scene_inw_ordered(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
+    const int blocks = s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 16 : 15);
+    const size_t ring_bytes = size_t(blocks) * rtk::kInwRingBytesPerBlock;
+    if (s->inw_ring.bytes < ring_bytes) {
+        s->inw_ring.~DevBuf();
+        new (&s->inw_ring) DevBuf();
+        if (s->inw_ring.alloc(ring_bytes) != hipSuccess) return RT_E_HIP;
+    }
+    rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
+                     s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>(),
+                     s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
+    set_wide(s, sc);
+    s->last_kernel = s->layout == 4 ? "k_inw_o<true>" : "k_inw_o<false>";
+    s->last_launches = 1;
+    s->last_chunks = 1;
+    s->kt_used = 0;
+    std::pair<hipEvent_t, hipEvent_t> *ev = nullptr;
+    hipError_t e = hipSuccess;
+    if (g_time_kernels) {
+        if (s->kt_ev.empty()) {
+            std::pair<hipEvent_t, hipEvent_t> p{nullptr, nullptr};
+            if (hipEventCreate(&p.first) != hipSuccess || hipEventCreate(&p.second) != hipSuccess) return RT_E_HIP;
+            s->kt_ev.push_back(p);
+        }
+        ev = &s->kt_ev[0];
+        s->kt_used = 1;
+    }
+    // the ring reset and queue counter first, so the events bracket the kernel alone
+    e = hipMemsetAsync(s->inw_ring.p, 0xff, ring_bytes, st);
+    if (e == hipSuccess && ev) e = hipEventRecord(ev->first, st);
+    if (e == hipSuccess)
+        e = rtk::launch_inw_ordered(f, sc, s->inw_ring.as<float4>(), s->counter.as<unsigned>(), blocks, st);
+    if (e == hipSuccess && ev) e = hipEventRecord(ev->second, st);
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
+        return RT_E_HIP;
+    }
+    return RT_OK;
+}
+
 // Sample-parallel INW: chunks of ns samples; each chunk runs all its (pixel, sample) units
 // (compacted passes), then End() over the chunk adds the samples in order.
 int launch_scene_inw_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st, int ns) {
@@ -1283,8 +1332,8 @@ int rt_debug_spec_dump(rt_dev_scene *s, uint32_t *rays_out, size_t cap, uint32_t
 }
 
 int rt_debug_spec_times(rt_dev_scene *s, uint32_t *start_out, uint32_t *end_out, size_t cap) {
-    if (!s || !start_out || !end_out || !s->spec_cap || !s->spec_units || !s->sp_dbg_t.p) return RT_E_ARG;
-    const size_t n = size_t(s->spec_units) * (s->spec_cap / s->spec_units);
+    if (!s || !start_out || !end_out || !s->sp_dbg_n || !s->sp_dbg_t.p) return RT_E_ARG;
+    const size_t n = s->sp_dbg_n;  // the last render's P * S: its end times start at offset n
     if (n > cap || s->sp_dbg_t.bytes < 2 * n * sizeof(uint32_t)) return RT_E_ARG;
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipMemcpy(start_out, s->sp_dbg_t.p, n * 4, hipMemcpyDeviceToHost));

@@ -1006,7 +1006,7 @@ __device__ uint32_t alt_adopt(const SpecRecs &R, uint32_t u, uint32_t E1, uint32
     for (uint32_t i = 0; i < fk.y; i++) {
         const AltRec &A = R.alt[fk.x + i];
         const uint32_t st = __hip_atomic_load(&A.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (st == 0u || st == launch + 1u) continue;
+        if (st == 0u || st == launch + 1u || A.u != u) continue;  // (A.u: a record of this unit only)
         const unsigned fl = __float_as_uint(A.col.w), rm = fl & 15u;
         if (((rm & 2u) && __float_as_uint(A.assume.x) != E1) || ((rm & 4u) && __float_as_uint(A.assume.y) != E2) ||
             ((rm & 8u) && __float_as_uint(A.assume.z) != E3))
@@ -1696,6 +1696,23 @@ __device__ __forceinline__ bool test_aabb(float4 n0, float4 n1, f3 o, f3 id, flo
     return tlim > 0.0f ? tlim > tmin : true;
 }
 
+// The same test, also returning the entry t it compares (te) -- the wide walk's guard below.
+__device__ __forceinline__ bool test_aabb_te(float4 n0, float4 n1, f3 o, f3 id, float tlim, float &te) {
+    float a = (n0.x - o.x) * id.x, b = (n0.w - o.x) * id.x;
+    float tmin = fminf(a, b), tmax = fmaxf(a, b);
+    te = tmin;
+    if (tmax <= tmin) return false;
+    a = (n0.y - o.y) * id.y; b = (n1.x - o.y) * id.y;
+    tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
+    te = tmin;
+    if (tmax <= tmin) return false;
+    a = (n0.z - o.z) * id.z; b = (n1.y - o.z) * id.z;
+    tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
+    te = tmin;
+    if (tmax <= tmin) return false;
+    return tlim > 0.0f ? tlim > tmin : true;
+}
+
 // closest-hit LBVH DFS (01_BVH...glsl:431-473, 04...glsl:524-563, shadow 620-657)
 template <bool WANT_NORMAL>
 __device__ float inw_traverse(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
@@ -1793,6 +1810,11 @@ __device__ float inw_surrounding_ri(const InwScene &S, FStack &K, f3 hp, float r
 // walk's stack lives in the free part of the shared stack above K.size.  Node and primitive
 // counters count this walk's own work.  ok = false: the conditions do not hold (or the walk's
 // stack overflowed) and the caller runs the reference walk.
+// One more condition: the reference tests a leaf box against its running limit, so it skips an
+// object whose box entry te is not below the best t found so far.  Normally t >= te for a hit
+// inside its own box, and then skipping it changes nothing; but where an object's face coincides
+// with its box face, rounding can put t an ulp below te.  Any accepted candidate with t < te
+// therefore hands the ray to the reference walk (ok = false).
 template <bool WANT_NORMAL>
 __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
                                    f3 &normal, float &extra, float init_geom, Ctr &c, bool &ok) {
@@ -1814,13 +1836,15 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
         c.prims++;
         const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
         const Xf x = load_xf(S, g);  // loaded with the box, before its test: one memory latency
-        if (!test_aabb(n0, n1, o, id, tlim0)) return;
+        float te;
+        if (!test_aabb_te(n0, n1, o, id, tlim0, te)) return;
         f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
         f3 to = tmul(x.R, ov), td = tmul(x.R, d);
         float t = -1.0f;
         if (x.type == 1) t = t_ellipsoid(to, td, x.is);
         else if (x.type == 2) t = t_cuboid(to, td, x.scale);
         if (t > 0.0f && t < tlim0) {
+            if (t < te) ovf = true;  // the guard above: the reference walk decides this ray
             const uint32_t r = rank[g];
             if (t < bt || (t == bt && r < br)) { bt = t; bg = g; br = r; lim = bt * 1.0001f + 1e-3f; }
         }
@@ -2107,7 +2131,16 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
                 m_color = mulv(m_color, inw_tex_color(S, ti - 1u, tmul(R, hitpoint - mk(h0.x, h0.y, h0.z))));
             }
         }
-        const float surr = inw_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
+        // The surrounding RI (01_BVH...glsl:486-502) is read only by the refract calls below: on an
+        // outer hit of a refractive object, or on an inner hit.  Where the scatter branch will not
+        // run or reads no RI, the walk is skipped -- when it cannot drop a push (the wide walk's
+        // condition; its drops are counted) and the walk is the wide one (whose node counts are
+        // this build's own).  INW-04 decides after its shadow rays, which scale the contribution.
+        const bool ri_forced = S.wnodes == nullptr || K.size + S.dfs_high > (uint32_t)kFStack;
+        const bool ri_read = (m_refl > 0.002f || m_refr > 0.002f) && (m_refr > 0.002f || dot(normal, cd) > 0.0f);
+        float surr = 1.0f;
+        if (!LIGHTS && (ri_forced || (ri_read && contribution > 0.01f && bounced + 1.0f < (float)F.max_bounces)))
+            surr = inw_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
         if (mf0) K.size = 0;  // 01_BVH...glsl:544-549: the lens record goes after a primary hit
         if (LIGHTS) {  // 04...glsl:604-665
             uint32_t is_lit = S.n_lights > 0 ? 0u : (uint32_t)is_lit_geom(S, f2u(fg + 0.1f));
@@ -2125,7 +2158,10 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
                 }
                 const uint32_t nl = S.n_lights > 1 ? S.n_lights : 1u;
                 contribution *= (float)is_lit * rcp((float)nl);
+                if (ri_forced || (ri_read && contribution > 0.01f && bounced < (float)F.max_bounces))
+                    surr = inw_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
             } else {
+                if (ri_forced) (void)inw_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
                 color = f3{1, 1, 1};
                 K.size = 0;
                 break;
@@ -2545,12 +2581,158 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ?
         }
         if (busy) inw_segment<LIGHTS>(S, f, K, s0 + (int)(u / R.P), col, dep, c);
         if (busy && K.size == 0) {  // sample done
+#if defined(RT_EXP_NOREC)  // timing experiment only: no records (wrong image)
+            if (col.x == 12345.0f) R.col[u] = make_float4(col.x, col.y, col.z, dep);
+#elif defined(RT_EXP_NT)   // timing experiment: streaming (non-temporal) record stores
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(v4f{__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z), dep}, reinterpret_cast<v4f *>(&R.col[u]));
+            __builtin_nontemporal_store(v4f{ubits(c.seg), ubits(c.nodes), ubits(c.prims), ubits(c.shadow)}, reinterpret_cast<v4f *>(&R.ctr[u]));
+            __builtin_nontemporal_store(v4f{ubits(c.drops), ubits(c.nans), 0.0f, 0.0f}, reinterpret_cast<v4f *>(&R.fin[u]));
+#else
             R.col[u] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z), dep);
             R.ctr[u] = make_uint4(c.seg, c.nodes, c.prims, c.shadow);
             R.fin[u] = make_float4(ubits(c.drops), ubits(c.nans), 0.0f, 0.0f);
+#endif
             busy = false;
         }
     }
+}
+
+// ---------------------------------------------------------------- INW, wave-ordered (default)
+// End() (01_BVH...glsl:625-653, 664-675) adds each sample's sqrt(colour) in sample order.  Here a
+// wave owns whole pixels: it claims pixel units from the global queue and hands their samples to
+// its lanes in order -- the wave's stream g = 0, 1, 2, ... runs over (claimed pixel j, sample s) --
+// and a lane that finishes a sample takes the next stream entry at once (lane persistence).  A
+// finished sample stores {sqrt(colour), tag g} into the wave's private ring of kInwRing entries;
+// once per iteration the wave loads the next 64 entries from the fold pointer, and folds the
+// leading run of finished ones in stream order, with every lane computing the same serial sum
+// (End()'s float order).  A pixel's colour is written when its last sample is folded; the middle
+// sample's depth by the lane that finishes it.  The only per-sample traffic is that wave-private
+// ring (a few KB per wave, L2-resident); nothing else per sample leaves the chip.  Entries beyond
+// fold + kInwRing, and pixels beyond fold + 64, are not issued (a straggling sample holds the
+// window; the other lanes keep running until it fills).  Counters accumulate per lane.
+constexpr uint32_t kInwRing = 256;
+__device__ __forceinline__ float rdl(float v, uint32_t l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
+}
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+template <bool LIGHTS>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES))) void k_inw_o(Frame f, InwScene S, float4 *ring, unsigned *counter) {
+    __shared__ float lds[kFStack * kBlock];
+    Ctr c;
+    FStack K{lds + threadIdx.x, 0};
+    const uint32_t lane = threadIdx.x & 63u;
+    float4 *wr = ring + (size_t)uni((blockIdx.x * kBlock + threadIdx.x) >> 6) * kInwRing;
+    const uint32_t spp = (uint32_t)f.spp, mid = spp / 2u, total = units_total(f);
+    const float inv = rcp((float)f.spp);
+    // wave-uniform: stream positions (entry gi / fold gf) as (pixel ordinal, sample), claims
+    uint32_t gi = 0, ji = 0, si = 0;   // next entry to issue: pixel ordinal ji, sample si
+    uint32_t gf = 0, jf = 0, sf = 0;   // next entry to fold
+    uint32_t nclaimed = 0;             // pixel ordinals claimed so far
+    bool qdone = false;
+    f3 acc = f3{0, 0, 0};              // running End() sum of pixel jf (the same in every lane)
+    uint32_t pix_slot = 0xffffffffu;   // lane l: the unit of the claimed ordinal j with j % 64 == l
+    // per lane: the sample it traces
+    bool busy = false;
+    uint32_t g = 0;
+    int s = 0;
+    UnitPix px{};
+    f3 col = f3{0, 0, 0};
+    float dep = 0.0f;
+    K.size = 0;
+    for (;;) {
+        // ---- fold the finished entries gf, gf+1, ... (stored in earlier iterations)
+        if (gf != gi) {
+            __builtin_amdgcn_s_waitcnt(0);  // this wave's ring stores have landed (same CU: L1 write-through)
+            const uint32_t k = gf + lane;
+            bool fin = false;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (k - gf < gi - gf) {
+                v = wr[k % kInwRing];
+                fin = __float_as_uint(v.w) == k;
+            }
+            const unsigned long long m = __ballot(fin);
+            const uint32_t n = ~m == 0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
+            for (uint32_t i = 0; i < n; i++) {
+                const f3 gv = f3{rdl(v.x, i), rdl(v.y, i), rdl(v.z, i)};
+                acc = sf == 0 ? gv : acc + gv;
+                if (++sf == spp) {  // pixel jf complete: End()'s imageStore (01_BVH...glsl:652)
+                    const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
+                    if (lane == 0) {
+                        const UnitPix p = unit_pixel(f, unit);
+                        if (p.out != (size_t)-1)
+                            reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
+                                make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
+                                            p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
+                    }
+                    sf = 0;
+                    jf++;
+                }
+            }
+            gf += n;
+        }
+        // ---- claim pixels for the free lanes (at most 64 pixels between fold and issue)
+        const unsigned long long fm = __ballot(!busy);
+        const uint32_t nfree = (uint32_t)__popcll(fm);
+        if (!qdone && nfree) {
+            // ordinals the free lanes would reach: ji + (si + nfree - 1) / spp, capped at jf + 63
+            uint32_t need = ji + (si + nfree - 1u) / spp + 1u;
+            if (need > jf + 64u) need = jf + 64u;
+            if (need > nclaimed) {
+                const uint32_t want = need - nclaimed;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(counter, want);
+                base = uni((uint32_t)__shfl((int)base, 0, 64));
+                uint32_t got = want;
+                if (base >= total) { got = 0; qdone = true; }
+                else if (base + want >= total) { got = total - base; qdone = true; }
+                const uint32_t rel = (lane - nclaimed) & 63u;
+                if (rel < got) pix_slot = base + rel;
+                nclaimed += got;
+            }
+        }
+        // ---- issue: free lanes take stream entries in lane order, within the window
+        {
+            const uint32_t rank = (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+            // entries available: up to fold + ring, and inside claimed pixels
+            uint32_t avail = kInwRing - (gi - gf);
+            const uint64_t left = (uint64_t)(nclaimed - ji) * spp - si;  // entries of claimed pixels not issued
+            if ((uint64_t)avail > left) avail = (uint32_t)left;
+            const uint32_t take = nfree < avail ? nfree : avail;
+            const uint32_t adv = si + rank;  // this lane's entry: pixel ji + adv / spp, sample adv % spp
+            const uint32_t jl = ji + adv / spp;
+            const uint32_t unit = (uint32_t)__shfl((int)pix_slot, (int)(jl & 63u), 64);
+            if (!busy && rank < take) {
+                g = gi + rank;
+                s = (int)(adv % spp);
+                px = unit_pixel(f, unit);
+                col = f3{0, 0, 0};
+                dep = 0.0f;
+                if (px.in_image) {
+                    busy = true;
+                    inw_start_sample(S, f, K, px.x, px.y, s, c);
+                } else {  // a padding slot: an empty sample, folded as zero
+                    if ((uint32_t)s == mid && f.out_depth && px.out != (size_t)-1) f.out_depth[px.out] = 0.0f;
+                    wr[g % kInwRing] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
+                }
+            }
+            gi += take;
+            const uint32_t a2 = si + take;
+            ji += a2 / spp;
+            si = a2 % spp;
+        }
+        if (qdone && ji == nclaimed && gf == gi && __ballot(busy) == 0) break;
+        // ---- one ray segment per busy lane (samples are independent invocations)
+        if (busy) inw_segment<LIGHTS>(S, f, K, s, col, dep, c);
+        if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
+            wr[g % kInwRing] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
+                                           __uint_as_float(g));
+            if ((uint32_t)s == mid && f.out_depth) f.out_depth[px.out] = dep;  // 01_BVH...glsl:667-668
+            busy = false;
+        }
+    }
+    flush(f, c);
 }
 
 // End() (01_BVH...glsl:664-675) over one chunk of samples: sum in sample order, depth of the
@@ -2632,6 +2814,8 @@ int resident_blocks_per_cu(int kind) {
     else if (kind == 6) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_s<false>, kBlock, 0);
     else if (kind == 7) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_s<true>, kBlock, 0);
     else if (kind == 14) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<true>, kBlock, 0);
+    else if (kind == 15) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_o<false>, kBlock, 0);
+    else if (kind == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_o<true>, kBlock, 0);
     else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<false>, kBlock, 0);
     return (e == hipSuccess && nb > 0) ? nb : 2;
 }
@@ -2884,6 +3068,15 @@ hipError_t launch_inw_spec(const Frame &f, const InwScene &sc, const SpecRecs &R
     const dim3 g(grid_of(n_units, blocks_cap));
     if (sc.layout == 4) hipLaunchKernelGGL(k_inw_s<true>, g, dim3(kBlock), 0, s, f, sc, R, s0, ns, ct, counter);
     else hipLaunchKernelGGL(k_inw_s<false>, g, dim3(kBlock), 0, s, f, sc, R, s0, ns, ct, counter);
+    return hipGetLastError();
+}
+hipError_t launch_inw_ordered(const Frame &f, const InwScene &sc, float4 *ring, unsigned *counter, int blocks,
+                              hipStream_t s) {
+    static_assert(kInwRingBytesPerBlock == (kBlock / 64) * kInwRing * sizeof(float4), "ring size");
+    hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    if (sc.layout == 4) hipLaunchKernelGGL(k_inw_o<true>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, counter);
+    else hipLaunchKernelGGL(k_inw_o<false>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, counter);
     return hipGetLastError();
 }
 hipError_t launch_inw_fin(const Frame &f, const SpecRecs &R, int s0, int ns, bool final_chunk, float4 *state,

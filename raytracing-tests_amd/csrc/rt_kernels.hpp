@@ -269,6 +269,9 @@ hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pa
 // then End() over that chunk: carry the sum in `state` or write the pixels
 hipError_t launch_inw_spec(const Frame &f, const InwScene &sc, const SpecRecs &R, int s0, int ns, const Cont &ct,
                            uint32_t n_units, unsigned *counter, int blocks_cap, hipStream_t s);
+hipError_t launch_inw_ordered(const Frame &f, const InwScene &sc, float4 *ring, unsigned *counter, int blocks,
+                              hipStream_t s);
+constexpr size_t kInwRingBytesPerBlock = 4 * 256 * 16;  // 4 waves x kInwRing entries x float4
 hipError_t launch_inw_fin(const Frame &f, const SpecRecs &R, int s0, int ns, bool final_chunk, float4 *state,
                           hipStream_t s);
 

@@ -25,6 +25,27 @@ def _no_lights(sc):
     return sc
 
 
+def _touching_cuboids(n=25, **over):
+    """INW-01 with unit cubes at unit spacing on the grid stage's layout: neighbouring cubes share
+    faces, and every face lies on its LBVH leaf box, where rounding can put an object's hit an ulp
+    before its box's entry t (the wide walk's leaf-entry guard, rt_kernels.hip inw_traverse_wide)."""
+    sc = R.make_scene(R.PRESET_INW01_GRID, 0, n, **over)
+    arr = sc.desc
+    for i in range(sc.n):
+        d = arr[i]
+        d.type = R.RT_INW_CUBOID
+        for k in range(3):
+            d.scale[k] = 1.0
+        d.position[2] = float(i % 2)  # a second row of faces along z
+        d.last_position[0], d.last_position[1], d.last_position[2] = d.position[0], d.position[1], d.position[2]
+        d.refractivity, d.reflectivity = (0.3, 0.6) if i % 3 else (0.0, 0.8)
+        d.scat_reflect = 0.0
+        d.scat_refract = 0.0
+    for k, v in R.pack(arr, sc.n, sc.stage).items():
+        setattr(sc, k, v)
+    return sc
+
+
 CASES = {
     # name: callable -> Scene (IOW-01 handled separately)
     "iow03_ref3": lambda: _scene(R.PRESET_IOW03_REF3, spp=4),
@@ -46,6 +67,7 @@ CASES = {
     "iow03_ref3_b1": lambda: _scene(R.PRESET_IOW03_REF3, spp=2, max_bounces=1),
     "inw01_random_one": lambda: _scene(R.PRESET_INW01_RANDOM, 5, 1, width=17, height=3, spp=4),
     "inw01_random_two": lambda: _scene(R.PRESET_INW01_RANDOM, 5, 2, width=33, height=7, spp=4),
+    "inw01_touching_cuboids": lambda: _touching_cuboids(25, width=64, height=64, spp=4, max_bounces=12),
     "inw04_cornell_odd": lambda: _scene(R.PRESET_INW04_CORNELL, 7, 0, width=13, height=11, spp=3, max_bounces=3),
 }
 
