@@ -96,8 +96,10 @@ rtk::Frame make_frame(const rt_camera *cam, const rt_params *p) {
     // (0 = off; every mode is bit-identical, tests/test_gpu_bvh_exact.py)
     const char *co = std::getenv("RT_COOP");
     f.coop_max = (co && *co) ? std::max(0, std::atoi(co)) : 4;
+#ifdef RT_DIAG  // diagnostic builds only (make variant VDEFS=-DRT_DIAG)
     const char *fs = std::getenv("RT_DEBUG_FIRST_STALE");
     f.dbg_first_stale = (fs && fs[0] == '1') ? 1 : 0;
+#endif
     return f;
 }
 
@@ -692,7 +694,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     if (rc != RT_OK) return rc;
     const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 1)));
     const int iters = std::max(0, env_int("RT_SPEC_ITERS", 1));
-    const int groups = S > 1 ? std::max(1, std::min(32, env_int("RT_SPEC_GROUPS", 1))) : 1;
+    const int groups = 1;  // one pipeline (per-group streams measured slower: 8.8 s with 4 groups)
     const size_t gmax = size_t(P + groups - 1) / groups + 1;  // pixels in the largest group
     if ((rc = ensure_cont(s)) != RT_OK) return rc;
     if ((rc = ensure_lanes(s, groups, rtk::sort_pairs_temp_bytes(gmax * S, 24))) != RT_OK) return rc;
@@ -706,7 +708,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                                                                                                   int(S - 1) / 20))))
                                                : 0u};
     s->launch_seq = 0;
-    if (env_int("RT_DEBUG_TIMES", 0) != 0) {  // diagnostics only (rt_debug_spec_times)
+#ifdef RT_DIAG
+    if (env_int("RT_DEBUG_TIMES", 0) != 0) {  // diagnostic builds only (rt_debug_spec_times)
         const size_t n = size_t(P) * S * 2 * sizeof(uint32_t);
         if (s->sp_dbg_t.bytes < n) {
             s->sp_dbg_t.~DevBuf();
@@ -718,6 +721,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         R.dbg_end = R.dbg_start + size_t(P) * S;
         s->sp_dbg_n = size_t(P) * S;
     }
+#endif
     const bool alt_on = env_int("RT_SPEC_ALT", 1) != 0 && s->n_alt_vals > 1 && S > 1;
     if (alt_on) {  // alternative runs (DESIGN.md "Alternative runs")
         // slots pack as first | count << 24 in the hash (alt_find): the cap stays below 2^24
@@ -746,7 +750,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     R.front2 = s->sp_front.as<uint4>() + P;  // the anchored scan's secondary frontier
     R.scan_max = uint32_t(std::max(0, env_int("RT_SPEC_SCAN", 128)));
     if (R.scan_max == 0) R.front2 = nullptr;
-    if (env_int("RT_SPEC_ORACLE", 0) != 0) {  // diagnostics only (see SpecRecs::exact)
+#ifdef RT_DIAG  // diagnostic builds only: copy one render's exact per-sample state into the next
+    if (env_int("RT_SPEC_ORACLE", 0) != 0) {  // (see SpecRecs::exact)
         const size_t n = size_t(P) * S;
         if (s->sp_exact_n != n) {
             s->sp_exact.~DevBuf();
@@ -759,6 +764,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         R.exact_mode = 1 | (s->sp_exact_valid ? 2 : 0);
         s->sp_exact_valid = true;
     }
+#endif
     rtk::IowScene scene{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
                         s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link,
                                  s->obox.as<float4>(), s->n_wide};
@@ -770,12 +776,10 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // one compacted pass on a stream with its own queue counter and continuation buffers: the
     // first launch takes `n0` units, resume launches take the parked lanes
     struct Lane { hipStream_t st; unsigned *counter; const DevBuf *cont; unsigned *cnt; };
-    // fix = true: before each resume launch, make the parked samples exact where possible
-    const bool fix_on = env_int("RT_SPEC_FIX", 0) != 0;  // measured neutral: off by default
     const bool spread_last = env_int("RT_SPEC_SPREAD", 1) != 0;
     // the first launch of the next pass takes its sorted head one unit per wave (Cont.solo_n)
     uint32_t solo_first = 0;
-    auto pass = [&](const Lane &q, auto &&launch, uint32_t n0, int cap, bool fix = false) {
+    auto pass = [&](const Lane &q, auto &&launch, uint32_t n0, int cap) {
         const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
         for (int r = 0; r <= rounds && e == hipSuccess; r++) {
             rtk::Cont ct{};
@@ -784,11 +788,6 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                 ct.in = q.cont[(r - 1) & 1].as<float4>();
                 ct.in_count = q.cnt + 16 * std::min(r - 1, 15);
                 n_units = uint32_t(cap) * rtk::kBlock;
-                if (fix && fix_on) {
-                    e = rtk::launch_iow03_fix(f, R, q.cont[(r - 1) & 1].as<float4>(), ct.in_count,
-                                              cap * rtk::kBlock, q.st);
-                    if (e != hipSuccess) break;
-                }
             }
             if (r < rounds) {
                 ct.out = q.cont[r & 1].as<float4>();
@@ -925,33 +924,14 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const Lane L0{st, s->counter.as<unsigned>(), s->cont, s->cont_count.as<unsigned>()};
     e = hipMemsetAsync(R.assume, 0, size_t(P) * sizeof(float4), st);
     if (e == hipSuccess) pass(L0, spec(R, rtk::kSpecFirst), P, cap_s);
-    if (S > 1 && env_int("RT_IOW_ASYNC", 0) != 0) {
-        // (2') asynchronous windows: the rest of the frame in one persistent launch
-        if (e == hipSuccess) e = rtk::launch_iow03_keys0(f, R, s->ws_cost.as<unsigned>(), st);
-        if (e == hipSuccess)
-            e = rtk::sort_units_by_cost(s->ws_cost.as<unsigned>(), s->ws_keys.as<unsigned>(), s->ws_iota.as<unsigned>(),
-                                        s->ws_order.as<unsigned>(), P, s->ws_temp.p, s->ws_temp_bytes, st);
-        s->last_kernel = "k_iow03a";
-        s->last_launches = 1;
-        if (e == hipSuccess)
-            e = rtk::launch_iow03_async(f, scene, R, s->counter.as<unsigned>(), R.epoch,
-                                        s->cus * rtk::resident_blocks_per_cu(8), st);
-        if (e != hipSuccess) {
-            std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
-            return RT_E_HIP;
-        }
-        return RT_OK;
-    }
     if (S > 1) {
         // Sample 1 starts from sample 0's final stack (exact: its written entries, 0 elsewhere).
         // From RT_SPEC_PRIOR_FROM (2) on every entry is guessed as the scene's most common RI
-        // (RT_SPEC_PRIOR_S0=1: keep sample 0's values where it wrote them, the round-1 rule).
         // The prior misses far less often (the re-run pass re-traces ~1% of the rays instead of
         // ~20% with zeros); the dependent chains it forms are cheap for the validating pass.
         const uint32_t prior_from = uint32_t(std::max(1, env_int("RT_SPEC_PRIOR_FROM", 2)));
         if (e == hipSuccess)
-            e = rtk::launch_iow03_prep(f, R, s->ws_cost.as<unsigned>(), s->ri_prior, prior_from,
-                                         env_int("RT_SPEC_PRIOR_S0", 0), st);
+            e = rtk::launch_iow03_prep(f, R, s->ws_cost.as<unsigned>(), s->ri_prior, prior_from, st);
         if (e == hipSuccess)
             e = rtk::sort_units_by_cost(s->ws_cost.as<unsigned>(), s->ws_keys.as<unsigned>(), s->ws_iota.as<unsigned>(),
                                         s->ws_order.as<unsigned>(), P, s->ws_temp.p, s->ws_temp_bytes, st);
@@ -976,7 +956,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         e = hipStreamWaitEvent(L.st, s->ev_start, 0);
         if (S > 1 && e == hipSuccess) {
             if (ckpt > 0) ckpt_pass(L, RG, cnt_g * (S - 1));
-            else pass(L, spec(RG, rtk::kSpecRest), cnt_g * (S - 1), cap_s, true);
+            else pass(L, spec(RG, rtk::kSpecRest), cnt_g * (S - 1), cap_s);
         }
         for (int it = 0; it < iters && e == hipSuccess; it++) {
             e = hipMemsetAsync(RG.list_count, 0, sizeof(unsigned), L.st);
@@ -993,9 +973,9 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                 rtk::SpecRecs R2 = RG;
                 R2.list = l2;
                 solo_first = uint32_t(std::max(0, env_int("RT_SOLO", 4096)));
-                if (e == hipSuccess) pass(L, spec(R2, rtk::kSpecList), uint32_t(nmax), cap_s, true);
+                if (e == hipSuccess) pass(L, spec(R2, rtk::kSpecList), uint32_t(nmax), cap_s);
                 solo_first = 0;
-            } else if (e == hipSuccess) pass(L, spec(RG, rtk::kSpecList), uint32_t(nmax), cap_s, true);
+            } else if (e == hipSuccess) pass(L, spec(RG, rtk::kSpecList), uint32_t(nmax), cap_s);
         }
         if (e == hipSuccess) e = hipMemsetAsync(RG.fb_count, 0, sizeof(unsigned), L.st);
         if (e == hipSuccess) e = rtk::launch_iow03_resolve(f, RG, true, s->ws_state.as<float4>(), L.st);

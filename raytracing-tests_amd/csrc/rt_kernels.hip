@@ -602,7 +602,9 @@ __device__ __forceinline__ void iow_seg_shade(const IowScene &S, const Frame &F,
             if (cos_t > 0.0f && pi >= 0 && pi < kIowStack && !((K.wmask >> pi) & 1u)) {
                 // diagnostics (RT_DEBUG_FIRST_STALE): the segment of the first stale read replaces
                 // the unit's drop counter
+#ifdef RT_DIAG
                 if (F.dbg_first_stale && K.rmask == 0u) c.drops = 0x80000000u | c.seg;
+#endif
                 K.rmask |= 1u << pi;
             }
         }
@@ -1079,7 +1081,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         p[0] = make_float4(ubits(u), ibits(skip), ibits(K.size), ubits(K.wmask | (K.rmask << 4)));
         p[1] = make_float4(sample.x, sample.y, sample.z, ubits(urays));
         p[2] = make_float4(ubits(c.seg), ubits(c.nodes), ubits(c.prims), ubits(c.drops));
-        // .y: restart flag (k_iow03_fix), .z: exact, .w: alternative slot + 1 (bits)
+        // .y: restart flag (k_iow03_fixf), .z: exact, .w: alternative slot + 1 (bits)
         p[12] = make_float4(ubits(c.nans), 0.0f, exact ? 1.0f : 0.0f, ubits(alt_slot));
         float *fl = reinterpret_cast<float *>(p + 3);
         for (int k = 0; k < kFl; k++) fl[k] = K.base[k * kBlock];
@@ -1089,7 +1091,9 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     // start unit u (sample s of pixel pu) with assumed stack RI a.xyz in entries 1..3
     auto begin = [&](uint32_t u_, float4 a) {
         u = u_;
+#ifdef RT_DIAG
         if (R.dbg_start) R.dbg_start[u] = (ct.launch_id & 0xffffu) | ((R.dbg_start[u] >> 16) + 1u) << 16;
+#endif
         const uint32_t pu = u % R.P;
         const int s = (int)(u / R.P);
         const UnitPix px = unit_pixel(f, pu);
@@ -1224,7 +1228,9 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                                    ubits(K.rmask | (K.wmask << 4) | done_tag | ((ct.launch_id & 63u) << 10)));
             R.fin[u] = make_float4(K.at(1, 7), K.at(2, 7), K.at(3, 7), ubits(c.prims));
             R.ctr[u] = make_uint4(c.seg, c.drops, c.nans, c.nodes);
+#ifdef RT_DIAG
             if (R.dbg_end) R.dbg_end[u] = ct.launch_id;
+#endif
             busy = false;
             if (exact) {
                 // Chain following: the stack this exact sample left is the exact incoming state of
@@ -1286,56 +1292,6 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
         for (int i = 0; i < kDbgSlots; i++) atomicAdd(f.dbg + i, c.wdbg[i]);
 }
 
-// Between launches of a sample-parallel pass (a kernel boundary, so every record written so far
-// is visible): for each parked sample whose pixel's earlier samples are all finished and valid,
-// the exact incoming stack state E is known.  Entries the sample neither read nor wrote are set
-// to E (exact: it would have started with them); if an entry it already read differs from E,
-// it is doomed and restarts with E on resume.  Either way its assumption becomes exact, so long
-// samples stop waiting for a later resolve pass to be found wrong.
-__global__ __launch_bounds__(kBlock) void k_iow03_fix(Frame f, SpecRecs R, float4 *cont, const unsigned *count) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= *count) return;  // no cross-lane work in this kernel
-    float4 *p = cont + (size_t)i * kContSlots;
-    const uint32_t u = __float_as_uint(p[0].x);
-    if (p[12].y != 0.0f || __float_as_uint(p[12].w) != 0u) return;  // a restart / an alternative run
-    const uint32_t pu = u % R.P, s = u / R.P;
-    const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
-    unsigned E1 = 0, E2 = 0, E3 = 0;
-    for (uint32_t t = 0; t < s; t++) {
-        const size_t uu = (size_t)t * R.P + pu;
-        const unsigned fl = __float_as_uint(R.col[uu].w);
-        if ((fl & 0xffff0100u) != done_tag) return;  // an earlier sample is still running
-        const float4 a = R.assume[uu];
-        const unsigned rm = fl & 15u, wm = (fl >> 4) & 15u;
-        if (((rm & 2u) && __float_as_uint(a.x) != E1) || ((rm & 4u) && __float_as_uint(a.y) != E2) ||
-            ((rm & 8u) && __float_as_uint(a.z) != E3))
-            return;  // an earlier sample is itself wrong: E is not known yet
-        const float4 fn = R.fin[uu];
-        if (wm & 2u) E1 = __float_as_uint(fn.x);
-        if (wm & 4u) E2 = __float_as_uint(fn.y);
-        if (wm & 8u) E3 = __float_as_uint(fn.z);
-    }
-    const unsigned masks = __float_as_uint(p[0].w), wm = masks & 15u, rm = masks >> 4;
-    float4 a = R.assume[u];
-    const unsigned E[3] = {E1, E2, E3};
-    float *av = &a.x;
-    bool doomed = false;
-    for (int k = 1; k <= 3; k++)
-        if (((rm >> k) & 1u) && __float_as_uint(av[k - 1]) != E[k - 1]) doomed = true;
-    if (doomed) {
-        R.assume[u] = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
-        p[12].y = 1.0f;
-        return;
-    }
-    float *fl = reinterpret_cast<float *>(p + 3);  // parked stack, [entry*9 + field], RI = field 7
-    for (int k = 1; k <= 3; k++)
-        if (!((wm >> k) & 1u) && !((rm >> k) & 1u)) {
-            fl[k * 9 + 7] = __uint_as_float(E[k - 1]);
-            av[k - 1] = __uint_as_float(E[k - 1]);
-        }
-    R.assume[u] = a;
-}
-
 __global__ __launch_bounds__(kBlock) void k_iow03s(Frame f, IowScene S, SpecRecs R, int mode, Cont ct,
                                                    unsigned *counter) {
     iow03s_body<false, 1, false>(f, S, R, mode, ct, counter);
@@ -1351,7 +1307,7 @@ __global__ __launch_bounds__(3 * kBlock) void k_iow03sL(Frame f, IowScene S, Spe
 // almost always hold once any sample has pushed there).  Pixels are keyed by sample 0's ray
 // count so the rest run heaviest first.
 __global__ __launch_bounds__(kBlock) void k_iow03_prep(Frame f, SpecRecs R, unsigned *key, float prior,
-                                                       uint32_t prior_from, int keep_s0) {
+                                                       uint32_t prior_from) {
     const uint32_t pu = blockIdx.x * kBlock + threadIdx.x;
     if (pu >= R.P) return;  // no cross-lane work in this kernel
     const UnitPix px = unit_pixel(f, pu);
@@ -1359,16 +1315,16 @@ __global__ __launch_bounds__(kBlock) void k_iow03_prep(Frame f, SpecRecs R, unsi
     const uint32_t wm = (__float_as_uint(R.col[pu].w) >> 4) & 15u;
     const float4 fn = R.fin[pu];
     const float4 e0 = make_float4((wm & 2u) ? fn.x : 0.0f, (wm & 4u) ? fn.y : 0.0f, (wm & 8u) ? fn.z : 0.0f, 0.0f);
-    // From prior_from on every entry is guessed as the prior unless keep_s0: sample 0 starts from
-    // the all-zero stack no later sample sees (a stale 0 makes target_RI 0 and forces TIR,
-    // 03...glsl:316-327), so the values it leaves are a worse guess of the steady state than the
-    // scene's most common RI (tests/analysis/fork_stats.py: mispredicted rays 2.6% -> 0.8% on C2).
-    const bool k0 = keep_s0 != 0;
-    const float4 e1 = make_float4((k0 && (wm & 2u)) ? fn.x : prior, (k0 && (wm & 4u)) ? fn.y : prior,
-                                  (k0 && (wm & 8u)) ? fn.z : prior, 0.0f);
+    // From prior_from on every entry is guessed as the prior: sample 0 starts from the all-zero
+    // stack no later sample sees (a stale 0 makes target_RI 0 and forces TIR, 03...glsl:316-327),
+    // so the values it leaves are a worse guess of the steady state than the scene's most common
+    // RI (tests/analysis/fork_stats.py: mispredicted rays 2.6% -> 0.8% on C2).
+    const float4 e1 = make_float4(prior, prior, prior, 0.0f);
     for (uint32_t s = 1; s < R.S; s++) R.assume[(size_t)s * R.P + pu] = s >= prior_from ? e1 : e0;
+#ifdef RT_DIAG
     if (R.exact && (R.exact_mode & 2))
         for (uint32_t s = 1; s < R.S; s++) R.assume[(size_t)s * R.P + pu] = R.exact[(size_t)s * R.P + pu];
+#endif
     if (R.front)  // sample 0 is exact: the frontier starts at sample 1 with its final entries
         R.front[pu] = make_uint4(1u, __float_as_uint(e0.x), __float_as_uint(e0.y), __float_as_uint(e0.z));
     if (R.front2) R.front2[pu] = make_uint4(0xffffffffu, 0u, 0u, 0u);
@@ -1539,9 +1495,10 @@ __global__ __launch_bounds__(kBlock) void k_iow03_altspawn(Frame f, SpecRecs R, 
     }
 }
 
-// Parked samples at their pixel's frontier: the exact incoming state E is known.  As in
-// k_iow03_fix: entries the sample neither read nor wrote get E; if an entry it read differs
-// from E it restarts with E.  Either way its assumption becomes exact.
+// Parked samples at their pixel's frontier: the exact incoming state E is known.  Entries the
+// sample neither read nor wrote get E (exact: it would have started with them); if an entry it
+// already read differs from E it restarts with E.  Either way its assumption becomes exact, so
+// long samples stop waiting for a later resolve pass to find them wrong.
 __global__ __launch_bounds__(kBlock) void k_iow03_fixf(Frame f, SpecRecs R, float4 *cont, const unsigned *count) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= *count) return;  // no cross-lane work in this kernel
@@ -1594,8 +1551,10 @@ __global__ __launch_bounds__(kBlock) void k_iow03_resolve(Frame f, SpecRecs R, i
         float4 cl = R.col[u];
         uint32_t fl = __float_as_uint(cl.w), rm = fl & 15u, wm = (fl >> 4) & 15u;
         float4 a = R.assume[u];
+#ifdef RT_DIAG
         if (final_pass && R.exact && (R.exact_mode & 1) && first_bad < 0)
             R.exact[u] = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
+#endif
         bool bad = ((rm & 2u) && __float_as_uint(a.x) != E1) || ((rm & 4u) && __float_as_uint(a.y) != E2) ||
                    ((rm & 8u) && __float_as_uint(a.z) != E3);
         if (bad && first_bad < 0 && R.alt && alt_adopt(R, (uint32_t)u, E1, E2, E3, 0xffffffffu, 0u)) {
@@ -2291,229 +2250,6 @@ __global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S, Chunk ch, C
     flush(f, c);
 }
 
-// ============================================================================ IOW-03, asynchronous windows
-// The sample-parallel scheme without global passes.  A wave takes pixels from the global queue
-// and issues all their samples to its own lanes, so every record of a pixel is written and read
-// by one wave (workgroup-scope visibility, no cross-CU hand-off).  Per pixel the wave keeps, in
-// global memory, a frontier: samples below it are validated and the exact stack state E before
-// it is known.  When a sample finishes, the frontier of its pixel advances over finished samples
-// in sample order; a misprediction is re-run at once, by the lane that found it, with E, which
-// is exact there, so re-runs never chain.  A sample issued when the frontier already stands at
-// it also uses E.  A pixel whose samples are all issued no longer holds a slot, so the wave keeps
-// issuing new pixels while long samples finish; nothing waits for a global pass.
-constexpr int kIss = 2;   // pixels a wave is issuing samples from
-constexpr int kBvA = 28;  // BVH stack entries
-struct IssueSlot {
-    int pu;             // pixel unit, -1 = empty
-    int next;           // next sample to issue
-    unsigned G[3];      // guess for samples issued ahead of the frontier (state after sample 0)
-};
-// per-pixel frontier state in global memory (SpecRecs.pstate, 3 x uint4 per pixel unit):
-//   [0] fr, E0, E1, E2   [1] fc.xyz (bits), seg   [2] drops, nans, nodes, prims
-
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-__global__ __launch_bounds__(kBlock) void k_iow03a(Frame f, IowScene S, SpecRecs R, unsigned *counter, unsigned epoch) {
-    constexpr int kFl = kIowStack * 9;
-    constexpr int BCAP = kBvA - 3;
-    __shared__ float lds[kFl * kBlock];
-    __shared__ short lds_bvh[kBvA * kBlock];
-    __shared__ unsigned long long s_dbg[kBlock / 64][kDbgSlots];
-    __shared__ IssueSlot s_iss[kBlock / 64][kIss];
-    short *bstk = lds_bvh + threadIdx.x;
-    const int lane = (int)(threadIdx.x & 63);
-    IssueSlot *iss = s_iss[threadIdx.x >> 6];
-    Ctr c;  // counters of the lane's current unit
-    if (f.dbg) {
-        c.wdbg = s_dbg[threadIdx.x >> 6];
-        if (lane < kDbgSlots) c.wdbg[lane] = 0;
-    }
-    IowStack<false> K{lds + threadIdx.x, nullptr, 0};
-    if (lane < kIss) iss[lane].pu = -1;
-    wave_sync_lds();
-    const uint32_t P = R.P, SS = R.S;
-    const int W = f.W, H = f.H;
-    int grid = 1;
-    while (grid * grid < f.spp) grid++;
-    const float aspect = (float)W * rcp((float)H);
-    const float dsx = aspect * rcp((float)(W * grid));
-    const float dsy = 1.0f * rcp((float)(H * grid));
-    const unsigned done_tag = (1u << 8) | ((epoch & 0xffffu) << 16);
-    bool busy = false, exhausted = false;
-    uint32_t u = 0, pu = 0;
-    int s = 0, skip = 0;
-    f3 sample = f3{0, 0, 0};
-    unsigned long long acc[5] = {0, 0, 0, 0, 0};  // seg, nodes, prims, drops, nans of finished pixels
-    // start sample s of pixel pu on this lane with assumed stack RI a1..a3
-    auto start = [&](uint32_t p_, int s_, unsigned a1, unsigned a2, unsigned a3) {
-        pu = p_; s = s_;
-        u = (uint32_t)s * P + pu;
-        R.assume[u] = make_float4(__uint_as_float(a1), __uint_as_float(a2), __uint_as_float(a3), 0.0f);
-        busy = true;
-        c.seg = c.nodes = c.prims = c.drops = c.nans = 0;
-        skip = 0;
-        sample = f3{0, 0, 0};
-        K.size = 0; K.wmask = 0; K.rmask = 0;
-        K.at(0, 7) = 0.0f; K.at(1, 7) = __uint_as_float(a1); K.at(2, 7) = __uint_as_float(a2); K.at(3, 7) = __uint_as_float(a3);
-        const UnitPix px = unit_pixel(f, pu);
-        const float sx = (aspect * ((float)px.x * 2.0f - (float)W)) * rcp(2.0f * (float)W);
-        const float sy = ((float)px.y * 2.0f - (float)H) * rcp(2.0f * (float)H);
-        f3 ro, rd;
-        iow_camera_ray(S, f, sx, sy, dsx, dsy, s, ro, rd);
-        if (f.show_normal) sample = iow_launch_ray<BCAP>(S, f, ro, rd, 32000.0f, 1.0f, c, bstk, S.nodes).normal;
-        else K.push(ro, rd, 1.0f, 1.0f, 0, c);
-    };
-    for (;;) {
-        // (1) refill empty issue slots from the global pixel queue (heaviest sample 0 first)
-        const bool empty = lane < kIss && iss[lane].pu < 0;
-        const unsigned long long em = __ballot(empty);
-        if (!exhausted && em) {
-            const int leader = __ffsll((long long)em) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(counter, (unsigned)__popcll(em));
-            base = __shfl(base, leader, 64);
-            const uint32_t q = base + (uint32_t)__popcll(em & ((1ull << lane) - 1ull));
-            if (empty && q < P) {
-                const uint32_t p_ = R.order[q];
-                const UnitPix px = unit_pixel(f, p_);
-                if (!px.in_image) write_px(f, px, f3{0, 0, 0}, 0.0f);  // tile padding: done
-                else {  // sample 0 ran exactly in the first pass: frontier at 1
-                    const float4 c0 = R.col[p_], f0 = R.fin[p_];
-                    const uint4 k0 = R.ctr[p_];
-                    const unsigned wm = (__float_as_uint(c0.w) >> 4) & 15u;
-                    const unsigned e0 = (wm & 2u) ? __float_as_uint(f0.x) : 0u;
-                    const unsigned e1 = (wm & 4u) ? __float_as_uint(f0.y) : 0u;
-                    const unsigned e2 = (wm & 8u) ? __float_as_uint(f0.z) : 0u;
-                    uint4 *ps = R.pstate + 3 * (size_t)p_;
-                    ps[0] = make_uint4(1u, e0, e1, e2);
-                    ps[1] = make_uint4(__float_as_uint(c0.x), __float_as_uint(c0.y), __float_as_uint(c0.z), k0.x);
-                    ps[2] = make_uint4(k0.y, k0.z, k0.w, __float_as_uint(f0.w));
-                    if (SS <= 1) {  // nothing left to issue
-                        write_px(f, px, f3{c0.x, c0.y, c0.z} * rcp((float)SS), 0.0f);
-                        acc[0] += k0.x; acc[1] += k0.w; acc[2] += __float_as_uint(f0.w); acc[3] += k0.y; acc[4] += k0.z;
-                        if (f.px_rays) f.px_rays[p_] = k0.x;
-                    } else {
-                        iss[lane].G[0] = e0; iss[lane].G[1] = e1; iss[lane].G[2] = e2;
-                        iss[lane].next = 1;
-                        iss[lane].pu = (int)p_;
-                    }
-                }
-            }
-            if (__ballot(empty && q >= P) != 0) exhausted = true;
-        }
-        __threadfence_block();  // pixel states before any lane reads them
-        wave_sync_lds();
-        // (2) idle lanes take the next samples of the issue slots, in slot order
-        const unsigned long long idle = __ballot(!busy);
-        if (idle) {
-            const int me = (int)__popcll(idle & ((1ull << lane) - 1ull));
-            const int n_idle = (int)__popcll(idle);
-            int before = 0;
-            for (int k = 0; k < kIss && before < n_idle; k++) {
-                const int pk = iss[k].pu;
-                if (pk < 0) continue;
-                const int nx = iss[k].next;
-                const int take = min((int)SS - nx, n_idle - before);
-                if (!busy && me >= before && me < before + take) {
-                    const int s_ = nx + (me - before);
-                    const uint4 st0 = R.pstate[3 * (size_t)pk];  // frontier and exact state
-                    const bool exact = (int)st0.x == s_;
-                    start((uint32_t)pk, s_, exact ? st0.y : iss[k].G[0], exact ? st0.z : iss[k].G[1],
-                          exact ? st0.w : iss[k].G[2]);
-                }
-                if (lane == k) {  // one writer per slot
-                    iss[k].next = nx + take;
-                    if (nx + take >= (int)SS) iss[k].pu = -1;  // all issued: the pixel leaves the window
-                }
-                before += take;
-            }
-        }
-        wave_sync_lds();
-        // (3) one ray segment per busy lane
-        DBG_TALLY(f, c, kDbgOuter, busy);
-        DBG_TALLY(f, c, kDbgSeg, busy && K.size > 0);
-        DBG_T0(f, t_seg);
-        if (busy && K.size > 0) iow_segment<false, kBvA, 8>(S, f, K, skip, sample, s, c, bstk, S.nodes);
-        DBG_CYC(f, c, kDbgCycSeg, t_seg);
-        // (4) finished samples write their record
-        const bool fin = busy && K.size == 0;
-        if (fin) {
-            R.col[u] = make_float4(sample.x, sample.y, sample.z, __uint_as_float(K.rmask | (K.wmask << 4) | done_tag));
-            R.fin[u] = make_float4(K.at(1, 7), K.at(2, 7), K.at(3, 7), __uint_as_float(c.prims));
-            R.ctr[u] = make_uint4(c.seg, c.drops, c.nans, c.nodes);
-            busy = false;
-        }
-        __threadfence_block();  // the records before the frontier reads them
-        // (5) advance the frontier of every pixel that just had a sample finish, one lane per pixel
-        unsigned long long fm = __ballot(fin);
-        while (fm) {
-            const int ld = __ffsll((long long)fm) - 1;
-            const uint32_t pid = __shfl(pu, ld, 64);
-            fm &= ~__ballot(fin && pu == pid);
-            if (lane == ld) {
-                uint4 *ps = R.pstate + 3 * (size_t)pid;
-                uint4 st0 = ps[0], st1 = ps[1], st2 = ps[2];
-                int fr = (int)st0.x;
-                f3 fc = f3{__uint_as_float(st1.x), __uint_as_float(st1.y), __uint_as_float(st1.z)};
-                bool bad = false;
-                while (fr < (int)SS) {
-                    const size_t uu = (size_t)fr * P + pid;
-                    const float4 cl = R.col[uu];
-                    const unsigned fl = __float_as_uint(cl.w);
-                    if ((fl & 0xffff0100u) != done_tag) break;  // not finished in this frame yet
-                    const float4 a = R.assume[uu];
-                    const unsigned rm = fl & 15u, wm = (fl >> 4) & 15u;
-                    if (((rm & 2u) && __float_as_uint(a.x) != st0.y) || ((rm & 4u) && __float_as_uint(a.y) != st0.z) ||
-                        ((rm & 8u) && __float_as_uint(a.z) != st0.w)) { bad = true; break; }
-                    fc = fc + f3{cl.x, cl.y, cl.z};
-                    const float4 fn = R.fin[uu];
-                    const uint4 k4 = R.ctr[uu];
-                    st1.w += k4.x; st2.x += k4.y; st2.y += k4.z; st2.z += k4.w; st2.w += __float_as_uint(fn.w);
-                    if (wm & 2u) st0.y = __float_as_uint(fn.x);
-                    if (wm & 4u) st0.z = __float_as_uint(fn.y);
-                    if (wm & 8u) st0.w = __float_as_uint(fn.z);
-                    fr++;
-                }
-                st0.x = (unsigned)fr;
-                st1.x = __float_as_uint(fc.x); st1.y = __float_as_uint(fc.y); st1.z = __float_as_uint(fc.z);
-                ps[0] = st0; ps[1] = st1; ps[2] = st2;
-                if (bad) {
-                    // mark the record unfinished (its re-run rewrites it) and re-run it here with E
-                    R.col[(size_t)fr * P + pid].w = 0.0f;
-                    start(pid, fr, st0.y, st0.z, st0.w);
-                } else if (fr >= (int)SS) {  // pixel complete
-                    write_px(f, unit_pixel(f, pid), fc * rcp((float)SS), 0.0f);
-                    acc[0] += st1.w; acc[1] += st2.z; acc[2] += st2.w; acc[3] += st2.x; acc[4] += st2.y;
-                    if (f.px_rays) f.px_rays[pid] = st1.w;
-                }
-            }
-        }
-        __threadfence_block();
-        wave_sync_lds();
-        if (exhausted && __ballot(busy) == 0 && __ballot(lane < kIss && iss[lane].pu >= 0) == 0) break;
-    }
-    if (c.wdbg && lane == 0)
-        for (int i = 0; i < kDbgSlots; i++) atomicAdd(f.dbg + i, c.wdbg[i]);
-    if (f.counters) {
-        const int slot_of[5] = {0, 1, 2, 4, 5};
-#pragma unroll
-        for (int i = 0; i < 5; i++) {
-            const unsigned long long t = wave_sum(acc[i]);
-            if (lane == 0 && t) atomicAdd(f.counters + slot_of[i], t);
-        }
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_iow03_keys0(Frame f, SpecRecs R, unsigned *key) {
-    const uint32_t pu = blockIdx.x * kBlock + threadIdx.x;
-    if (pu >= R.P) return;  // no cross-lane work
-    key[pu] = unit_pixel(f, pu).in_image ? R.ctr[pu].x : 0u;
-}
-
 // ---------------------------------------------------------------- INW, sample-parallel
 // One unit = one sample of one pixel (u = (s - s0)*P + pu within a chunk of samples [s0, s0+ns)).
 // INW samples are independent invocations (01_BVH...glsl:601-675), so no speculation is needed:
@@ -2810,7 +2546,6 @@ int resident_blocks_per_cu(int kind) {
     else if (kind == 10) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03sL, 3 * kBlock, 0);
     else if (kind == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03n, kBlock, 0);
     else if (kind == 5) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03s, kBlock, 0);
-    else if (kind == 8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03a, kBlock, 0);
     else if (kind == 6) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_s<false>, kBlock, 0);
     else if (kind == 7) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_s<true>, kBlock, 0);
     else if (kind == 14) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<true>, kBlock, 0);
@@ -2931,24 +2666,6 @@ hipError_t spec_list_keys(const SpecRecs &R, unsigned *keys, size_t n, hipStream
     hipLaunchKernelGGL(k_spec_list_keys, dim3(4096), dim3(256), 0, s, R, keys, n);
     return hipGetLastError();
 }
-hipError_t launch_iow03_async(const Frame &f, const IowScene &sc, const SpecRecs &R, unsigned *counter,
-                              unsigned epoch, int blocks, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_iow03a, dim3(blocks > 0 ? blocks : 1), dim3(kBlock), 0, s, f, sc, R, counter, epoch);
-    return hipGetLastError();
-}
-hipError_t launch_iow03_fix(const Frame &f, const SpecRecs &R, float4 *cont, const unsigned *count, int max_lanes,
-                            hipStream_t s) {
-    const unsigned blocks = (unsigned)((max_lanes + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_iow03_fix, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, cont, count);
-    return hipGetLastError();
-}
-hipError_t launch_iow03_keys0(const Frame &f, const SpecRecs &R, unsigned *key, hipStream_t s) {
-    const unsigned blocks = (R.P + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_iow03_keys0, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, key);
-    return hipGetLastError();
-}
 // ---------------------------------------------------------------- heavy-first enumeration
 // cost of sample index s (1..S-1) over the probe pixels: finished records (block s-1)
 __global__ __launch_bounds__(kBlock) void k_sample_cost(SpecRecs R, unsigned long long *fcost) {
@@ -3050,10 +2767,9 @@ hipError_t launch_iow03_fixf(const Frame &f, const SpecRecs &R, float4 *cont, co
     return hipGetLastError();
 }
 hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,
-                             int keep_s0, hipStream_t s) {
+                             hipStream_t s) {
     const unsigned blocks = (R.P + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_iow03_prep, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, key, prior, prior_from,
-                       keep_s0);
+    hipLaunchKernelGGL(k_iow03_prep, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, key, prior, prior_from);
     return hipGetLastError();
 }
 hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pass, float4 *state, hipStream_t s) {

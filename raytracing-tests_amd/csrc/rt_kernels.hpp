@@ -229,16 +229,6 @@ hipError_t spec_list_hist(const uint4 *ctr, const uint32_t *list, const unsigned
                           hipStream_t s);  // diagnostics
 hipError_t spec_pixels(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *order, uint32_t *d_out,
                        hipStream_t s);  // diagnostics
-// asynchronous-window IOW-03 over samples 1.. (after the kSpecFirst pass and the pixel order):
-// every pixel's samples, validation and re-runs inside one persistent launch; writes the pixels
-hipError_t launch_iow03_async(const Frame &f, const IowScene &sc, const SpecRecs &R, unsigned *counter,
-                              unsigned epoch, int blocks, hipStream_t s);
-// between launches of a pass: make parked samples exact where their pixel's earlier samples are
-// all finished and validated (patch unread stack entries, or restart a doomed sample)
-hipError_t launch_iow03_fix(const Frame &f, const SpecRecs &R, float4 *cont, const unsigned *count, int max_lanes,
-                            hipStream_t s);
-// sort keys = sample 0's ray count per pixel unit (0 for tile padding)
-hipError_t launch_iow03_keys0(const Frame &f, const SpecRecs &R, unsigned *key, hipStream_t s);
 // after the kSpecFirst pass: assumptions for samples 1.. and the per-pixel ordering keys
 // checkpoint rounds: advance each pixel's frontier over finished, valid samples and
 // queue a finished sample at the frontier whose assumption was wrong for an exact re-run
@@ -260,7 +250,7 @@ hipError_t launch_check_fastmath(int which, unsigned long long *bad, unsigned *f
 hipError_t launch_iow03_altspawn(const Frame &f, const SpecRecs &R, float4 *cont, unsigned *count, uint32_t cap,
                                  hipStream_t s);
 hipError_t launch_iow03_prep(const Frame &f, const SpecRecs &R, unsigned *key, float prior, uint32_t prior_from,
-                             int keep_s0, hipStream_t s);
+                             hipStream_t s);
 // replay each pixel's samples: re-queue wrong assumptions; final: write clean pixels, hand
 // the rest (with their resume state in `state`) to the sequential kernel via R.fb_list
 hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pass, float4 *state, hipStream_t s);

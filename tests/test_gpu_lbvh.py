@@ -1,6 +1,7 @@
 """GPU LBVH builder (rt_lbvh_build_gpu / rt_lbvh_build_async): node-for-node
-bit-identical to the host builder (rt_lbvh_build), which the CPU tests pin against the oracle's
-restatement of LBVH::ConstructLBVH_Buff (lbvh.h:215-269).  Edge cases: N = 1 and 2, duplicate
+bit-identical to the oracle's restatement of LBVH::ConstructLBVH_Buff (lbvh.h:215-269,
+oracle/rt_oracle_host.c via O.lbvh_build), and to the host product builder (rt_lbvh_build).
+Edge cases: N = 1 and 2, duplicate
 centroids (equal Morton codes: the chain the reference's index-ordered merge builds), a
 degenerate scene (every box identical, scene extent 0), signed zeros, and the INW presets'
 own boxes, up to N = 200k."""
@@ -8,6 +9,7 @@ import numpy as np
 import pytest
 
 import rt_amd as R
+from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
@@ -45,11 +47,12 @@ CASES = [
 
 
 @pytest.mark.parametrize("name,boxes", CASES, ids=[c[0] for c in CASES])
-def test_gpu_lbvh_equals_host(gpu, name, boxes):
-    host = R.lbvh_build(boxes)
+def test_gpu_lbvh_equals_oracle(gpu, name, boxes):
+    ref = O.lbvh_build(boxes)
     dev, ms = R.lbvh_build_gpu(boxes)
-    bad = np.argwhere(~(host.view(np.uint32) == dev.view(np.uint32)).all(axis=1))
-    assert _same(host, dev), f"{len(bad)} nodes differ, first {bad[:5].ravel().tolist()}"
+    bad = np.argwhere(~(ref.view(np.uint32) == dev.view(np.uint32)).all(axis=1))
+    assert _same(ref, dev), f"{len(bad)} nodes differ from the oracle, first {bad[:5].ravel().tolist()}"
+    assert _same(R.lbvh_build(boxes), dev)  # and the host product builder agrees
 
 
 @pytest.mark.parametrize("preset,seed,n_hint", [(R.PRESET_INW01_RANDOM, 1234, 10_000),
@@ -58,4 +61,4 @@ def test_gpu_lbvh_equals_host(gpu, name, boxes):
 def test_gpu_lbvh_on_preset_scenes(gpu, preset, seed, n_hint):
     sc = R.make_scene(preset, seed, n_hint)
     dev, _ = R.lbvh_build_gpu(sc.aabbs)
-    assert _same(sc.nodes, dev)
+    assert _same(O.lbvh_build(sc.aabbs), dev)

@@ -63,7 +63,8 @@ def test_spiral_progressive_equals_full_frame(gpu, preset, seed, n_hint, w, h, s
 
 def _unorm8(x):
     x = np.asarray(x, np.float32)
-    out = np.floor(np.clip(x, 0, 1) * np.float32(255) + np.float32(0.5)).astype(np.uint8)
+    # NaN -> 0 before the cast (casting NaN to uint8 is undefined and warns)
+    out = np.floor(np.nan_to_num(np.clip(x, 0, 1), nan=0.0) * np.float32(255) + np.float32(0.5)).astype(np.uint8)
     out[~(x > 0)] = 0
     out[x >= 1] = 255
     return out
