@@ -145,7 +145,8 @@ struct rt_dev_scene {
     DevBuf sp_pstate;  // asynchronous windows: per-pixel frontier state
     DevBuf sp_front;   // checkpoint rounds: per-pixel frontier (uint4)
     DevBuf sp_sorder, sp_fcost;  // heavy-first enumeration: sample indices by cost, their costs
-    DevBuf inw_ring;             // k_inw_o: the waves' fold rings (kInwRingBytesPerBlock per block)
+    DevBuf inw_ring;             // k_inw_pm / k_inw_sm: the waves' fold rings
+    DevBuf inw_mode;             // k_inw_probe's verdict (2 uints)
     DevBuf sp_dbg_t;             // RT_DEBUG_TIMES diagnostics: per unit start / end launch
     size_t sp_dbg_n = 0;         // units (P * S) of the render that last wrote sp_dbg_t
     uint32_t launch_seq = 0;
@@ -195,7 +196,8 @@ int build_tables(rt_dev_scene *s, int spp) {
     s->s_stop = spp;
     for (int i = 0; i < spp; i++)
         if (ring[size_t(i) * 2] < 0) { s->s_stop = i; break; }
-    HIP_OK(s->counter.alloc(64));
+    HIP_OK(s->counter.alloc(256));  // queue counters 64 B apart (the INW fold launches use two)
+    HIP_OK(s->inw_mode.alloc(64));
     return RT_OK;
 }
 
@@ -563,7 +565,7 @@ int ensure_inw_spec(rt_dev_scene *s, uint32_t P, int spp) {
 }
 
 int launch_scene_inw_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st, int ns);
-int launch_scene_inw_ordered(rt_dev_scene *s, rtk::Frame &f, hipStream_t st);
+int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st);
 
 // Enqueue a whole render (all chunks) on `st`.  The first call for a given frame size
 // allocates the chunk workspace; later calls allocate nothing.
@@ -575,7 +577,7 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     if (s->kind == 3 && env_int("RT_IOW_SPEC", 1) != 0 && !rtk::iow_narrow(f) && s->s_stop > 0 &&
         ensure_spec(s, rtk::units_of(f), uint32_t(s->s_stop)))
         return launch_scene_spec(s, f, st);
-    if (s->kind != 3 && env_int("RT_INW_ORDER", 1) != 0) return launch_scene_inw_ordered(s, f, st);
+    if (s->kind != 3 && env_int("RT_INW_ORDER", 0) >= 0) return launch_scene_inw_fold(s, f, st);
     if (s->kind != 3 && env_int("RT_INW_SPEC", 1) != 0) {
         const int ns = ensure_inw_spec(s, rtk::units_of(f), f.spp);
         if (ns > 0) return launch_scene_inw_spec(s, f, st, ns);
@@ -1006,12 +1008,19 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     return RT_OK;
 }
 
-// INW, wave-ordered (k_inw_o): one persistent launch per frame, the per-pixel End() sums folded
-// on chip in sample order (DESIGN.md "k_inw_o").  The launch is bracketed by HIP events on its
-// stream when kernel timing is on (rt_debug_kernel_time).
-int launch_scene_inw_ordered(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
+// INW with on-chip End() folds (DESIGN.md §5 "INW: on-chip End() folds"): the probe, then
+// k_inw_pm and k_inw_sm (one of them exits at once), persistent launches of one frame.  The
+// launches are bracketed by HIP events on their stream when kernel timing is on
+// (rt_debug_kernel_time).  RT_INW_ORDER = 1 / 2 forces pixel- / sample-major (tests, A/B);
+// RT_INW_RING_PM / RT_INW_RING_SM set the fold windows (samples per wave, powers of two).
+int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const int blocks = s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 16 : 15);
-    const size_t ring_bytes = size_t(blocks) * rtk::kInwRingBytesPerBlock;
+    auto ring_of = [](const char *name, uint32_t dflt) {
+        const int r = env_int(name, 0);
+        return (r >= 64 && (r & (r - 1)) == 0) ? uint32_t(r) : dflt;
+    };
+    const uint32_t ring_pm = ring_of("RT_INW_RING_PM", 1024), ring_sm = ring_of("RT_INW_RING_SM", 256);
+    const size_t ring_bytes = size_t(blocks) * (rtk::kBlock / 64) * std::max(ring_pm, ring_sm) * sizeof(float4);
     if (s->inw_ring.bytes < ring_bytes) {
         s->inw_ring.~DevBuf();
         new (&s->inw_ring) DevBuf();
@@ -1021,7 +1030,9 @@ int launch_scene_inw_ordered(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                      s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>(),
                      s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
     set_wide(s, sc);
-    s->last_kernel = s->layout == 4 ? "k_inw_o<true>" : "k_inw_o<false>";
+    const int ord = env_int("RT_INW_ORDER", 0);
+    const uint32_t force = (ord == 1 || ord == 2) ? uint32_t(ord) : 0u;
+    s->last_kernel = s->layout == 4 ? "k_inw_fold<true>" : "k_inw_fold<false>";
     s->last_launches = 1;
     s->last_chunks = 1;
     s->kt_used = 0;
@@ -1036,11 +1047,12 @@ int launch_scene_inw_ordered(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         ev = &s->kt_ev[0];
         s->kt_used = 1;
     }
-    // the ring reset and queue counter first, so the events bracket the kernel alone
+    // the rings are reset first, so the events bracket the probe and the two fold kernels
     e = hipMemsetAsync(s->inw_ring.p, 0xff, ring_bytes, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->first, st);
     if (e == hipSuccess)
-        e = rtk::launch_inw_ordered(f, sc, s->inw_ring.as<float4>(), s->counter.as<unsigned>(), blocks, st);
+        e = rtk::launch_inw_fold(f, sc, s->inw_ring.as<float4>(), ring_pm, ring_sm, s->counter.as<unsigned>(),
+                                 s->inw_mode.as<uint32_t>(), force, blocks, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->second, st);
     if (e != hipSuccess) {
         std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
@@ -1323,6 +1335,16 @@ int rt_debug_spec_times(rt_dev_scene *s, uint32_t *start_out, uint32_t *end_out,
 
 int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {
     if (!s) return RT_E_ARG;
+    if (s->last_kernel == std::string("k_inw_fold<true>") || s->last_kernel == std::string("k_inw_fold<false>")) {
+        // the probe picked the fold kernel on the device: read its verdict (synchronises)
+        uint32_t m[2] = {0, 0};
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipMemcpy(m, s->inw_mode.p, sizeof(m), hipMemcpyDeviceToHost));
+        const int ord = env_int("RT_INW_ORDER", 0);
+        const bool sm = ord == 2 || (ord != 1 && m[0] > 0 && 2 * m[1] >= m[0]);
+        static const char *names[2][2] = {{"k_inw_pm<false>", "k_inw_pm<true>"}, {"k_inw_sm<false>", "k_inw_sm<true>"}};
+        s->last_kernel = names[sm ? 1 : 0][s->layout == 4 ? 1 : 0];
+    }
     if (name_out && name_cap > 0) {
         std::strncpy(name_out, s->last_kernel, size_t(name_cap) - 1);
         name_out[name_cap - 1] = 0;

@@ -2334,32 +2334,83 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ?
     }
 }
 
-// ---------------------------------------------------------------- INW, wave-ordered (default)
-// End() (01_BVH...glsl:625-653, 664-675) adds each sample's sqrt(colour) in sample order.  Here a
-// wave owns whole pixels: it claims pixel units from the global queue and hands their samples to
-// its lanes in order -- the wave's stream g = 0, 1, 2, ... runs over (claimed pixel j, sample s) --
-// and a lane that finishes a sample takes the next stream entry at once (lane persistence).  A
-// finished sample stores {sqrt(colour), tag g} into the wave's private ring of kInwRing entries;
-// once per iteration the wave loads the next 64 entries from the fold pointer, and folds the
-// leading run of finished ones in stream order, with every lane computing the same serial sum
-// (End()'s float order).  A pixel's colour is written when its last sample is folded; the middle
-// sample's depth by the lane that finishes it.  The only per-sample traffic is that wave-private
-// ring (a few KB per wave, L2-resident); nothing else per sample leaves the chip.  Entries beyond
-// fold + kInwRing, and pixels beyond fold + 64, are not issued (a straggling sample holds the
-// window; the other lanes keep running until it fills).  Counters accumulate per lane.
-constexpr uint32_t kInwRing = 256;
+// ---------------------------------------------------------------- INW: on-chip End() folds
+// End() (01_BVH...glsl:625-653, 664-675) adds each sample's sqrt(colour) in sample order and
+// stores the mean.  The INW kernels below keep that sum on chip.  A wave claims work from the
+// global queue, hands its samples to its lanes as a stream g = 0, 1, 2, ... in a fixed order, and
+// a lane that finishes a sample takes the next stream entry at once (lane persistence).  A
+// finished sample stores {sqrt(colour), tag g} into the wave's private ring (a few KB per wave,
+// L2-resident); the wave folds the ring in each pixel's sample order, End()'s float order, and
+// writes a pixel when its last sample is folded.  The middle sample's depth is written by the
+// lane that finishes it.  Entries beyond the oldest unfolded one + ring size are not issued (a
+// straggling sample holds the window; the other lanes keep running until it fills).  Counters
+// accumulate per lane.  Two stream orders, one per kind of ray coherence:
+//  - k_inw_pm (pixel-major): the wave claims pixels and runs all samples of one pixel back to
+//    back, so its 64 lanes trace 64 consecutive samples of one pixel -- nearly the same ray where
+//    lens, motion and scatter offsets are small next to the scene's detail (C3: 10k small
+//    spheres, neighbouring pixels see different spheres).  The fold is wave-serial: once per
+//    iteration the wave loads the next 64 ring entries and every lane adds the leading finished
+//    run in order (each lane computes the same sum).
+//  - k_inw_sm (sample-major): the wave claims 8x8 pixel blocks and runs one sample index over the
+//    64 pixels of the block at a time (rows s = 0, 1, ...), so its lanes trace neighbouring
+//    pixels at one lens offset, time and scatter direction -- the same ray where the scene is
+//    coarse next to a pixel (C5: the Cornell walls).  The fold is lane-parallel: lane p holds
+//    pixel p's sum and adds its own samples as they finish.
+// k_inw_probe picks one per frame on the device (mode[]): over a sparse set of 8x8 blocks it
+// traces one primary ray per pixel; the frame is "coarse" when most blocks with a hit see one
+// object in all their pixels.  Both kernels are launched; the one not picked exits at once.
 __device__ __forceinline__ float rdl(float v, uint32_t l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
 }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-
+// the probe's verdict: mode[0] = blocks with a hit, mode[1] = those whose pixels all see one object
+__device__ __forceinline__ bool inw_sample_major(const uint32_t *mode, uint32_t force) {
+    if (force == 1u) return false;
+    if (force == 2u) return true;
+    const uint32_t hit = uni(mode[0]), same = uni(mode[1]);
+    return 2u * same >= hit && hit > 0u;
+}
 template <bool LIGHTS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES))) void k_inw_o(Frame f, InwScene S, float4 *ring, unsigned *counter) {
+__global__ __launch_bounds__(kBlock) void k_inw_probe(Frame f, InwScene S, uint32_t stride, uint32_t *mode) {
+    __shared__ float lds[kFStack * kBlock];
+    Ctr c;  // not flushed: the probe's rays are not the frame's
+    FStack K{lds + threadIdx.x, 0};
+    const uint32_t lane = threadIdx.x & 63u, nblk = units_total(f) / 64u;
+    const uint32_t blk = ((blockIdx.x * kBlock + threadIdx.x) >> 6) * stride;
+    if (blk >= nblk) return;  // whole waves (blk is per wave)
+    const UnitPix px = unit_pixel(f, blk * 64u + lane);
+    int id = -2;  // -2: outside the image, -1: no hit, else the object
+    if (px.in_image) {
+        const int s = f.spp / 2;
+        inw_start_sample(S, f, K, px.x, px.y, s, c);
+        K.size -= 8;
+        const uint32_t b = K.size;
+        const f3 o = mk(K.at(b), K.at(b + 1), K.at(b + 2)), d = mk(K.at(b + 3), K.at(b + 4), K.at(b + 5));
+        const f3 D = mk(f.dir[0], f.dir[1], f.dir[2]);
+        float tlim = kMaxT, extra = 0.0f;
+        f3 nrm;
+        const float g = inw_closest<false>(S, K, o, d, (float)s * f.inv_spp, dot(D, f3{1, 1, 1}) > 0.0f, tlim, nrm,
+                                           extra, -1.0f, c);
+        id = tlim < kMaxT ? (int)g : -1;
+    }
+    const int id0 = __shfl(id, __ffsll((long long)__ballot(id != -2)) - 1, 64);
+    const bool any_hit = __ballot(id >= 0) != 0ull, same = __ballot(id != -2 && id != id0) == 0ull;
+    if (lane == 0 && any_hit) {
+        atomicAdd(mode, 1u);
+        if (same) atomicAdd(mode + 1, 1u);
+    }
+}
+
+// pixel-major stream (see above): entry g = (claimed pixel ordinal j, sample s)
+template <bool LIGHTS>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES))) void k_inw_pm(Frame f, InwScene S, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force) {
+    if (inw_sample_major(mode, force)) return;  // the probe picked k_inw_sm for this frame
     __shared__ float lds[kFStack * kBlock];
     Ctr c;
     FStack K{lds + threadIdx.x, 0};
     const uint32_t lane = threadIdx.x & 63u;
-    float4 *wr = ring + (size_t)uni((blockIdx.x * kBlock + threadIdx.x) >> 6) * kInwRing;
+    const uint32_t rsize = rmask + 1u;
+    float4 *wr = ring + (size_t)uni((blockIdx.x * kBlock + threadIdx.x) >> 6) * rsize;
     const uint32_t spp = (uint32_t)f.spp, mid = spp / 2u, total = units_total(f);
     const float inv = rcp((float)f.spp);
     // wave-uniform: stream positions (entry gi / fold gf) as (pixel ordinal, sample), claims
@@ -2385,7 +2436,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ?
             bool fin = false;
             float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             if (k - gf < gi - gf) {
-                v = wr[k % kInwRing];
+                v = wr[k & rmask];
                 fin = __float_as_uint(v.w) == k;
             }
             const unsigned long long m = __ballot(fin);
@@ -2431,39 +2482,172 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ?
         // ---- issue: free lanes take stream entries in lane order, within the window
         {
             const uint32_t rank = (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
-            // entries available: up to fold + ring, and inside claimed pixels
-            uint32_t avail = kInwRing - (gi - gf);
+            uint32_t avail = rsize - (gi - gf);
             const uint64_t left = (uint64_t)(nclaimed - ji) * spp - si;  // entries of claimed pixels not issued
             if ((uint64_t)avail > left) avail = (uint32_t)left;
             const uint32_t take = nfree < avail ? nfree : avail;
-            const uint32_t adv = si + rank;  // this lane's entry: pixel ji + adv / spp, sample adv % spp
-            const uint32_t jl = ji + adv / spp;
-            const uint32_t unit = (uint32_t)__shfl((int)pix_slot, (int)(jl & 63u), 64);
-            if (!busy && rank < take) {
-                g = gi + rank;
-                s = (int)(adv % spp);
-                px = unit_pixel(f, unit);
-                col = f3{0, 0, 0};
-                dep = 0.0f;
-                if (px.in_image) {
-                    busy = true;
-                    inw_start_sample(S, f, K, px.x, px.y, s, c);
-                } else {  // a padding slot: an empty sample, folded as zero
-                    if ((uint32_t)s == mid && f.out_depth && px.out != (size_t)-1) f.out_depth[px.out] = 0.0f;
-                    wr[g % kInwRing] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
+            if (take) {
+                const uint32_t adv = si + rank;  // this lane's entry: pixel ji + adv / spp, sample adv % spp
+                const uint32_t jl = ji + adv / spp;
+                const uint32_t unit = (uint32_t)__shfl((int)pix_slot, (int)(jl & 63u), 64);
+                if (!busy && rank < take) {
+                    g = gi + rank;
+                    s = (int)(adv % spp);
+                    px = unit_pixel(f, unit);
+                    col = f3{0, 0, 0};
+                    dep = 0.0f;
+                    if (px.in_image) {
+                        busy = true;
+                        inw_start_sample(S, f, K, px.x, px.y, s, c);
+                    } else {  // a padding slot: an empty sample, folded as zero
+                        if ((uint32_t)s == mid && f.out_depth && px.out != (size_t)-1) f.out_depth[px.out] = 0.0f;
+                        wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
+                    }
                 }
+                gi += take;
+                const uint32_t a2 = si + take;
+                ji += a2 / spp;
+                si = a2 % spp;
             }
-            gi += take;
-            const uint32_t a2 = si + take;
-            ji += a2 / spp;
-            si = a2 % spp;
         }
         if (qdone && ji == nclaimed && gf == gi && __ballot(busy) == 0) break;
         // ---- one ray segment per busy lane (samples are independent invocations)
         if (busy) inw_segment<LIGHTS>(S, f, K, s, col, dep, c);
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
-            wr[g % kInwRing] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
-                                           __uint_as_float(g));
+            wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
+                                        __uint_as_float(g));
+            if ((uint32_t)s == mid && f.out_depth) f.out_depth[px.out] = dep;  // 01_BVH...glsl:667-668
+            busy = false;
+        }
+    }
+    flush(f, c);
+}
+
+// sample-major stream (see above): entry g = block ordinal b, sample s, pixel p (b * 64 * spp + s * 64 + p)
+template <bool LIGHTS>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES))) void k_inw_sm(Frame f, InwScene S, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force) {
+    if (!inw_sample_major(mode, force)) return;  // the probe picked k_inw_pm for this frame
+    __shared__ float lds[kFStack * kBlock];
+    Ctr c;
+    FStack K{lds + threadIdx.x, 0};
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t rsize = rmask + 1u;
+    float4 *wr = ring + (size_t)uni((blockIdx.x * kBlock + threadIdx.x) >> 6) * rsize;
+    const uint32_t spp = (uint32_t)f.spp, mid = spp / 2u, nblk = units_total(f) / 64u;
+    const uint32_t E = 64u * spp;  // entries per block
+    const float inv = rcp((float)f.spp);
+    // wave-uniform issue state: next entry = offset ei of block ordinal bi; gi = bi * E + ei
+    uint32_t gi = 0, bi = 0, ei = 0, nclaimed = 0;
+    bool qdone = false;
+    uint32_t blk_slot = 0xffffffffu;  // lane l: the block id of ordinal j with j % 64 == l
+    // per-lane fold state: pixel `lane` of block ordinal bf, next sample sf
+    uint32_t bf = 0, sf = 0;
+    f3 acc = f3{0, 0, 0};
+    // per-lane trace state
+    bool busy = false;
+    uint32_t g = 0;
+    int s = 0;
+    UnitPix px{};
+    f3 col = f3{0, 0, 0};
+    float dep = 0.0f;
+    K.size = 0;
+    for (;;) {
+        // ---- fold: lane p adds the finished samples of its pixel, in order (up to 2 per iteration)
+        {
+            __builtin_amdgcn_s_waitcnt(0);  // this wave's ring stores have landed (same CU: L1 write-through)
+            const uint32_t my_blk = (uint32_t)__shfl((int)blk_slot, (int)(bf & 63u), 64);
+            if (bf != nclaimed) {
+                uint32_t gg[2];
+                float4 v[2];
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    const uint32_t sk = sf + (uint32_t)k;
+                    gg[k] = bf * E + (sk < spp ? sk : spp - 1u) * 64u + lane;
+                    const bool ok = sk < spp && gg[k] - (gi - rsize) < rsize;  // issued (and inside the window)
+                    v[k] = ok ? wr[gg[k] & rmask] : make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(~gg[k]));
+                }
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    if (__float_as_uint(v[k].w) != gg[k] || sf == spp) break;
+                    const f3 gv = f3{v[k].x, v[k].y, v[k].z};
+                    acc = sf == 0 ? gv : acc + gv;
+                    if (++sf == spp) {  // pixel complete: End()'s imageStore (01_BVH...glsl:652)
+                        const UnitPix p = unit_pixel(f, my_blk * 64u + lane);
+                        if (p.out != (size_t)-1)
+                            reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
+                                make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
+                                            p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
+                    }
+                }
+                if (sf == spp) { sf = 0; bf++; }
+            }
+        }
+        // the ring window starts at the oldest unfolded entry of the wave (a lane whose next sample
+        // is not issued yet holds nothing back)
+        const uint32_t gnext = bf == nclaimed ? gi : bf * E + sf * 64u + lane;
+        const int dl = (int)(gi - gnext);
+        uint32_t dmax = dl > 0 ? (uint32_t)dl : 0u, bmin = bf;
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t t = (uint32_t)__shfl_xor((int)dmax, o, 64), tb = (uint32_t)__shfl_xor((int)bmin, o, 64);
+            dmax = t > dmax ? t : dmax;
+            bmin = tb < bmin ? tb : bmin;
+        }
+        dmax = uni(dmax);
+        bmin = uni(bmin);
+        // ---- claim blocks for the free lanes (at most 64 blocks between fold and issue)
+        const unsigned long long fm = __ballot(!busy);
+        const uint32_t nfree = (uint32_t)__popcll(fm);
+        if (!qdone && nfree) {
+            uint32_t need = bi + (ei + nfree - 1u) / E + 1u;
+            if (need > bmin + 64u) need = bmin + 64u;
+            if (need > nclaimed) {
+                const uint32_t want = need - nclaimed;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(counter, want);
+                base = uni((uint32_t)__shfl((int)base, 0, 64));
+                uint32_t got = want;
+                if (base >= nblk) { got = 0; qdone = true; }
+                else if (base + want >= nblk) { got = nblk - base; qdone = true; }
+                const uint32_t rel = (lane - nclaimed) & 63u;
+                if (rel < got) blk_slot = base + rel;
+                nclaimed += got;
+            }
+        }
+        // ---- issue: free lanes take the next stream entries in lane order, inside the window
+        {
+            const uint32_t rank = (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+            uint32_t avail = rsize - dmax;
+            const uint64_t left = (uint64_t)(nclaimed - bi) * E - ei;
+            if ((uint64_t)avail > left) avail = (uint32_t)left;
+            const uint32_t take = nfree < avail ? nfree : avail;
+            if (take) {
+                uint32_t b = bi, e = ei + rank;
+                if (e >= E) { e -= E; b++; }
+                const uint32_t blk = (uint32_t)__shfl((int)blk_slot, (int)(b & 63u), 64);
+                if (!busy && rank < take) {
+                    g = gi + rank;
+                    s = (int)(e >> 6);
+                    px = unit_pixel(f, blk * 64u + (e & 63u));
+                    col = f3{0, 0, 0};
+                    dep = 0.0f;
+                    if (px.in_image) {
+                        busy = true;
+                        inw_start_sample(S, f, K, px.x, px.y, s, c);
+                    } else {  // a padding slot: an empty sample, folded as zero
+                        if ((uint32_t)s == mid && f.out_depth && px.out != (size_t)-1) f.out_depth[px.out] = 0.0f;
+                        wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
+                    }
+                }
+                gi += take;
+                ei += take;
+                if (ei >= E) { ei -= E; bi++; }
+            }
+        }
+        if (qdone && bi == nclaimed && bmin == nclaimed && __ballot(busy) == 0) break;
+        if (busy) inw_segment<LIGHTS>(S, f, K, s, col, dep, c);
+        if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
+            wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
+                                        __uint_as_float(g));
             if ((uint32_t)s == mid && f.out_depth) f.out_depth[px.out] = dep;  // 01_BVH...glsl:667-668
             busy = false;
         }
@@ -2549,8 +2733,8 @@ int resident_blocks_per_cu(int kind) {
     else if (kind == 6) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_s<false>, kBlock, 0);
     else if (kind == 7) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_s<true>, kBlock, 0);
     else if (kind == 14) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<true>, kBlock, 0);
-    else if (kind == 15) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_o<false>, kBlock, 0);
-    else if (kind == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_o<true>, kBlock, 0);
+    else if (kind == 15) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<false>, kBlock, 0);
+    else if (kind == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<true>, kBlock, 0);
     else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<false>, kBlock, 0);
     return (e == hipSuccess && nb > 0) ? nb : 2;
 }
@@ -2786,14 +2970,36 @@ hipError_t launch_inw_spec(const Frame &f, const InwScene &sc, const SpecRecs &R
     else hipLaunchKernelGGL(k_inw_s<false>, g, dim3(kBlock), 0, s, f, sc, R, s0, ns, ct, counter);
     return hipGetLastError();
 }
-hipError_t launch_inw_ordered(const Frame &f, const InwScene &sc, float4 *ring, unsigned *counter, int blocks,
-                              hipStream_t s) {
-    static_assert(kInwRingBytesPerBlock == (kBlock / 64) * kInwRing * sizeof(float4), "ring size");
-    hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
+// One frame of the on-chip-fold INW kernels: the probe (unless forced), then k_inw_pm and
+// k_inw_sm, of which the one the probe did not pick exits at once.  ring: blocks * 4 waves *
+// max(ring_pm, ring_sm) float4; mode: 2 uints (zeroed here).  force: 0 = probe, 1 = pm, 2 = sm.
+hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uint32_t ring_pm, uint32_t ring_sm,
+                           unsigned *counter, uint32_t *mode, uint32_t force, int blocks, hipStream_t s) {
+    for (uint32_t r : {ring_pm, ring_sm})
+        if (r < 64 || (r & (r - 1))) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(mode, 0, 2 * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
-    if (sc.layout == 4) hipLaunchKernelGGL(k_inw_o<true>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, counter);
-    else hipLaunchKernelGGL(k_inw_o<false>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, counter);
-    return hipGetLastError();
+    if (force == 0) {
+        const uint32_t nblk = units_of(f) / 64u, waves = 1024u;  // ~1024 probe blocks of 8x8 pixels
+        const uint32_t stride = nblk > waves ? nblk / waves : 1u, nw = (nblk + stride - 1u) / stride;
+        const dim3 g((nw + 3u) / 4u);
+        if (sc.layout == 4) hipLaunchKernelGGL(k_inw_probe<true>, g, dim3(kBlock), 0, s, f, sc, stride, mode);
+        else hipLaunchKernelGGL(k_inw_probe<false>, g, dim3(kBlock), 0, s, f, sc, stride, mode);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    for (int k = 0; k < 2; k++) {  // (pm, then sm) each with its own queue counter
+        if ((e = hipMemsetAsync(counter + 16 * k, 0, sizeof(unsigned), s)) != hipSuccess) return e;
+        const uint32_t rm = (k == 0 ? ring_pm : ring_sm) - 1u;
+        if (sc.layout == 4) {
+            if (k == 0) hipLaunchKernelGGL(k_inw_pm<true>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter, mode, force);
+            else hipLaunchKernelGGL(k_inw_sm<true>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter + 16, mode, force);
+        } else {
+            if (k == 0) hipLaunchKernelGGL(k_inw_pm<false>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter, mode, force);
+            else hipLaunchKernelGGL(k_inw_sm<false>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter + 16, mode, force);
+        }
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 hipError_t launch_inw_fin(const Frame &f, const SpecRecs &R, int s0, int ns, bool final_chunk, float4 *state,
                           hipStream_t s) {

@@ -38,13 +38,16 @@ def test_iow01_c1_matches_oracle(gpu):
     assert gst["segments"] == ost["segments"] == 400 * 225
 
 
-@pytest.mark.parametrize("wide", ["1", "0"])
+@pytest.mark.parametrize("wide,order", [("1", "0"), ("0", "0"), ("1", "1"), ("1", "2")])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_render_matches_oracle(gpu, name, wide, monkeypatch):
+def test_render_matches_oracle(gpu, name, wide, order, monkeypatch):
+    """wide: RT_INW_FAST (the INW wide walk, 1, or the reference's LBVH walk, 0); order:
+    RT_INW_ORDER (0: the probe picks the INW fold kernel, 1: pixel-major, 2: sample-major)."""
     monkeypatch.setenv("RT_INW_FAST", wide)  # read by the library when it builds the device scene
+    monkeypatch.setenv("RT_INW_ORDER", order)  # read at every render
     sc = CASES[name]()
-    if sc.stage == R.RT_STAGE_IOW03 and wide == "0":
-        pytest.skip("RT_INW_FAST only switches the INW walk")
+    if sc.stage == R.RT_STAGE_IOW03 and (wide == "0" or order != "0"):
+        pytest.skip("RT_INW_FAST / RT_INW_ORDER only switch the INW kernels")
     g, gd, gst = R.render(sc)
     o, od, ost = O.render(sc)
     c = _check(name, g, o)

@@ -98,13 +98,29 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--full", action="store_true", help="C3, C5 and IOW-03 at 1920x1080 at BASELINE's full spp")
     ap.add_argument("--reps", type=int, default=1, help="timed renders per row (after the warm-up)")
+    ap.add_argument("--inw-only", action="store_true", help="with --full: C3 and C5 only")
+    ap.add_argument("--row", choices=("c3", "c5", "ns", "c2"), help="one row only, at --spp (and --reps)")
+    ap.add_argument("--spp", type=int, default=0)
     a = ap.parse_args()
+    if a.row:
+        preset = {"c3": (R.PRESET_INW01_RANDOM, 1234, 10_000), "c5": (R.PRESET_INW04_CORNELL, 7, 0),
+                  "ns": (R.PRESET_IOW03_FINAL, 20250131, 0), "c2": (R.PRESET_IOW03_FINAL, 20250131, 0)}[a.row]
+        kw = dict(width=1920, height=1080) if a.row == "ns" else {}
+        if a.spp:
+            kw["spp"] = a.spp
+        elif a.row == "ns":
+            kw["spp"] = 500
+        row = run(a.row, *preset, reps=a.reps, **kw)
+        row["env"] = {k: v for k, v in os.environ.items() if k.startswith("RT_")}
+        print(json.dumps(row), flush=True)
+        return
     if a.full:
-        for args, kw in ((("C3 INW-01 LBVH 10k moving spheres (full)", R.PRESET_INW01_RANDOM, 1234, 10_000),
-                          dict(spp=500)),
-                         (("C5 INW-04 Cornell (full)", R.PRESET_INW04_CORNELL, 7, 0), dict(spp=2000)),
-                         (("IOW-03 final scene, 1920x1080, 500 spp (north-star target)", R.PRESET_IOW03_FINAL,
-                           20250131, 0), dict(spp=500, width=1920, height=1080))):
+        rows = [(("C3 INW-01 LBVH 10k moving spheres (full)", R.PRESET_INW01_RANDOM, 1234, 10_000), dict(spp=500)),
+                (("C5 INW-04 Cornell (full)", R.PRESET_INW04_CORNELL, 7, 0), dict(spp=2000))]
+        if not a.inw_only:
+            rows.append((("IOW-03 final scene, 1920x1080, 500 spp (north-star target)", R.PRESET_IOW03_FINAL,
+                          20250131, 0), dict(spp=500, width=1920, height=1080)))
+        for args, kw in rows:
             print(json.dumps(run(*args, reps=a.reps, **kw)), flush=True)
         return
     q = a.quick
