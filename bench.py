@@ -153,16 +153,16 @@ def host_cores() -> int:
         return os.cpu_count() or 1
 
 
-def cpu_baseline(sc, threads: int, spp: int) -> dict:
+def cpu_baseline(sc, threads: int, spp: int, bw: int = 64, rows_per_core: int = 1) -> dict:
     """The CPU oracle (the C restatement of the reference shader, OpenMP schedule(dynamic, 1) over
     pixel rows) on all `threads` host cores, on a bounded sample of the same frame: the central
-    64 x `threads` pixel block (one row per core, so every core has rows to take), at `spp`
-    samples (Mrays/s is a rate) and the full bounce count."""
+    bw x (rows_per_core * threads) pixel block (every core has rows to take), at `spp` samples
+    (Mrays/s is a rate) and the full bounce count."""
     from oracle import oracle as O
     O.set_threads(threads)
     p = R.RtParams()
     C.memmove(C.addressof(p), C.addressof(sc.params), C.sizeof(p))
-    bw, bh = 64, max(threads, 8)
+    bh = max(threads, 8) * rows_per_core
     p.spp = min(spp, sc.params.spp)
     p.tile_x0, p.tile_y0 = sc.params.width // 2 - bw // 2, sc.params.height // 2 - bh // 2
     p.tile_w, p.tile_h = bw, bh
@@ -184,7 +184,7 @@ def main():
     ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--height", type=int, default=0)
     ap.add_argument("--cpu-spp", type=int, default=0,
-                    help="CPU baseline samples per pixel (default: 128 for c3, the config's spp for c2/ns)")
+                    help="CPU baseline samples per pixel (default: the config's spp)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="host cores for the CPU baseline (default: nproc)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--balance", action="store_true",
@@ -416,7 +416,11 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cores = args.cpu_threads or host_cores()
-            cpu = cpu_baseline(sc, cores, args.cpu_spp or (128 if cfg == "c3" else sc.params.spp))
+            # ~10-20 s of host work on the GPU box (C3: 3.2 Mrays/s on 16 cores for the central block)
+            if cfg == "c3":
+                cpu = cpu_baseline(sc, cores, args.cpu_spp or sc.params.spp, bw=256, rows_per_core=4)
+            else:  # IOW-03: ~280 rays per sample; ns has 5x the samples per pixel of c2
+                cpu = cpu_baseline(sc, cores, args.cpu_spp or sc.params.spp, bw=16 if cfg == "ns" else 64)
         out = {
             "metric": METRIC,
             "value": round(value, 3),
