@@ -130,6 +130,7 @@ struct rt_dev_scene {
     DevBuf obox;  // IOW-03: per-object culling boxes (2 float4 each) for wave-cooperative queries
     DevBuf tex, tex_info;  // INW-04 material textures (float4 texels, (first, w, h, 0) per texture)
     DevBuf wnodes, wrank, wleaf;  // INW wide walk: culling BVH, depth-first ranks, LBVH leaf boxes
+    int wdepth = 0;               // levels of the 4-wide culling BVH
     uint32_t dfs_high = 0;
     uint32_t n_tex = 0;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
@@ -321,6 +322,7 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     sc.rank = s->wrank.as<uint32_t>();
     sc.leafbox = s->wleaf.as<float4>();
     sc.dfs_high = s->dfs_high;
+    sc.n_wnodes = uint32_t(s->wnodes.bytes / (8 * sizeof(float4)));
 }
 
 int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
@@ -388,6 +390,7 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
     for (uint32_t g = 0; g < n; g++) std::memcpy(&lbox[size_t(g) * 8], nodes + size_t(leaf[g]) * 8, 8 * sizeof(float));
     HIP_OK(s->wleaf.upload(lbox.data(), lbox.size() * sizeof(float)));
     s->dfs_high = high;
+    s->wdepth = depth4;
     return RT_OK;
 }
 
@@ -1020,7 +1023,12 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         return (r >= 64 && (r & (r - 1)) == 0) ? uint32_t(r) : dflt;
     };
     const uint32_t ring_pm = ring_of("RT_INW_RING_PM", 1024), ring_sm = ring_of("RT_INW_RING_SM", 256);
-    const size_t ring_bytes = size_t(blocks) * (rtk::kBlock / 64) * std::max(ring_pm, ring_sm) * sizeof(float4);
+    // the top of the wide BVH staged in LDS (768-lane blocks, 3 waves per SIMD);
+    // RT_INW_LDS=0: 256-lane blocks reading every node from L1 / L2 (A/B)
+    const int blocks_ln = env_int("RT_INW_LDS", 1) == 1 && s->dfs_high
+                              ? s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 18 : 17) : 0;
+    const size_t waves = std::max(size_t(blocks) * (rtk::kBlock / 64), size_t(blocks_ln) * (3 * rtk::kBlock / 64));
+    const size_t ring_bytes = waves * std::max(ring_pm, ring_sm) * sizeof(float4);
     if (s->inw_ring.bytes < ring_bytes) {
         s->inw_ring.~DevBuf();
         new (&s->inw_ring) DevBuf();
@@ -1052,7 +1060,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     if (e == hipSuccess && ev) e = hipEventRecord(ev->first, st);
     if (e == hipSuccess)
         e = rtk::launch_inw_fold(f, sc, s->inw_ring.as<float4>(), ring_pm, ring_sm, s->counter.as<unsigned>(),
-                                 s->inw_mode.as<uint32_t>(), force, blocks, st);
+                                 s->inw_mode.as<uint32_t>(), force, blocks, blocks_ln, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->second, st);
     if (e != hipSuccess) {
         std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));

@@ -1757,6 +1757,24 @@ __device__ float inw_surrounding_ri(const InwScene &S, FStack &K, f3 hp, float r
     return acc;
 }
 
+// ---------------------------------------------------------------- LDS-staged top of the wide BVH
+// (measured in DESIGN.md §5): kernels instantiated with LN copy the first n_lnodes wide
+// nodes -- the top levels, as bvh4_collapse numbers them breadth first -- into LDS and read them
+// there; deeper nodes come from global memory.
+constexpr int kInwLdsNodes = 320;  // 40 KB: what 3 x 256-lane stacks (120 KB) leave of 160 KB
+__shared__ float4 g_inw_lnodes[kInwLdsNodes * 8];
+template <bool LN>
+__device__ __forceinline__ void inw_wnode(const InwScene &S, int cur, float4 &lx, float4 &ly, float4 &lz, float4 &hx,
+                                          float4 &hy, float4 &hz, float4 &lk) {
+    if (LN && (uint32_t)(cur - 1) < S.n_lnodes) {
+        const float4 *nd = g_inw_lnodes + 8 * (cur - 1);
+        lx = nd[0]; ly = nd[1]; lz = nd[2]; hx = nd[3]; hy = nd[4]; hz = nd[5]; lk = nd[6];
+    } else {
+        const float4 *nd = S.wnodes + 8 * (cur - 1);
+        lx = nd[0]; ly = nd[1]; lz = nd[2]; hx = nd[3]; hy = nd[4]; hz = nd[5]; lk = nd[6];
+    }
+}
+
 // ---------------------------------------------------------------- INW wide walk
 // The reference's closest hit (01_BVH...glsl:431-473) is the nearest hit among the objects whose
 // LBVH leaf box its depth-first walk reaches, ties to the one it reaches first.  With finite ray
@@ -1774,7 +1792,7 @@ __device__ float inw_surrounding_ri(const InwScene &S, FStack &K, f3 hp, float r
 // inside its own box, and then skipping it changes nothing; but where an object's face coincides
 // with its box face, rounding can put t an ulp below te.  Any accepted candidate with t < te
 // therefore hands the ray to the reference walk (ok = false).
-template <bool WANT_NORMAL>
+template <bool WANT_NORMAL, bool LN = false>
 __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
                                    f3 &normal, float &extra, float init_geom, Ctr &c, bool &ok) {
     const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};  // the reference's reciprocals (test_aabb)
@@ -1812,8 +1830,8 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
         if (walking) {
             bool pop;
             if (cur > 0) {
-                const float4 *nd = S.wnodes + 8 * (cur - 1);
-                const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], lk = nd[6];
+                float4 lx, ly, lz, hx, hy, hz, lk;
+                inw_wnode<LN>(S, cur, lx, ly, lz, hx, hy, hz, lk);
                 c.nodes += 4;
                 float t0, t1, t2, t3;
                 cull4(lx, ly, lz, hx, hy, hz, o, fid, lim, t0, t1, t2, t3);
@@ -1868,6 +1886,7 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
 // whose leaf box holds the point (inclusive, as the reference compares) and whose inside test
 // passes, found by a walk of the culling BVH and summed in rank order.  ok = false: fall back.
 constexpr int kRiMax = 8;
+template <bool LN = false>
 __device__ float inw_surrounding_ri_wide(const InwScene &S, FStack &K, f3 hp, float ratio, Ctr &c, bool &ok) {
     ok = S.wnodes != nullptr && K.size + S.dfs_high <= (uint32_t)kFStack;
     if (!__any(ok)) return 1.0f;
@@ -1879,8 +1898,8 @@ __device__ float inw_surrounding_ri_wide(const InwScene &S, FStack &K, f3 hp, fl
     bool walking = ok;
     while (walking) {
         if (cur > 0) {
-            const float4 *nd = S.wnodes + 8 * (cur - 1);
-            const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], lk = nd[6];
+            float4 lx, ly, lz, hx, hy, hz, lk;
+            inw_wnode<LN>(S, cur, lx, ly, lz, hx, hy, hz, lk);
             c.nodes += 4;
             const bool i0 = hp.x >= lx.x && hp.x <= hx.x && hp.y >= ly.x && hp.y <= hy.x && hp.z >= lz.x && hp.z <= hz.x;
             const bool i1 = hp.x >= lx.y && hp.x <= hx.y && hp.y >= ly.y && hp.y <= hy.y && hp.z >= lz.y && hp.z <= hz.y;
@@ -1931,17 +1950,18 @@ __device__ float inw_surrounding_ri_wide(const InwScene &S, FStack &K, f3 hp, fl
     return acc;
 }
 
-template <bool WANT_NORMAL>
+template <bool WANT_NORMAL, bool LN = false>
 __device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
                                              float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c) {
     bool ok = false;
-    const float g = inw_traverse_wide<WANT_NORMAL>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c, ok);
+    const float g = inw_traverse_wide<WANT_NORMAL, LN>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c, ok);
     if (ok) return g;
     return inw_traverse<WANT_NORMAL>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
 }
+template <bool LN = false>
 __device__ __forceinline__ float inw_ri(const InwScene &S, FStack &K, f3 hp, float ratio, Ctr &c) {
     bool ok = false;
-    const float r = inw_surrounding_ri_wide(S, K, hp, ratio, c, ok);
+    const float r = inw_surrounding_ri_wide<LN>(S, K, hp, ratio, c, ok);
     if (ok) return r;
     return inw_surrounding_ri(S, K, hp, ratio, c);
 }
@@ -2038,7 +2058,7 @@ __device__ f3 inw_tex_color(const InwScene &S, uint32_t k, f3 lp) {
 
 // One iteration of out_Pixel's ray loop (01_BVH...glsl:414-597 / 04...glsl:510-713):
 // pop a ray, closest hit, surrounding RI, shadow rays, push reflect/refract, accumulate.
-template <bool LIGHTS>
+template <bool LIGHTS, bool LN = false>
 __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s, f3 &color, float &depth, Ctr &c) {
     const f3 D = mk(F.dir[0], F.dir[1], F.dir[2]);
     const float ratio = (float)s * F.inv_spp;
@@ -2054,7 +2074,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         const float tlim0 = mf0 ? K.at(4) : kMaxT;
         float tlim = tlim0, extra = 0.0f;
         f3 normal = f3{0, 0, 0};
-        float fg = inw_closest<true>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
+        float fg = inw_closest<true, LN>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
         const f3 hitpoint = co + cd * tlim;
         if (!(tlim < tlim0)) {
             if (mf0 && (int)(K.at(5) + 0.1f) < F.n_focus) {  // next focal lens, 01_BVH...glsl:506-528
@@ -2099,7 +2119,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         const bool ri_read = (m_refl > 0.002f || m_refr > 0.002f) && (m_refr > 0.002f || dot(normal, cd) > 0.0f);
         float surr = 1.0f;
         if (!LIGHTS && (ri_forced || (ri_read && contribution > 0.01f && bounced + 1.0f < (float)F.max_bounces)))
-            surr = inw_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
+            surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
         if (mf0) K.size = 0;  // 01_BVH...glsl:544-549: the lens record goes after a primary hit
         if (LIGHTS) {  // 04...glsl:604-665
             uint32_t is_lit = S.n_lights > 0 ? 0u : (uint32_t)is_lit_geom(S, f2u(fg + 0.1f));
@@ -2112,15 +2132,15 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
                     f3 sd = normalize((bmin + (bmax - bmin) * ratio) - so);
                     c.shadow++;
                     f3 dummy_n; float dummy_e;
-                    float sg = inw_closest<false>(S, K, so, sd, ratio, invert, sl, dummy_n, dummy_e, -1.0f, c);
+                    float sg = inw_closest<false, LN>(S, K, so, sd, ratio, invert, sl, dummy_n, dummy_e, -1.0f, c);
                     is_lit += (uint32_t)is_lit_geom(S, f2u(sg + 0.1f));
                 }
                 const uint32_t nl = S.n_lights > 1 ? S.n_lights : 1u;
                 contribution *= (float)is_lit * rcp((float)nl);
                 if (ri_forced || (ri_read && contribution > 0.01f && bounced < (float)F.max_bounces))
-                    surr = inw_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
+                    surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
             } else {
-                if (ri_forced) (void)inw_ri(S, K, hitpoint + normal * 0.001f, ratio, c);
+                if (ri_forced) (void)inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
                 color = f3{1, 1, 1};
                 K.size = 0;
                 break;
@@ -2401,16 +2421,26 @@ __global__ __launch_bounds__(kBlock) void k_inw_probe(Frame f, InwScene S, uint3
     }
 }
 
-// pixel-major stream (see above): entry g = (claimed pixel ordinal j, sample s)
-template <bool LIGHTS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES))) void k_inw_pm(Frame f, InwScene S, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force) {
+// pixel-major stream (see above): entry g = (claimed pixel ordinal j, sample s).  LN: 768-lane
+// blocks (3 waves per SIMD) that stage the top of the wide BVH in the LDS their three 256-lane
+// stacks leave free (kInwLdsNodes nodes)
+template <bool LIGHTS, bool LN = false>
+__global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_waves_per_eu(LN ? 3 : (LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES)))) void k_inw_pm(Frame f, InwScene S0, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force) {
     if (inw_sample_major(mode, force)) return;  // the probe picked k_inw_sm for this frame
-    __shared__ float lds[kFStack * kBlock];
+    constexpr int SUB = LN ? 3 : 1;
+    __shared__ float lds[SUB * kFStack * kBlock];
+    InwScene S = S0;
+    if constexpr (LN) {
+        const uint32_t n = S.wnodes ? (S.n_wnodes < (uint32_t)kInwLdsNodes ? S.n_wnodes : (uint32_t)kInwLdsNodes) : 0u;
+        for (uint32_t i = threadIdx.x; i < n * 8u; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
+        __syncthreads();
+        S.n_lnodes = n;
+    }
     Ctr c;
-    FStack K{lds + threadIdx.x, 0};
+    FStack K{lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock), 0};
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t rsize = rmask + 1u;
-    float4 *wr = ring + (size_t)uni((blockIdx.x * kBlock + threadIdx.x) >> 6) * rsize;
+    float4 *wr = ring + (size_t)uni((blockIdx.x * (SUB * kBlock) + threadIdx.x) >> 6) * rsize;
     const uint32_t spp = (uint32_t)f.spp, mid = spp / 2u, total = units_total(f);
     const float inv = rcp((float)f.spp);
     // wave-uniform: stream positions (entry gi / fold gf) as (pixel ordinal, sample), claims
@@ -2431,7 +2461,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ?
     for (;;) {
         // ---- fold the finished entries gf, gf+1, ... (stored in earlier iterations)
         if (gf != gi) {
-            __builtin_amdgcn_s_waitcnt(0);  // this wave's ring stores have landed (same CU: L1 write-through)
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's ring stores have landed (same CU: L1 write-through)
             const uint32_t k = gf + lane;
             bool fin = false;
             float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -2487,12 +2517,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ?
             if ((uint64_t)avail > left) avail = (uint32_t)left;
             const uint32_t take = nfree < avail ? nfree : avail;
             if (take) {
-                const uint32_t adv = si + rank;  // this lane's entry: pixel ji + adv / spp, sample adv % spp
-                const uint32_t jl = ji + adv / spp;
+                // this lane's entry: pixel ji + adv / spp, sample adv % spp (adv < spp + 64: one
+                // subtraction when spp >= 64)
+                const uint32_t adv = si + rank;
+                const uint32_t q = spp >= 64u ? (adv >= spp ? 1u : 0u) : adv / spp;
+                const uint32_t jl = ji + q;
                 const uint32_t unit = (uint32_t)__shfl((int)pix_slot, (int)(jl & 63u), 64);
                 if (!busy && rank < take) {
                     g = gi + rank;
-                    s = (int)(adv % spp);
+                    s = (int)(adv - q * spp);
                     px = unit_pixel(f, unit);
                     col = f3{0, 0, 0};
                     dep = 0.0f;
@@ -2512,7 +2545,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ?
         }
         if (qdone && ji == nclaimed && gf == gi && __ballot(busy) == 0) break;
         // ---- one ray segment per busy lane (samples are independent invocations)
-        if (busy) inw_segment<LIGHTS>(S, f, K, s, col, dep, c);
+        if (busy) inw_segment<LIGHTS, LN>(S, f, K, s, col, dep, c);
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
                                         __uint_as_float(g));
@@ -2524,15 +2557,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ?
 }
 
 // sample-major stream (see above): entry g = block ordinal b, sample s, pixel p (b * 64 * spp + s * 64 + p)
-template <bool LIGHTS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES))) void k_inw_sm(Frame f, InwScene S, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force) {
+template <bool LIGHTS, bool LN = false>
+__global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_waves_per_eu(LN ? 3 : (LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES)))) void k_inw_sm(Frame f, InwScene S0, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force) {
     if (!inw_sample_major(mode, force)) return;  // the probe picked k_inw_pm for this frame
-    __shared__ float lds[kFStack * kBlock];
+    constexpr int SUB = LN ? 3 : 1;
+    __shared__ float lds[SUB * kFStack * kBlock];
+    InwScene S = S0;
+    if constexpr (LN) {
+        const uint32_t n = S.wnodes ? (S.n_wnodes < (uint32_t)kInwLdsNodes ? S.n_wnodes : (uint32_t)kInwLdsNodes) : 0u;
+        for (uint32_t i = threadIdx.x; i < n * 8u; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
+        __syncthreads();
+        S.n_lnodes = n;
+    }
     Ctr c;
-    FStack K{lds + threadIdx.x, 0};
+    FStack K{lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock), 0};
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t rsize = rmask + 1u;
-    float4 *wr = ring + (size_t)uni((blockIdx.x * kBlock + threadIdx.x) >> 6) * rsize;
+    float4 *wr = ring + (size_t)uni((blockIdx.x * (SUB * kBlock) + threadIdx.x) >> 6) * rsize;
     const uint32_t spp = (uint32_t)f.spp, mid = spp / 2u, nblk = units_total(f) / 64u;
     const uint32_t E = 64u * spp;  // entries per block
     const float inv = rcp((float)f.spp);
@@ -2554,7 +2595,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ?
     for (;;) {
         // ---- fold: lane p adds the finished samples of its pixel, in order (up to 2 per iteration)
         {
-            __builtin_amdgcn_s_waitcnt(0);  // this wave's ring stores have landed (same CU: L1 write-through)
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's ring stores have landed (same CU: L1 write-through)
             const uint32_t my_blk = (uint32_t)__shfl((int)blk_slot, (int)(bf & 63u), 64);
             if (bf != nclaimed) {
                 uint32_t gg[2];
@@ -2644,7 +2685,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ?
             }
         }
         if (qdone && bi == nclaimed && bmin == nclaimed && __ballot(busy) == 0) break;
-        if (busy) inw_segment<LIGHTS>(S, f, K, s, col, dep, c);
+        if (busy) inw_segment<LIGHTS, LN>(S, f, K, s, col, dep, c);
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
                                         __uint_as_float(g));
@@ -2735,6 +2776,8 @@ int resident_blocks_per_cu(int kind) {
     else if (kind == 14) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<true>, kBlock, 0);
     else if (kind == 15) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<false>, kBlock, 0);
     else if (kind == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<true>, kBlock, 0);
+    else if (kind == 17) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<false, true>, 3 * kBlock, 0);
+    else if (kind == 18) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<true, true>, 3 * kBlock, 0);
     else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<false>, kBlock, 0);
     return (e == hipSuccess && nb > 0) ? nb : 2;
 }
@@ -2974,7 +3017,8 @@ hipError_t launch_inw_spec(const Frame &f, const InwScene &sc, const SpecRecs &R
 // k_inw_sm, of which the one the probe did not pick exits at once.  ring: blocks * 4 waves *
 // max(ring_pm, ring_sm) float4; mode: 2 uints (zeroed here).  force: 0 = probe, 1 = pm, 2 = sm.
 hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uint32_t ring_pm, uint32_t ring_sm,
-                           unsigned *counter, uint32_t *mode, uint32_t force, int blocks, hipStream_t s) {
+                           unsigned *counter, uint32_t *mode, uint32_t force, int blocks, int blocks_ln,
+                           hipStream_t s) {
     for (uint32_t r : {ring_pm, ring_sm})
         if (r < 64 || (r & (r - 1))) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(mode, 0, 2 * sizeof(uint32_t), s);
@@ -2990,7 +3034,17 @@ hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uin
     for (int k = 0; k < 2; k++) {  // (pm, then sm) each with its own queue counter
         if ((e = hipMemsetAsync(counter + 16 * k, 0, sizeof(unsigned), s)) != hipSuccess) return e;
         const uint32_t rm = (k == 0 ? ring_pm : ring_sm) - 1u;
-        if (sc.layout == 4) {
+        unsigned *ctr = counter + 16 * k;
+        if (blocks_ln > 0) {  // the LDS-staged BVH top (768-lane blocks)
+            const dim3 g(blocks_ln), b(3 * kBlock);
+            if (sc.layout == 4) {
+                if (k == 0) hipLaunchKernelGGL((k_inw_pm<true, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force);
+                else hipLaunchKernelGGL((k_inw_sm<true, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force);
+            } else {
+                if (k == 0) hipLaunchKernelGGL((k_inw_pm<false, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force);
+                else hipLaunchKernelGGL((k_inw_sm<false, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force);
+            }
+        } else if (sc.layout == 4) {
             if (k == 0) hipLaunchKernelGGL(k_inw_pm<true>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter, mode, force);
             else hipLaunchKernelGGL(k_inw_sm<true>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter + 16, mode, force);
         } else {

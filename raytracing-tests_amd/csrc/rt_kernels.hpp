@@ -77,6 +77,8 @@ struct InwScene {
     const uint32_t *rank = nullptr;
     const float4 *leafbox = nullptr;  // per object: its LBVH leaf node (2 float4: the reference's leaf box)
     uint32_t dfs_high = 0;
+    uint32_t n_wnodes = 0;  // wide nodes
+    uint32_t n_lnodes = 0;  // the first n_lnodes wide nodes are staged in LDS (LN kernels only)
 };
 
 // One launch of a chunked render: samples [s_begin, s_end) of every pixel unit.  A pixel's
@@ -262,8 +264,11 @@ hipError_t launch_inw_spec(const Frame &f, const InwScene &sc, const SpecRecs &R
 // INW with the on-chip End() folds (k_inw_probe + k_inw_pm / k_inw_sm); ring:
 // blocks * (kBlock / 64) * max(ring_pm, ring_sm) float4 (powers of two >= 64); counter: 2 queue
 // counters 64 B apart; mode: 2 uints; force: 0 = probe decides, 1 = pixel-major, 2 = sample-major
+// blocks_ln > 0: the fold kernels run as blocks_ln 768-lane blocks with the top of the wide BVH
+// staged in LDS (ring: max(blocks * 4, blocks_ln * 12) waves)
 hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uint32_t ring_pm, uint32_t ring_sm,
-                           unsigned *counter, uint32_t *mode, uint32_t force, int blocks, hipStream_t s);
+                           unsigned *counter, uint32_t *mode, uint32_t force, int blocks, int blocks_ln,
+                           hipStream_t s);
 hipError_t launch_inw_fin(const Frame &f, const SpecRecs &R, int s0, int ns, bool final_chunk, float4 *state,
                           hipStream_t s);
 
