@@ -542,32 +542,7 @@ bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
     return true;
 }
 
-// INW sample-parallel records for P pixel units x ns samples (ns chosen to fit); 0 = no room.
-int ensure_inw_spec(rt_dev_scene *s, uint32_t P, int spp) {
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 0;
-    const char *mx = std::getenv("RT_SPEC_MAX_GB");
-    const double budget = std::min(double(free_b + 3 * 16 * double(s->spec_cap)) / 2.0, (mx ? std::atof(mx) : 96.0) * 1e9);
-    const size_t per = size_t(P) * 3 * sizeof(float4);
-    const int ns = int(std::min<double>(spp, std::floor(budget / double(per))));
-    if (ns < 1) return 0;
-    const size_t n = size_t(P) * ns;
-    if (n > s->spec_cap) {
-        for (DevBuf *b : {&s->sp_col, &s->sp_fin, &s->sp_ctr}) {
-            b->~DevBuf();
-            new (b) DevBuf();
-        }
-        if (s->sp_col.alloc(n * sizeof(float4)) != hipSuccess || s->sp_fin.alloc(n * sizeof(float4)) != hipSuccess ||
-            s->sp_ctr.alloc(n * sizeof(uint4)) != hipSuccess) {
-            s->spec_cap = 0;
-            return 0;
-        }
-        s->spec_cap = n;
-    }
-    return ns;
-}
 
-int launch_scene_inw_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st, int ns);
 int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st);
 
 // Enqueue a whole render (all chunks) on `st`.  The first call for a given frame size
@@ -580,11 +555,9 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     if (s->kind == 3 && env_int("RT_IOW_SPEC", 1) != 0 && !rtk::iow_narrow(f) && s->s_stop > 0 &&
         ensure_spec(s, rtk::units_of(f), uint32_t(s->s_stop)))
         return launch_scene_spec(s, f, st);
+    // INW: the on-chip fold kernels; RT_INW_ORDER=-1 runs the per-pixel sequential kernel k_inw
+    // (a second restatement of End()'s loop, kept for the strategy-exactness tests)
     if (s->kind != 3 && env_int("RT_INW_ORDER", 0) >= 0) return launch_scene_inw_fold(s, f, st);
-    if (s->kind != 3 && env_int("RT_INW_SPEC", 1) != 0) {
-        const int ns = ensure_inw_spec(s, rtk::units_of(f), f.spp);
-        if (ns > 0) return launch_scene_inw_spec(s, f, st, ns);
-    }
     const std::vector<std::pair<int, int>> plan = chunk_plan(f.spp);
     const uint32_t units = rtk::units_of(f);
     s->last_kernel = s->kind == 3 ? (rtk::iow_narrow(f) ? "k_iow03n" : "k_iow03") : (s->layout == 4 ? "k_inw<true>" : "k_inw<false>");
@@ -1069,58 +1042,6 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     return RT_OK;
 }
 
-// Sample-parallel INW: chunks of ns samples; each chunk runs all its (pixel, sample) units
-// (compacted passes), then End() over the chunk adds the samples in order.
-int launch_scene_inw_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st, int ns) {
-    const uint32_t P = rtk::units_of(f);
-    int rc = ensure_workspace(s, P);
-    if (rc != RT_OK) return rc;
-    const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 6)));
-    if (rounds > 0 && (rc = ensure_cont(s)) != RT_OK) return rc;
-    unsigned *cnt = s->cont_count.as<unsigned>();
-    rtk::SpecRecs R{};
-    R.col = s->sp_col.as<float4>();
-    R.fin = s->sp_fin.as<float4>();
-    R.ctr = s->sp_ctr.as<uint4>();
-    R.P = P;
-    R.S = uint32_t(f.spp);
-    rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
-                     s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>(),
-                     s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
-    set_wide(s, sc);
-    const int cap = s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 7 : 6);
-    const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
-    hipError_t e = hipSuccess;
-    s->last_kernel = s->layout == 4 ? "k_inw_s<true>" : "k_inw_s<false>";
-    s->last_launches = (1 + rounds) * ((f.spp + ns - 1) / ns);
-    s->last_chunks = (f.spp + ns - 1) / ns;
-    for (int s0 = 0; s0 < f.spp && e == hipSuccess; s0 += ns) {
-        const int k = std::min(ns, f.spp - s0);
-        for (int r = 0; r <= rounds && e == hipSuccess; r++) {
-            rtk::Cont ct{};
-            uint32_t n_units = P * uint32_t(k);
-            if (r > 0) {
-                ct.in = s->cont[(r - 1) & 1].as<float4>();
-                ct.in_count = cnt + 16 * std::min(r - 1, 15);
-                n_units = uint32_t(cap) * rtk::kBlock;
-            }
-            if (r < rounds) {
-                ct.out = s->cont[r & 1].as<float4>();
-                ct.out_count = cnt + 16 * std::min(r, 15);
-                ct.park_min = park_min;
-                e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), st);
-                if (e != hipSuccess) break;
-            }
-            e = rtk::launch_inw_spec(f, sc, R, s0, k, ct, n_units, s->counter.as<unsigned>(), cap, st);
-        }
-        if (e == hipSuccess) e = rtk::launch_inw_fin(f, R, s0, k, s0 + k >= f.spp, s->ws_state.as<float4>(), st);
-    }
-    if (e != hipSuccess) {
-        std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
-        return RT_E_HIP;
-    }
-    return RT_OK;
-}
 
 // blocking render of one scene into host buffers
 int render_blocking(rt_dev_scene *s, const rt_camera *cam, const rt_params *p, float *rgba, float *depth,

@@ -2270,89 +2270,15 @@ __global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S, Chunk ch, C
     flush(f, c);
 }
 
-// ---------------------------------------------------------------- INW, sample-parallel
-// One unit = one sample of one pixel (u = (s - s0)*P + pu within a chunk of samples [s0, s0+ns)).
-// INW samples are independent invocations (01_BVH...glsl:601-675), so no speculation is needed:
-// each writes sqrt(colour), its depth and its counters to a record, and k_inw_fin adds the
-// records in sample order exactly as End() does.
-// 3 waves per SIMD: the kernel needs 149 (INW-01) / 159 (INW-04) VGPRs under that cap with no
-// spills; uncapped it took 169 and ran 2 waves per SIMD (LDS allows 4 blocks per CU).
+// ---------------------------------------------------------------- INW wave counts
+// Waves per SIMD of the 256-lane INW kernels: INW-04 (LIGHTS) at 3 (159 VGPRs, no spills);
+// INW-01 at 4 (128 VGPRs with a few spills, 8% faster on C3 than 3 waves in round 2).
 #ifndef RT_INW_WAVES
 #define RT_INW_WAVES 3
 #endif
 #ifndef RT_INW01_WAVES
 #define RT_INW01_WAVES 4  // INW-01: 128 VGPRs with a few spills, 8% faster on C3 than 3 waves
 #endif
-template <bool LIGHTS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES))) void k_inw_s(Frame f, InwScene S, SpecRecs R, int s0, int ns, Cont ct,
-                                                  unsigned *counter) {
-    __shared__ float lds[kFStack * kBlock];
-    Ctr c;
-    FStack K{lds + threadIdx.x, 0};
-    const uint32_t total = ct.in ? *ct.in_count : R.P * (uint32_t)ns;
-    const bool may_park = ct.out != nullptr && total >= ct.park_min;
-    bool live = true, busy = false;
-    uint32_t u = 0;
-    f3 col = f3{0, 0, 0};
-    float dep = 0.0f;
-    K.size = 0;
-    for (;;) {
-        const uint32_t q = fetch_unit(counter, live && !busy);
-        if (live && !busy) {
-            if (q >= total) live = false;
-            else if (ct.in) {  // resume a parked lane
-                const float4 *p = ct.in + (size_t)q * kContSlots;
-                const float4 m = p[0], a = p[1], b = p[2];
-                u = __float_as_uint(m.x); K.size = __float_as_uint(m.y); dep = m.z; c.seg = __float_as_uint(m.w);
-                col = f3{a.x, a.y, a.z}; c.nodes = __float_as_uint(a.w);
-                c.prims = __float_as_uint(b.x); c.shadow = __float_as_uint(b.y);
-                c.drops = __float_as_uint(b.z); c.nans = __float_as_uint(b.w);
-                const float *fl = reinterpret_cast<const float *>(p + 3);
-                for (int k = 0; k < kFStack; k++) K.base[k * kBlock] = fl[k];
-                busy = true;
-            } else {
-                u = q;
-                const UnitPix px = unit_pixel(f, u % R.P);
-                if (px.in_image) {
-                    busy = true;
-                    c.seg = c.nodes = c.prims = c.shadow = c.drops = c.nans = 0;
-                    inw_start_sample(S, f, K, px.x, px.y, s0 + (int)(u / R.P), c);
-                    col = f3{0, 0, 0};
-                    dep = 0.0f;
-                }
-            }
-        }
-        if (__ballot(live) == 0) break;
-        if (may_park && __ballot(!live) != 0 && __popcll(__ballot(busy)) < kParkBelow) {
-            const uint32_t slot = park_slot(ct.out_count, busy);
-            if (busy) {
-                float4 *p = ct.out + (size_t)slot * kContSlots;
-                p[0] = make_float4(ubits(u), ubits(K.size), dep, ubits(c.seg));
-                p[1] = make_float4(col.x, col.y, col.z, ubits(c.nodes));
-                p[2] = make_float4(ubits(c.prims), ubits(c.shadow), ubits(c.drops), ubits(c.nans));
-                float *fl = reinterpret_cast<float *>(p + 3);
-                for (int k = 0; k < kFStack; k++) fl[k] = K.base[k * kBlock];
-            }
-            break;
-        }
-        if (busy) inw_segment<LIGHTS>(S, f, K, s0 + (int)(u / R.P), col, dep, c);
-        if (busy && K.size == 0) {  // sample done
-#if defined(RT_EXP_NOREC)  // timing experiment only: no records (wrong image)
-            if (col.x == 12345.0f) R.col[u] = make_float4(col.x, col.y, col.z, dep);
-#elif defined(RT_EXP_NT)   // timing experiment: streaming (non-temporal) record stores
-            typedef float v4f __attribute__((ext_vector_type(4)));
-            __builtin_nontemporal_store(v4f{__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z), dep}, reinterpret_cast<v4f *>(&R.col[u]));
-            __builtin_nontemporal_store(v4f{ubits(c.seg), ubits(c.nodes), ubits(c.prims), ubits(c.shadow)}, reinterpret_cast<v4f *>(&R.ctr[u]));
-            __builtin_nontemporal_store(v4f{ubits(c.drops), ubits(c.nans), 0.0f, 0.0f}, reinterpret_cast<v4f *>(&R.fin[u]));
-#else
-            R.col[u] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z), dep);
-            R.ctr[u] = make_uint4(c.seg, c.nodes, c.prims, c.shadow);
-            R.fin[u] = make_float4(ubits(c.drops), ubits(c.nans), 0.0f, 0.0f);
-#endif
-            busy = false;
-        }
-    }
-}
 
 // ---------------------------------------------------------------- INW: on-chip End() folds
 // End() (01_BVH...glsl:625-653, 664-675) adds each sample's sqrt(colour) in sample order and
@@ -2696,46 +2622,6 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     flush(f, c);
 }
 
-// End() (01_BVH...glsl:664-675) over one chunk of samples: sum in sample order, depth of the
-// middle sample; the last chunk writes the pixel, the others carry the sum in `state`.
-__global__ __launch_bounds__(kBlock) void k_inw_fin(Frame f, SpecRecs R, int s0, int ns, int final_chunk,
-                                                    float4 *state) {
-    const uint32_t pu = blockIdx.x * kBlock + threadIdx.x;
-    const bool valid = pu < R.P;
-    const UnitPix px = unit_pixel(f, valid ? pu : 0);
-    const bool work = valid && px.in_image;
-    f3 acc = f3{0, 0, 0};
-    float dmid = 0.0f;
-    unsigned long long v[6] = {0, 0, 0, 0, 0, 0};
-    if (work && s0 > 0) {
-        const float4 a = state[pu];
-        acc = f3{a.x, a.y, a.z};
-        dmid = a.w;
-    }
-    for (int k = 0; work && k < ns; k++) {
-        const int s = s0 + k;
-        const size_t u = (size_t)k * R.P + pu;
-        const float4 cl = R.col[u];
-        const f3 g = f3{cl.x, cl.y, cl.z};
-        acc = sel(s == 0, g, acc + g);
-        if (s == f.spp / 2) dmid = cl.w;
-        const uint4 c4 = R.ctr[u];
-        const float4 fn = R.fin[u];
-        v[0] += c4.x; v[1] += c4.y; v[2] += c4.z; v[3] += c4.w;
-        v[4] += __float_as_uint(fn.x); v[5] += __float_as_uint(fn.y);
-    }
-    if (final_chunk && valid) {
-        if (work) write_px(f, px, acc * rcp((float)f.spp), dmid);
-        else write_px(f, px, f3{0, 0, 0}, 0.0f);
-    } else if (work) state[pu] = make_float4(acc.x, acc.y, acc.z, dmid);
-    if (f.counters) {
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-            const unsigned long long t = wave_sum(v[i]);
-            if ((threadIdx.x & 63) == 0 && t) atomicAdd(f.counters + i, t);
-        }
-    }
-}
 
 // ============================================================================ launch
 uint32_t units_of(const Frame &f) {
@@ -2771,8 +2657,6 @@ int resident_blocks_per_cu(int kind) {
     else if (kind == 10) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03sL, 3 * kBlock, 0);
     else if (kind == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03n, kBlock, 0);
     else if (kind == 5) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_iow03s, kBlock, 0);
-    else if (kind == 6) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_s<false>, kBlock, 0);
-    else if (kind == 7) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_s<true>, kBlock, 0);
     else if (kind == 14) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<true>, kBlock, 0);
     else if (kind == 15) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<false>, kBlock, 0);
     else if (kind == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<true>, kBlock, 0);
@@ -3004,15 +2888,6 @@ hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pa
     hipLaunchKernelGGL(k_iow03_resolve, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, final_pass ? 1 : 0, state);
     return hipGetLastError();
 }
-hipError_t launch_inw_spec(const Frame &f, const InwScene &sc, const SpecRecs &R, int s0, int ns, const Cont &ct,
-                           uint32_t n_units, unsigned *counter, int blocks_cap, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned), s);
-    if (e != hipSuccess) return e;
-    const dim3 g(grid_of(n_units, blocks_cap));
-    if (sc.layout == 4) hipLaunchKernelGGL(k_inw_s<true>, g, dim3(kBlock), 0, s, f, sc, R, s0, ns, ct, counter);
-    else hipLaunchKernelGGL(k_inw_s<false>, g, dim3(kBlock), 0, s, f, sc, R, s0, ns, ct, counter);
-    return hipGetLastError();
-}
 // One frame of the on-chip-fold INW kernels: the probe (unless forced), then k_inw_pm and
 // k_inw_sm, of which the one the probe did not pick exits at once.  ring: blocks * 4 waves *
 // max(ring_pm, ring_sm) float4; mode: 2 uints (zeroed here).  force: 0 = probe, 1 = pm, 2 = sm.
@@ -3054,13 +2929,6 @@ hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uin
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
-}
-hipError_t launch_inw_fin(const Frame &f, const SpecRecs &R, int s0, int ns, bool final_chunk, float4 *state,
-                          hipStream_t s) {
-    const unsigned blocks = (R.P + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_inw_fin, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, s0, ns, final_chunk ? 1 : 0,
-                       state);
-    return hipGetLastError();
 }
 hipError_t launch_inw(const Frame &f, const InwScene &sc, const Chunk &ch, const Cont &ct, uint32_t n_units,
                       unsigned *counter, int blocks_cap, hipStream_t s) {

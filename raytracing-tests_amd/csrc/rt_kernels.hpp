@@ -259,8 +259,6 @@ hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pa
 
 // sample-parallel INW over samples [s0, s0+ns) of every pixel (records indexed (s-s0)*P + pu),
 // then End() over that chunk: carry the sum in `state` or write the pixels
-hipError_t launch_inw_spec(const Frame &f, const InwScene &sc, const SpecRecs &R, int s0, int ns, const Cont &ct,
-                           uint32_t n_units, unsigned *counter, int blocks_cap, hipStream_t s);
 // INW with the on-chip End() folds (k_inw_probe + k_inw_pm / k_inw_sm); ring:
 // blocks * (kBlock / 64) * max(ring_pm, ring_sm) float4 (powers of two >= 64); counter: 2 queue
 // counters 64 B apart; mode: 2 uints; force: 0 = probe decides, 1 = pixel-major, 2 = sample-major
@@ -269,9 +267,6 @@ hipError_t launch_inw_spec(const Frame &f, const InwScene &sc, const SpecRecs &R
 hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uint32_t ring_pm, uint32_t ring_sm,
                            unsigned *counter, uint32_t *mode, uint32_t force, int blocks, int blocks_ln,
                            hipStream_t s);
-hipError_t launch_inw_fin(const Frame &f, const SpecRecs &R, int s0, int ns, bool final_chunk, float4 *state,
-                          hipStream_t s);
-
 // resident blocks per CU of the render kernel for `kind` (3 = IOW-03 wide, 4 = IOW-03 narrow,
 // 11/14 = INW layout 1/4)
 int resident_blocks_per_cu(int kind);  // 5 = sample-parallel IOW-03, 6/7 = sample-parallel INW 1/4,

@@ -28,9 +28,9 @@
 - a scene with 12 distinct refractive indices (more than the 8 alternative-run values the
   speculation tracks, DESIGN.md "Alternative runs"), default against the sequential kernel;
 - INW: RT_INW_ORDER=1/2 (the pixel- / sample-major on-chip fold instead of the probe's pick, with
-  small fold windows RT_INW_RING_PM / RT_INW_RING_SM), RT_INW_ORDER=-1 (per-sample records +
-  k_inw_fin), RT_INW_SPEC=0 (per-pixel sequential samples), RT_SPEC_MAX_GB tiny (record chunks) and
-  RT_INW_FAST=0 (the reference's LBVH walk instead of the wide walk; images and ray counts equal).
+  small fold windows RT_INW_RING_PM / RT_INW_RING_SM), RT_INW_ORDER=-1 (the per-pixel sequential
+  kernel k_inw), RT_INW_LDS=0 (no LDS-staged BVH top) and RT_INW_FAST=0 (the reference's LBVH walk
+  instead of the wide walk; images and ray counts equal).
 Each must give a bit-identical image of the final scene with identical ray counts.  The
 renders run in subprocesses because the switches are read by the library at scene build /
 launch time."""
@@ -75,7 +75,7 @@ def _render(tmp_path, over, w, h, spp, scene=IOW):
     out = str(tmp_path / f"img_{len(os.listdir(tmp_path))}.npy")
     env = dict(os.environ)
     for k in ("RT_IOW_LINEAR", "RT_IOW_NARROW", "RT_ROUNDS", "RT_CHUNKS", "RT_IOW_SPEC", "RT_SPEC_ITERS",
-              "RT_INW_SPEC", "RT_SPEC_MAX_GB", "RT_INW_ORDER", "RT_INW_RING_PM", "RT_INW_RING_SM",
+              "RT_INW_ORDER", "RT_INW_RING_PM", "RT_INW_RING_SM", "RT_INW_LDS",
               "RT_SPEC_VALIDATE", "RT_SPEC_PRIOR_FROM", "RT_COOP", "RT_IOW_LDS",
               "RT_SPEC_ROUNDS", "RT_SOLO", "RT_SPEC_HEAVY",
               "RT_SPEC_TAIL_ROUNDS", "RT_SPEC_TAIL_BUDGET", "RT_SPEC_SCAN",
@@ -155,7 +155,7 @@ def _same_frames(tmp_path, over, w, h, spp, scene):
 
 
 @pytest.mark.parametrize("over,scene,w,h,spp", [
-    ({"RT_INW_ORDER": "-1"}, INW1, 192, 108, 24),     # per-sample records + k_inw_fin
+    ({"RT_INW_ORDER": "-1"}, INW1, 192, 108, 24),     # the per-pixel sequential kernel k_inw
     ({"RT_INW_ORDER": "1"}, INW1, 200, 100, 37),       # pixel-major fold, spp not a multiple of the wave
     ({"RT_INW_ORDER": "2"}, INW1, 200, 100, 37),       # sample-major fold
     ({"RT_INW_ORDER": "1"}, INW1, 160, 96, 1),         # more than 64 pixels per fold window
@@ -167,12 +167,12 @@ def _same_frames(tmp_path, over, w, h, spp, scene):
     ({"RT_INW_ORDER": "-1"}, INW4, 128, 128, 16),
     ({"RT_INW_ORDER": "1"}, INW4, 128, 128, 16),
     ({"RT_INW_ORDER": "-1", "RT_INW_FAST": "0"}, INW4, 96, 96, 8),
-    ({"RT_INW_ORDER": "-1", "RT_INW_SPEC": "0"}, INW1, 192, 108, 24),
-    ({"RT_SPEC_MAX_GB": "0.005"}, INW1, 192, 108, 24),   # forces several sample chunks
-    ({"RT_INW_SPEC": "0"}, INW4, 128, 128, 16),
+    ({"RT_INW_ORDER": "-1"}, INW4, 96, 96, 12),
     ({"RT_INW_FAST": "0"}, INW1, 480, 270, 16),          # the reference's LBVH walk
     ({"RT_INW_FAST": "0"}, INW4, 256, 256, 12),
-    ({"RT_INW_FAST": "0", "RT_INW_SPEC": "0"}, INW1, 192, 108, 24),
+    ({"RT_INW_FAST": "0", "RT_INW_ORDER": "-1"}, INW1, 192, 108, 24),
+    ({"RT_INW_LDS": "0"}, INW1, 192, 108, 24),          # every wide node from global memory
+    ({"RT_INW_LDS": "0", "RT_INW_ORDER": "2"}, INW4, 128, 128, 16),
 ])
 def test_inw_strategies_bit_identical(tmp_path, gpu, over, scene, w, h, spp):
     a, sa = _render(tmp_path, {}, w, h, spp, scene)
