@@ -131,6 +131,7 @@ struct rt_dev_scene {
     DevBuf tex, tex_info;  // INW-04 material textures (float4 texels, (first, w, h, 0) per texture)
     DevBuf wnodes, wrank, wleaf;  // INW wide walk: culling BVH, depth-first ranks, LBVH leaf boxes
     int wdepth = 0;               // levels of the 4-wide culling BVH
+    bool last_ln = false;         // the last INW fold launch used the LDS-staged kernels
     uint32_t dfs_high = 0;
     uint32_t n_tex = 0;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
@@ -1014,6 +1015,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const int ord = env_int("RT_INW_ORDER", 0);
     const uint32_t force = (ord == 1 || ord == 2) ? uint32_t(ord) : 0u;
     s->last_kernel = s->layout == 4 ? "k_inw_fold<true>" : "k_inw_fold<false>";
+    s->last_ln = blocks_ln > 0;
     s->last_launches = 1;
     s->last_chunks = 1;
     s->kt_used = 0;
@@ -1271,8 +1273,11 @@ int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {
         HIP_OK(hipMemcpy(m, s->inw_mode.p, sizeof(m), hipMemcpyDeviceToHost));
         const int ord = env_int("RT_INW_ORDER", 0);
         const bool sm = ord == 2 || (ord != 1 && m[0] > 0 && 2 * m[1] >= m[0]);
-        static const char *names[2][2] = {{"k_inw_pm<false>", "k_inw_pm<true>"}, {"k_inw_sm<false>", "k_inw_sm<true>"}};
-        s->last_kernel = names[sm ? 1 : 0][s->layout == 4 ? 1 : 0];
+        // the template instance's name as rocprofv3 prints it (LN: the LDS-staged BVH top)
+        static const char *names[2][2][2] = {
+            {{"k_inw_pm<false>", "k_inw_pm<true>"}, {"k_inw_sm<false>", "k_inw_sm<true>"}},
+            {{"k_inw_pm<false, true>", "k_inw_pm<true, true>"}, {"k_inw_sm<false, true>", "k_inw_sm<true, true>"}}};
+        s->last_kernel = names[s->last_ln ? 1 : 0][sm ? 1 : 0][s->layout == 4 ? 1 : 0];
     }
     if (name_out && name_cap > 0) {
         std::strncpy(name_out, s->last_kernel, size_t(name_cap) - 1);

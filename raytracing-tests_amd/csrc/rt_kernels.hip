@@ -51,7 +51,19 @@ __device__ __forceinline__ Pix map_pixel(const Frame &f) {
 struct Ctr {
     uint32_t seg = 0, nodes = 0, prims = 0, shadow = 0, drops = 0, nans = 0;
     unsigned long long *wdbg = nullptr;  // diagnostics: this wave's kDbg* row in LDS, or null
+#ifdef RT_DIAG_SPLIT
+    unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // INW phase cycles of this wave (k_inw_pm/sm)
+#endif
 };
+// INW phase split (diagnostic builds, -DRT_DIAG_SPLIT): shader-clock cycles per wave of a phase,
+// summed into Frame::dbg slots by the fold kernels at exit
+#ifdef RT_DIAG_SPLIT
+#define INW_T0(t) const unsigned long long t = (unsigned long long)clock64()
+#define INW_CYC(c, k, t) ((c).cyc[k] += (unsigned long long)clock64() - (t))
+#else
+#define INW_T0(t) ((void)0)
+#define INW_CYC(c, k, t) ((void)0)
+#endif
 // Diagnostics (rt_debug_counters).  Tallies go to a per-wave LDS row, written by the first
 // active lane, so they cost no registers when off and are exact inside divergent code.
 __device__ __forceinline__ bool first_active_lane() {
@@ -2074,7 +2086,9 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         const float tlim0 = mf0 ? K.at(4) : kMaxT;
         float tlim = tlim0, extra = 0.0f;
         f3 normal = f3{0, 0, 0};
+        INW_T0(t_ch);
         float fg = inw_closest<true, LN>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
+        INW_CYC(c, 0, t_ch);
         const f3 hitpoint = co + cd * tlim;
         if (!(tlim < tlim0)) {
             if (mf0 && (int)(K.at(5) + 0.1f) < F.n_focus) {  // next focal lens, 01_BVH...glsl:506-528
@@ -2119,7 +2133,11 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         const bool ri_read = (m_refl > 0.002f || m_refr > 0.002f) && (m_refr > 0.002f || dot(normal, cd) > 0.0f);
         float surr = 1.0f;
         if (!LIGHTS && (ri_forced || (ri_read && contribution > 0.01f && bounced + 1.0f < (float)F.max_bounces)))
+        {
+            INW_T0(t_ri);
             surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
+            INW_CYC(c, 1, t_ri);
+        }
         if (mf0) K.size = 0;  // 01_BVH...glsl:544-549: the lens record goes after a primary hit
         if (LIGHTS) {  // 04...glsl:604-665
             uint32_t is_lit = S.n_lights > 0 ? 0u : (uint32_t)is_lit_geom(S, f2u(fg + 0.1f));
@@ -2385,36 +2403,14 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     float dep = 0.0f;
     K.size = 0;
     for (;;) {
-        // ---- fold the finished entries gf, gf+1, ... (stored in earlier iterations)
-        if (gf != gi) {
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's ring stores have landed (same CU: L1 write-through)
-            const uint32_t k = gf + lane;
-            bool fin = false;
-            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (k - gf < gi - gf) {
-                v = wr[k & rmask];
-                fin = __float_as_uint(v.w) == k;
-            }
-            const unsigned long long m = __ballot(fin);
-            const uint32_t n = ~m == 0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
-            for (uint32_t i = 0; i < n; i++) {
-                const f3 gv = f3{rdl(v.x, i), rdl(v.y, i), rdl(v.z, i)};
-                acc = sf == 0 ? gv : acc + gv;
-                if (++sf == spp) {  // pixel jf complete: End()'s imageStore (01_BVH...glsl:652)
-                    const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
-                    if (lane == 0) {
-                        const UnitPix p = unit_pixel(f, unit);
-                        if (p.out != (size_t)-1)
-                            reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
-                                make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
-                                            p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
-                    }
-                    sf = 0;
-                    jf++;
-                }
-            }
-            gf += n;
-        }
+        // ---- prefetch the fold window: ring entries gf .. gf + 63, loaded now and folded after
+        // this iteration's segment, so the load's latency hides behind the segment.  An entry
+        // stored in the previous iteration may read as not finished yet (the load may pass the
+        // store): it is then folded an iteration later.
+        const uint32_t gf0 = gf, gi0 = gi, kf = gf + lane;
+        float4 vf = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(~kf));  // (a tag that never matches)
+        if (kf - gf0 < gi0 - gf0) vf = wr[kf & rmask];
+        INW_T0(t_issue);
         // ---- claim pixels for the free lanes (at most 64 pixels between fold and issue)
         const unsigned long long fm = __ballot(!busy);
         const uint32_t nfree = (uint32_t)__popcll(fm);
@@ -2469,9 +2465,37 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 si = a2 % spp;
             }
         }
+        INW_CYC(c, 3, t_issue);
         if (qdone && ji == nclaimed && gf == gi && __ballot(busy) == 0) break;
         // ---- one ray segment per busy lane (samples are independent invocations)
+        INW_T0(t_seg);
         if (busy) inw_segment<LIGHTS, LN>(S, f, K, s, col, dep, c);
+        INW_CYC(c, 4, t_seg);
+        // ---- fold the prefetched window: its leading run of finished entries, in stream order
+        INW_T0(t_fold2);
+        {
+            const bool fin = kf - gf0 < gi0 - gf0 && __float_as_uint(vf.w) == kf;
+            const unsigned long long m = __ballot(fin);
+            const uint32_t n = ~m == 0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
+            for (uint32_t i = 0; i < n; i++) {
+                const f3 gv = f3{rdl(vf.x, i), rdl(vf.y, i), rdl(vf.z, i)};
+                acc = sf == 0 ? gv : acc + gv;
+                if (++sf == spp) {  // pixel jf complete: End()'s imageStore (01_BVH...glsl:652)
+                    const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
+                    if (lane == 0) {
+                        const UnitPix p = unit_pixel(f, unit);
+                        if (p.out != (size_t)-1)
+                            reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
+                                make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
+                                            p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
+                    }
+                    sf = 0;
+                    jf++;
+                }
+            }
+            gf += n;
+        }
+        INW_CYC(c, 2, t_fold2);
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
                                         __uint_as_float(g));
@@ -2479,6 +2503,16 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             busy = false;
         }
     }
+#ifdef RT_DIAG_SPLIT
+    // phases 0-1 run inside `if (busy)`: the wave's time there is the largest of its lanes'
+    for (int k = 0; k < 2; k++)
+        for (int o = 32; o >= 1; o >>= 1) {
+            const unsigned long long t = __shfl_xor(c.cyc[k], o, 64);
+            c.cyc[k] = t > c.cyc[k] ? t : c.cyc[k];
+        }
+    if (f.dbg && lane == 0)
+        for (int k = 0; k < 5; k++) atomicAdd(f.dbg + 8 + k, c.cyc[k]);
+#endif
     flush(f, c);
 }
 

@@ -17,3 +17,4 @@ for n in (2, 3):
     b = np.load('$O/f%d.npy' % n)
     print('ranks', n, 'bit-identical to 1 rank:', np.array_equal(a.view(np.uint32), b.view(np.uint32)), a.shape)
 " | tee $O/check.txt
+rm -f $O/f*.npy  # frames are 33 MB each: keep gpurun_out under its copy-back limit
