@@ -471,6 +471,9 @@ def main():
             out["lane_occupancy"] = {name: round(d[2 * i + 1] / max(d[2 * i], 1) / 64, 4)
                                      for i, name in enumerate(("outer", "bvh_walk", "leaf_tests", "segments"))}
             out["wave_iterations"] = {name: d[2 * i] for i, name in enumerate(("outer", "bvh_walk", "leaf_tests", "segments"))}
+            # wave cycles per phase (shader clock, summed over waves; kDbgCyc* slots)
+            out["wave_cycles"] = dict(zip(("camera", "launch_ray", "bvh_walk", "leaf_tests", "segment", "coop_query",
+                                           "coop_shade", "coop_pop"), d[8:16]))
             px_rays = buf["px_rays"]
             pr = px_rays[px_rays > 0].double()
             q = torch.quantile(pr.float().cpu(), torch.tensor([0.5, 0.9, 0.99, 0.999])).tolist()

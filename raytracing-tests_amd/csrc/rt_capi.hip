@@ -132,6 +132,8 @@ struct rt_dev_scene {
     DevBuf wnodes, wrank, wleaf;  // INW wide walk: culling BVH, depth-first ranks, LBVH leaf boxes
     int wdepth = 0;               // levels of the 4-wide culling BVH
     bool last_ln = false;         // the last INW fold launch used the LDS-staged kernels
+    bool last_fu = false;         // ... their fused-fma cull instances
+    float wbound = 0.0f;          // largest |coordinate| of the INW culling boxes (cull4f's condition)
     uint32_t dfs_high = 0;
     uint32_t n_tex = 0;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
@@ -149,6 +151,7 @@ struct rt_dev_scene {
     DevBuf sp_sorder, sp_fcost;  // heavy-first enumeration: sample indices by cost, their costs
     DevBuf inw_ring;             // k_inw_pm / k_inw_sm: the waves' fold rings
     DevBuf inw_mode;             // k_inw_probe's verdict (2 uints)
+    DevBuf inw_cost;             // claim order: block cost keys, the order, 256 bucket offsets
     DevBuf sp_dbg_t;             // RT_DEBUG_TIMES diagnostics: per unit start / end launch
     size_t sp_dbg_n = 0;         // units (P * S) of the render that last wrote sp_dbg_t
     uint32_t launch_seq = 0;
@@ -367,6 +370,7 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
     }
     // culling boxes: the leaf boxes, inflated as the IOW culling BVH's
     std::vector<float> boxes(size_t(n) * 6);
+    float wbound = 0.0f;
     for (uint32_t g = 0; g < n; g++) {
         const float *b = nodes + size_t(leaf[g]) * 8;  // bbmin xyz, bbmax xyz
         float big = 0.0f;
@@ -375,6 +379,7 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
             const float e = (b[3 + k] - b[k]) * 1e-3f + 1e-3f + big * 1e-5f;
             boxes[size_t(g) * 6 + k] = b[k] - e;
             boxes[size_t(g) * 6 + 3 + k] = b[3 + k] + e;
+            wbound = std::fmax(wbound, std::fmax(std::fabs(b[k] - e), std::fabs(b[3 + k] + e)));
         }
     }
     int depth = 0, depth4 = 0;
@@ -392,6 +397,7 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
     HIP_OK(s->wleaf.upload(lbox.data(), lbox.size() * sizeof(float)));
     s->dfs_high = high;
     s->wdepth = depth4;
+    s->wbound = wbound;
     return RT_OK;
 }
 
@@ -1012,10 +1018,19 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                      s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>(),
                      s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
     set_wide(s, sc);
+    // cull4f (one fma per plane) while every ray origin -- the camera (+ lens and the unit step
+    // of the primary ray), hit points inside the scene's boxes -- lies within 1000 of the origin
+    // (DESIGN.md §2); not with the MULTIFOCUS lens chain, whose lens points are farther out
+    {
+        const float cam = std::fmax(std::fabs(f.pos[0]), std::fmax(std::fabs(f.pos[1]), std::fabs(f.pos[2]))) +
+                          2.0f + std::fabs(f.aperture);
+        sc.fused = (env_int("RT_INW_FMA", 1) != 0 && f.n_focus == 0 && std::fmax(cam, s->wbound) <= 1000.0f) ? 1 : 0;
+    }
     const int ord = env_int("RT_INW_ORDER", 0);
     const uint32_t force = (ord == 1 || ord == 2) ? uint32_t(ord) : 0u;
     s->last_kernel = s->layout == 4 ? "k_inw_fold<true>" : "k_inw_fold<false>";
     s->last_ln = blocks_ln > 0;
+    s->last_fu = s->last_ln && sc.fused;
     s->last_launches = 1;
     s->last_chunks = 1;
     s->kt_used = 0;
@@ -1031,11 +1046,22 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         s->kt_used = 1;
     }
     // the rings are reset first, so the events bracket the probe and the two fold kernels
+    // claim order, costliest blocks first (RT_INW_COST=0: unit order)
+    uint32_t *cost = nullptr;
+    if (env_int("RT_INW_COST", 1) != 0) {
+        const size_t need = (2 * size_t(rtk::units_of(f) / 64) + 256) * sizeof(uint32_t);
+        if (s->inw_cost.bytes < need) {
+            s->inw_cost.~DevBuf();
+            new (&s->inw_cost) DevBuf();
+            if (s->inw_cost.alloc(need) != hipSuccess) return RT_E_HIP;
+        }
+        cost = s->inw_cost.as<uint32_t>();
+    }
     e = hipMemsetAsync(s->inw_ring.p, 0xff, ring_bytes, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->first, st);
     if (e == hipSuccess)
         e = rtk::launch_inw_fold(f, sc, s->inw_ring.as<float4>(), ring_pm, ring_sm, s->counter.as<unsigned>(),
-                                 s->inw_mode.as<uint32_t>(), force, blocks, blocks_ln, st);
+                                 s->inw_mode.as<uint32_t>(), force, blocks, blocks_ln, cost, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->second, st);
     if (e != hipSuccess) {
         std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
@@ -1273,11 +1299,16 @@ int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {
         HIP_OK(hipMemcpy(m, s->inw_mode.p, sizeof(m), hipMemcpyDeviceToHost));
         const int ord = env_int("RT_INW_ORDER", 0);
         const bool sm = ord == 2 || (ord != 1 && m[0] > 0 && 2 * m[1] >= m[0]);
-        // the template instance's name as rocprofv3 prints it (LN: the LDS-staged BVH top)
+        // the template instance's name as rocprofv3 prints it, every argument: every template argument: <LIGHTS, LN (LDS-staged BVH top), FU (fused cull)>
         static const char *names[2][2][2] = {
-            {{"k_inw_pm<false>", "k_inw_pm<true>"}, {"k_inw_sm<false>", "k_inw_sm<true>"}},
-            {{"k_inw_pm<false, true>", "k_inw_pm<true, true>"}, {"k_inw_sm<false, true>", "k_inw_sm<true, true>"}}};
-        s->last_kernel = names[s->last_ln ? 1 : 0][sm ? 1 : 0][s->layout == 4 ? 1 : 0];
+            {{"k_inw_pm<false, false, false>", "k_inw_pm<true, false, false>"},
+             {"k_inw_sm<false, false, false>", "k_inw_sm<true, false, false>"}},
+            {{"k_inw_pm<false, true, false>", "k_inw_pm<true, true, false>"},
+             {"k_inw_sm<false, true, false>", "k_inw_sm<true, true, false>"}}};
+        static const char *names_fu[2][2] = {{"k_inw_pm<false, true, true>", "k_inw_pm<true, true, true>"},
+                                             {"k_inw_sm<false, true, true>", "k_inw_sm<true, true, true>"}};
+        s->last_kernel = s->last_fu ? names_fu[sm ? 1 : 0][s->layout == 4 ? 1 : 0]
+                                    : names[s->last_ln ? 1 : 0][sm ? 1 : 0][s->layout == 4 ? 1 : 0];
     }
     if (name_out && name_cap > 0) {
         std::strncpy(name_out, s->last_kernel, size_t(name_cap) - 1);

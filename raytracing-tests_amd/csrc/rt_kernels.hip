@@ -219,6 +219,33 @@ __device__ __forceinline__ void cull4(const float4 lx, const float4 ly, const fl
     t2 = one(ax23.x, bx23.x, ay23.x, by23.x, az23.x, bz23.x);
     t3 = one(ax23.y, bx23.y, ay23.y, by23.y, az23.y, bz23.y);
 }
+// The same test with one fused multiply-add per plane: plane * (1/d) + (-o * (1/d)), the second
+// term computed once per ray (noid).  Its rounding error in t is at most |o| * 2^-23 * |1/d| per
+// axis, against a culling-box inflation of e >= 1e-3 (x |1/d| in t), so it stays conservative
+// while |o| * 2^-23 < e: the host enables it (InwScene::fused) only when every ray origin (the
+// camera, the scene's boxes) lies within 1000 of the origin.  INW only: its wide walk runs with
+// finite reciprocals (an infinite one would make every plane's fma NaN).
+__device__ __forceinline__ void cull4f(const float4 lx, const float4 ly, const float4 lz, const float4 hx,
+                                       const float4 hy, const float4 hz, f3 id, f3 noid, float lim, float &t0,
+                                       float &t1, float &t2, float &t3) {
+    const pf2 ix = pk(id.x, id.x), iy = pk(id.y, id.y), iz = pk(id.z, id.z);
+    const pf2 nx = pk(noid.x, noid.x), ny = pk(noid.y, noid.y), nz = pk(noid.z, noid.z);
+    const pf2 ax01 = __builtin_elementwise_fma(pk(lx.x, lx.y), ix, nx), bx01 = __builtin_elementwise_fma(pk(hx.x, hx.y), ix, nx);
+    const pf2 ay01 = __builtin_elementwise_fma(pk(ly.x, ly.y), iy, ny), by01 = __builtin_elementwise_fma(pk(hy.x, hy.y), iy, ny);
+    const pf2 az01 = __builtin_elementwise_fma(pk(lz.x, lz.y), iz, nz), bz01 = __builtin_elementwise_fma(pk(hz.x, hz.y), iz, nz);
+    const pf2 ax23 = __builtin_elementwise_fma(pk(lx.z, lx.w), ix, nx), bx23 = __builtin_elementwise_fma(pk(hx.z, hx.w), ix, nx);
+    const pf2 ay23 = __builtin_elementwise_fma(pk(ly.z, ly.w), iy, ny), by23 = __builtin_elementwise_fma(pk(hy.z, hy.w), iy, ny);
+    const pf2 az23 = __builtin_elementwise_fma(pk(lz.z, lz.w), iz, nz), bz23 = __builtin_elementwise_fma(pk(hz.z, hz.w), iz, nz);
+    auto one = [&](float x0, float x1, float y0, float y1, float z0, float z1) {
+        const float te = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+        const float tx = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+        return (te <= tx && tx >= -1e-3f && te <= lim) ? te : kMiss;
+    };
+    t0 = one(ax01.x, bx01.x, ay01.x, by01.x, az01.x, bz01.x);
+    t1 = one(ax01.y, bx01.y, ay01.y, by01.y, az01.y, bz01.y);
+    t2 = one(ax23.x, bx23.x, ay23.x, by23.x, az23.x, bz23.x);
+    t3 = one(ax23.y, bx23.y, ay23.y, by23.y, az23.y, bz23.y);
+}
 __device__ __forceinline__ void cswap(float &ta, int &ka, float &tb, int &kb) {
     const bool sw = tb < ta;
     const float t = sw ? tb : ta;
@@ -351,6 +378,9 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
         // farthest-first.
         DBG_T0(F_, t_trav);
         int sp = 0, pend = -1, cur = S.root_link;
+#ifdef RT_IOW_PEND2  // experiment: two postponed leaves per lane
+        int pend2 = -1;
+#endif
         bool walking = true, ovf = false;  // ovf: a child was dropped by a full stack
         float lim = min_t * 1.0001f + 1e-3f;  // culling limit, follows min_t
         for (;;) {
@@ -381,15 +411,29 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
                     cur = k0;
                     pop = t0 == kMiss;
                 } else {
+#ifdef RT_IOW_PEND2
+                    pop = pend < 0 || pend2 < 0;
+                    if (pend < 0) pend = -cur;
+                    else if (pend2 < 0) pend2 = -cur;
+#else
                     pop = pend < 0;  // a leaf waits while the lane still holds one
                     if (pop) pend = -cur;
+#endif
                 }
                 if (pop) {
                     if (sp == 0) walking = false;
                     else cur = bstk[(--sp) * kBlock];
                 }
             }
+#ifdef RT_IOW_PEND2
+            if (__all(!walking || pend2 >= 0) || __popcll(__ballot(pend >= 0)) >= F_.leaf_batch) {
+                if (pend >= 0) { test(pend); pend = pend2; pend2 = -1; lim = min_t * 1.0001f + 1e-3f; }
+                if (__all(!walking && pend < 0)) break;
+            }
+            if (false) {
+#else
             if (__all(!walking || pend >= 0) || __popcll(__ballot(pend >= 0)) >= F_.leaf_batch) {
+#endif
                 DBG_TALLY(F_, c, kDbgLeaf, pend >= 0);
                 DBG_T0(F_, t_leaf);
                 if (pend >= 0) { test(pend); pend = -1; lim = min_t * 1.0001f + 1e-3f; }
@@ -1804,7 +1848,7 @@ __device__ __forceinline__ void inw_wnode(const InwScene &S, int cur, float4 &lx
 // inside its own box, and then skipping it changes nothing; but where an object's face coincides
 // with its box face, rounding can put t an ulp below te.  Any accepted candidate with t < te
 // therefore hands the ray to the reference walk (ok = false).
-template <bool WANT_NORMAL, bool LN = false>
+template <bool WANT_NORMAL, bool LN = false, bool FU = false>
 __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
                                    f3 &normal, float &extra, float init_geom, Ctr &c, bool &ok) {
     const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};  // the reference's reciprocals (test_aabb)
@@ -1817,6 +1861,7 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
     uint32_t br = 0xffffffffu;
     const uint32_t *rank = S.rank + (invert ? S.n : 0u);
     const f3 fid = f3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
+    const f3 noid = f3{-(o.x * fid.x), -(o.y * fid.y), -(o.z * fid.z)};  // cull4f's per-ray term (FU)
     const int base = (int)K.size, cap = kFStack - 3 - base;  // 3 spare slots for branch-free pushes
     int sp = 0, pend = -1, cur = S.wroot;
     bool walking = ok, ovf = false;
@@ -1846,7 +1891,8 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
                 inw_wnode<LN>(S, cur, lx, ly, lz, hx, hy, hz, lk);
                 c.nodes += 4;
                 float t0, t1, t2, t3;
-                cull4(lx, ly, lz, hx, hy, hz, o, fid, lim, t0, t1, t2, t3);
+                if constexpr (FU) cull4f(lx, ly, lz, hx, hy, hz, fid, noid, lim, t0, t1, t2, t3);
+                else cull4(lx, ly, lz, hx, hy, hz, o, fid, lim, t0, t1, t2, t3);
                 int k0 = __float_as_int(lk.x), k1 = __float_as_int(lk.y), k2 = __float_as_int(lk.z),
                     k3 = __float_as_int(lk.w);
                 cswap(t0, k0, t1, k1); cswap(t2, k2, t3, k3);
@@ -1962,11 +2008,11 @@ __device__ float inw_surrounding_ri_wide(const InwScene &S, FStack &K, f3 hp, fl
     return acc;
 }
 
-template <bool WANT_NORMAL, bool LN = false>
+template <bool WANT_NORMAL, bool LN = false, bool FU = false>
 __device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
                                              float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c) {
     bool ok = false;
-    const float g = inw_traverse_wide<WANT_NORMAL, LN>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c, ok);
+    const float g = inw_traverse_wide<WANT_NORMAL, LN, FU>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c, ok);
     if (ok) return g;
     return inw_traverse<WANT_NORMAL>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
 }
@@ -2070,7 +2116,7 @@ __device__ f3 inw_tex_color(const InwScene &S, uint32_t k, f3 lp) {
 
 // One iteration of out_Pixel's ray loop (01_BVH...glsl:414-597 / 04...glsl:510-713):
 // pop a ray, closest hit, surrounding RI, shadow rays, push reflect/refract, accumulate.
-template <bool LIGHTS, bool LN = false>
+template <bool LIGHTS, bool LN = false, bool FU = false>
 __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s, f3 &color, float &depth, Ctr &c) {
     const f3 D = mk(F.dir[0], F.dir[1], F.dir[2]);
     const float ratio = (float)s * F.inv_spp;
@@ -2087,7 +2133,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         float tlim = tlim0, extra = 0.0f;
         f3 normal = f3{0, 0, 0};
         INW_T0(t_ch);
-        float fg = inw_closest<true, LN>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
+        float fg = inw_closest<true, LN, FU>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
         INW_CYC(c, 0, t_ch);
         const f3 hitpoint = co + cd * tlim;
         if (!(tlim < tlim0)) {
@@ -2150,7 +2196,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
                     f3 sd = normalize((bmin + (bmax - bmin) * ratio) - so);
                     c.shadow++;
                     f3 dummy_n; float dummy_e;
-                    float sg = inw_closest<false, LN>(S, K, so, sd, ratio, invert, sl, dummy_n, dummy_e, -1.0f, c);
+                    float sg = inw_closest<false, LN, FU>(S, K, so, sd, ratio, invert, sl, dummy_n, dummy_e, -1.0f, c);
                     is_lit += (uint32_t)is_lit_geom(S, f2u(sg + 0.1f));
                 }
                 const uint32_t nl = S.n_lights > 1 ? S.n_lights : 1u;
@@ -2365,11 +2411,87 @@ __global__ __launch_bounds__(kBlock) void k_inw_probe(Frame f, InwScene S, uint3
     }
 }
 
+// Claim order (DESIGN.md §5 "Claim order"): a persistent fold kernel's tail is the last pixels
+// it claims -- a wave needs spp / 64 rounds of samples for one pixel, so expensive pixels claimed
+// last leave the rest of the chip idle.  k_inw_cost estimates each 8x8 block's cost from the
+// primary rays of 16 of its pixels (a miss or a diffuse hit ends the sample; a reflective /
+// refractive hit starts a chain of about log(0.01) / log(coefficient) segments, two-sided for
+// refraction) and buckets it (256 log-scale keys); k_inw_order_scan / k_inw_order_scatter lay
+// the blocks out costliest first, and k_inw_pm claims through that order.  The order only decides
+// which wave traces which pixel when: every pixel's samples and sums are the same.  Pixel-major
+// frames only: the three kernels exit at once when the probe picked k_inw_sm, whose 8x8 blocks
+// keep their spatial order (measured: C5 3% slower with it, the blocks' locality lost).
+template <bool LIGHTS>
+__global__ __launch_bounds__(kBlock) void k_inw_cost(Frame f, InwScene S, uint32_t *key, uint32_t *hist,
+                                                     const uint32_t *mode, uint32_t force) {
+    if (inw_sample_major(mode, force)) return;
+    __shared__ float lds[kFStack * kBlock];
+    Ctr c;  // not flushed: these rays are not the frame's
+    FStack K{lds + threadIdx.x, 0};
+    const uint32_t lane = threadIdx.x & 63u, nblk = units_total(f) / 64u, p = lane & 15u;
+    const uint32_t blk = ((blockIdx.x * kBlock + threadIdx.x) >> 4);  // 16 lanes per block
+    float est = 0.0f;
+    if (blk < nblk) {
+        const UnitPix px = unit_pixel(f, blk * 64u + (p >> 2) * 16u + (p & 3u) * 2u);
+        if (px.in_image) {
+            const int s = f.spp / 2;
+            inw_start_sample(S, f, K, px.x, px.y, s, c);
+            K.size -= 8;
+            const uint32_t b = K.size;
+            const f3 o = mk(K.at(b), K.at(b + 1), K.at(b + 2)), d = mk(K.at(b + 3), K.at(b + 4), K.at(b + 5));
+            const f3 D = mk(f.dir[0], f.dir[1], f.dir[2]);
+            float tlim = kMaxT, extra = 0.0f;
+            f3 nrm;
+            const float g = inw_closest<false>(S, K, o, d, (float)s * f.inv_spp, dot(D, f3{1, 1, 1}) > 0.0f, tlim,
+                                               nrm, extra, -1.0f, c);
+            est = 1.0f;
+            if (tlim < kMaxT) {
+                const float4 m0 = S.cold[2 * (int)g];
+                const float m = fminf(fmaxf(m0.x, m0.y), 0.99f);
+                if (LIGHTS) est += (float)S.n_lights;
+                if (m > 0.002f) {
+                    const float n = fminf((float)f.max_bounces, 1.0f + __logf(0.01f) / __logf(m));
+                    est += n * (m0.x > 0.002f ? 2.0f : 1.0f) * (LIGHTS ? 1.0f + (float)S.n_lights : 1.0f);
+                }
+            }
+        }
+    }
+    for (int o = 8; o >= 1; o >>= 1) est += __shfl_xor(est, o, 64);
+    if (p == 0 && blk < nblk) {
+        const uint32_t k = (uint32_t)fminf(255.0f, 16.0f * __log2f(1.0f + est));
+        key[blk] = k;
+        atomicAdd(hist + (255u - k), 1u);
+    }
+}
+// exclusive scan of the 256 bucket counts (one 256-lane block)
+__global__ __launch_bounds__(256) void k_inw_order_scan(uint32_t *hist, const uint32_t *mode, uint32_t force) {
+    if (inw_sample_major(mode, force)) return;
+    __shared__ uint32_t t[256];
+    const uint32_t i = threadIdx.x;
+    const uint32_t v = hist[i];
+    t[i] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < 256u; o <<= 1) {
+        const uint32_t a = i >= o ? t[i - o] : 0u;
+        __syncthreads();
+        t[i] += a;
+        __syncthreads();
+    }
+    hist[i] = t[i] - v;
+}
+__global__ __launch_bounds__(kBlock) void k_inw_order_scatter(const uint32_t *key, uint32_t *off, uint32_t *order,
+                                                               uint32_t nblk, const uint32_t *mode, uint32_t force) {
+    if (inw_sample_major(mode, force)) return;
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nblk) return;
+    order[atomicAdd(off + (255u - key[i]), 1u)] = i;
+}
+
 // pixel-major stream (see above): entry g = (claimed pixel ordinal j, sample s).  LN: 768-lane
 // blocks (3 waves per SIMD) that stage the top of the wide BVH in the LDS their three 256-lane
 // stacks leave free (kInwLdsNodes nodes)
-template <bool LIGHTS, bool LN = false>
-__global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_waves_per_eu(LN ? 3 : (LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES)))) void k_inw_pm(Frame f, InwScene S0, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force) {
+template <bool LIGHTS, bool LN = false, bool FU = false>
+__global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_waves_per_eu(LN ? 3 : (LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES)))) void k_inw_pm(Frame f, InwScene S0, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force, const uint32_t *border) {
     if (inw_sample_major(mode, force)) return;  // the probe picked k_inw_sm for this frame
     constexpr int SUB = LN ? 3 : 1;
     __shared__ float lds[SUB * kFStack * kBlock];
@@ -2381,6 +2503,10 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         S.n_lnodes = n;
     }
     Ctr c;
+#ifdef RT_DIAG_SPLIT
+    const unsigned long long t_start = wall_clock64();  // the tail split (tools/inw_split.py)
+    unsigned long long t_qd = 0;
+#endif
     FStack K{lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock), 0};
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t rsize = rmask + 1u;
@@ -2403,13 +2529,38 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     float dep = 0.0f;
     K.size = 0;
     for (;;) {
-        // ---- prefetch the fold window: ring entries gf .. gf + 63, loaded now and folded after
-        // this iteration's segment, so the load's latency hides behind the segment.  An entry
-        // stored in the previous iteration may read as not finished yet (the load may pass the
-        // store): it is then folded an iteration later.
-        const uint32_t gf0 = gf, gi0 = gi, kf = gf + lane;
-        float4 vf = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(~kf));  // (a tag that never matches)
-        if (kf - gf0 < gi0 - gf0) vf = wr[kf & rmask];
+        // ---- fold the finished entries gf, gf+1, ... (stored in earlier iterations)
+        INW_T0(t_fold);
+        if (gf != gi) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's ring stores have landed (same CU: L1 write-through)
+            const uint32_t k = gf + lane;
+            bool fin = false;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (k - gf < gi - gf) {
+                v = wr[k & rmask];
+                fin = __float_as_uint(v.w) == k;
+            }
+            const unsigned long long m = __ballot(fin);
+            const uint32_t n = ~m == 0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
+            for (uint32_t i = 0; i < n; i++) {
+                const f3 gv = f3{rdl(v.x, i), rdl(v.y, i), rdl(v.z, i)};
+                acc = sf == 0 ? gv : acc + gv;
+                if (++sf == spp) {  // pixel jf complete: End()'s imageStore (01_BVH...glsl:652)
+                    const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
+                    if (lane == 0) {
+                        const UnitPix p = unit_pixel(f, unit);
+                        if (p.out != (size_t)-1)
+                            reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
+                                make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
+                                            p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
+                    }
+                    sf = 0;
+                    jf++;
+                }
+            }
+            gf += n;
+        }
+        INW_CYC(c, 2, t_fold);
         INW_T0(t_issue);
         // ---- claim pixels for the free lanes (at most 64 pixels between fold and issue)
         const unsigned long long fm = __ballot(!busy);
@@ -2426,8 +2577,14 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 uint32_t got = want;
                 if (base >= total) { got = 0; qdone = true; }
                 else if (base + want >= total) { got = total - base; qdone = true; }
+#ifdef RT_DIAG_SPLIT
+                if (qdone && t_qd == 0) t_qd = wall_clock64();
+#endif
                 const uint32_t rel = (lane - nclaimed) & 63u;
-                if (rel < got) pix_slot = base + rel;
+                if (rel < got) {  // ordinal -> unit through the claim order (block-wise)
+                    const uint32_t u = base + rel;
+                    pix_slot = border ? border[u >> 6] * 64u + (u & 63u) : u;
+                }
                 nclaimed += got;
             }
         }
@@ -2469,33 +2626,8 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         if (qdone && ji == nclaimed && gf == gi && __ballot(busy) == 0) break;
         // ---- one ray segment per busy lane (samples are independent invocations)
         INW_T0(t_seg);
-        if (busy) inw_segment<LIGHTS, LN>(S, f, K, s, col, dep, c);
+        if (busy) inw_segment<LIGHTS, LN, FU>(S, f, K, s, col, dep, c);
         INW_CYC(c, 4, t_seg);
-        // ---- fold the prefetched window: its leading run of finished entries, in stream order
-        INW_T0(t_fold2);
-        {
-            const bool fin = kf - gf0 < gi0 - gf0 && __float_as_uint(vf.w) == kf;
-            const unsigned long long m = __ballot(fin);
-            const uint32_t n = ~m == 0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
-            for (uint32_t i = 0; i < n; i++) {
-                const f3 gv = f3{rdl(vf.x, i), rdl(vf.y, i), rdl(vf.z, i)};
-                acc = sf == 0 ? gv : acc + gv;
-                if (++sf == spp) {  // pixel jf complete: End()'s imageStore (01_BVH...glsl:652)
-                    const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
-                    if (lane == 0) {
-                        const UnitPix p = unit_pixel(f, unit);
-                        if (p.out != (size_t)-1)
-                            reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
-                                make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
-                                            p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
-                    }
-                    sf = 0;
-                    jf++;
-                }
-            }
-            gf += n;
-        }
-        INW_CYC(c, 2, t_fold2);
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
                                         __uint_as_float(g));
@@ -2510,15 +2642,22 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             const unsigned long long t = __shfl_xor(c.cyc[k], o, 64);
             c.cyc[k] = t > c.cyc[k] ? t : c.cyc[k];
         }
-    if (f.dbg && lane == 0)
+    if (f.dbg && lane == 0) {
         for (int k = 0; k < 5; k++) atomicAdd(f.dbg + 8 + k, c.cyc[k]);
+        // wall clock (100 MHz): first / last wave start, first queue drain, first / last wave exit
+        const unsigned long long t_end = wall_clock64();
+        unsigned long long *t = reinterpret_cast<unsigned long long *>(f.dbg) + 16;
+        atomicMin(t, t_start); atomicMax(t + 1, t_start);
+        if (t_qd) atomicMin(t + 2, t_qd);
+        atomicMin(t + 3, t_end); atomicMax(t + 4, t_end);
+    }
 #endif
     flush(f, c);
 }
 
 // sample-major stream (see above): entry g = block ordinal b, sample s, pixel p (b * 64 * spp + s * 64 + p)
-template <bool LIGHTS, bool LN = false>
-__global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_waves_per_eu(LN ? 3 : (LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES)))) void k_inw_sm(Frame f, InwScene S0, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force) {
+template <bool LIGHTS, bool LN = false, bool FU = false>
+__global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_waves_per_eu(LN ? 3 : (LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES)))) void k_inw_sm(Frame f, InwScene S0, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force, const uint32_t *) {
     if (!inw_sample_major(mode, force)) return;  // the probe picked k_inw_pm for this frame
     constexpr int SUB = LN ? 3 : 1;
     __shared__ float lds[SUB * kFStack * kBlock];
@@ -2645,7 +2784,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             }
         }
         if (qdone && bi == nclaimed && bmin == nclaimed && __ballot(busy) == 0) break;
-        if (busy) inw_segment<LIGHTS, LN>(S, f, K, s, col, dep, c);
+        if (busy) inw_segment<LIGHTS, LN, FU>(S, f, K, s, col, dep, c);
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
                                         __uint_as_float(g));
@@ -2927,11 +3066,26 @@ hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pa
 // max(ring_pm, ring_sm) float4; mode: 2 uints (zeroed here).  force: 0 = probe, 1 = pm, 2 = sm.
 hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uint32_t ring_pm, uint32_t ring_sm,
                            unsigned *counter, uint32_t *mode, uint32_t force, int blocks, int blocks_ln,
-                           hipStream_t s) {
+                           uint32_t *cost, hipStream_t s) {
     for (uint32_t r : {ring_pm, ring_sm})
         if (r < 64 || (r & (r - 1))) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(mode, 0, 2 * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
+    // claim order of k_inw_pm (cost: 2 * nblk + 256 uints, or null = unit order)
+    const uint32_t *border = nullptr;
+    if (cost && units_of(f) >= 64u) {
+        const uint32_t nblk = units_of(f) / 64u;
+        uint32_t *key = cost, *order = cost + nblk, *hist = cost + 2 * nblk;
+        if ((e = hipMemsetAsync(hist, 0, 256 * sizeof(uint32_t), s)) != hipSuccess) return e;
+        const dim3 g((nblk + 15u) / 16u);  // 16 blocks of 8x8 pixels per 256-lane block
+        if (sc.layout == 4) hipLaunchKernelGGL(k_inw_cost<true>, g, dim3(kBlock), 0, s, f, sc, key, hist, mode, force);
+        else hipLaunchKernelGGL(k_inw_cost<false>, g, dim3(kBlock), 0, s, f, sc, key, hist, mode, force);
+        hipLaunchKernelGGL(k_inw_order_scan, dim3(1), dim3(256), 0, s, hist, mode, force);
+        hipLaunchKernelGGL(k_inw_order_scatter, dim3((nblk + kBlock - 1) / kBlock), dim3(kBlock), 0, s, key, hist,
+                           order, nblk, mode, force);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        border = order;
+    }
     if (force == 0) {
         const uint32_t nblk = units_of(f) / 64u, waves = 1024u;  // ~1024 probe blocks of 8x8 pixels
         const uint32_t stride = nblk > waves ? nblk / waves : 1u, nw = (nblk + stride - 1u) / stride;
@@ -2944,21 +3098,27 @@ hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uin
         if ((e = hipMemsetAsync(counter + 16 * k, 0, sizeof(unsigned), s)) != hipSuccess) return e;
         const uint32_t rm = (k == 0 ? ring_pm : ring_sm) - 1u;
         unsigned *ctr = counter + 16 * k;
-        if (blocks_ln > 0) {  // the LDS-staged BVH top (768-lane blocks)
+        if (blocks_ln > 0) {  // the LDS-staged BVH top (768-lane blocks); FU: the fused-fma cull
             const dim3 g(blocks_ln), b(3 * kBlock);
+#define RT_INW_LN_LAUNCH(L, F)                                                                              \
+    do {                                                                                                    \
+        if (k == 0) hipLaunchKernelGGL((k_inw_pm<L, true, F>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border); \
+        else hipLaunchKernelGGL((k_inw_sm<L, true, F>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border);        \
+    } while (0)
             if (sc.layout == 4) {
-                if (k == 0) hipLaunchKernelGGL((k_inw_pm<true, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force);
-                else hipLaunchKernelGGL((k_inw_sm<true, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force);
+                if (sc.fused) RT_INW_LN_LAUNCH(true, true);
+                else RT_INW_LN_LAUNCH(true, false);
             } else {
-                if (k == 0) hipLaunchKernelGGL((k_inw_pm<false, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force);
-                else hipLaunchKernelGGL((k_inw_sm<false, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force);
+                if (sc.fused) RT_INW_LN_LAUNCH(false, true);
+                else RT_INW_LN_LAUNCH(false, false);
             }
+#undef RT_INW_LN_LAUNCH
         } else if (sc.layout == 4) {
-            if (k == 0) hipLaunchKernelGGL(k_inw_pm<true>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter, mode, force);
-            else hipLaunchKernelGGL(k_inw_sm<true>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter + 16, mode, force);
+            if (k == 0) hipLaunchKernelGGL(k_inw_pm<true>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter, mode, force, border);
+            else hipLaunchKernelGGL(k_inw_sm<true>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter + 16, mode, force, border);
         } else {
-            if (k == 0) hipLaunchKernelGGL(k_inw_pm<false>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter, mode, force);
-            else hipLaunchKernelGGL(k_inw_sm<false>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter + 16, mode, force);
+            if (k == 0) hipLaunchKernelGGL(k_inw_pm<false>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter, mode, force, border);
+            else hipLaunchKernelGGL(k_inw_sm<false>, dim3(blocks), dim3(kBlock), 0, s, f, sc, ring, rm, counter + 16, mode, force, border);
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }

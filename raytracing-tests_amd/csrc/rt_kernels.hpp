@@ -79,6 +79,7 @@ struct InwScene {
     uint32_t dfs_high = 0;
     uint32_t n_wnodes = 0;  // wide nodes
     uint32_t n_lnodes = 0;  // the first n_lnodes wide nodes are staged in LDS (LN kernels only)
+    int fused = 0;          // the wide walk culls with one fma per plane (cull4f; set per frame)
 };
 
 // One launch of a chunked render: samples [s_begin, s_end) of every pixel unit.  A pixel's
@@ -266,7 +267,7 @@ hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pa
 // staged in LDS (ring: max(blocks * 4, blocks_ln * 12) waves)
 hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uint32_t ring_pm, uint32_t ring_sm,
                            unsigned *counter, uint32_t *mode, uint32_t force, int blocks, int blocks_ln,
-                           hipStream_t s);
+                           uint32_t *cost, hipStream_t s);
 // resident blocks per CU of the render kernel for `kind` (3 = IOW-03 wide, 4 = IOW-03 narrow,
 // 11/14 = INW layout 1/4)
 int resident_blocks_per_cu(int kind);  // 5 = sample-parallel IOW-03, 6/7 = sample-parallel INW 1/4,
