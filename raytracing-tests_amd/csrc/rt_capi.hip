@@ -133,7 +133,7 @@ struct rt_dev_scene {
     int wdepth = 0;               // levels of the 4-wide culling BVH
     bool last_ln = false;         // the last INW fold launch used the LDS-staged kernels
     bool last_fu = false;         // ... their fused-fma cull instances
-    float wbound = 0.0f;          // largest |coordinate| of the INW culling boxes (cull4f's condition)
+    float wbound = 0.0f;          // largest |coordinate| of the INW culling boxes (the fused cull's condition)
     uint32_t dfs_high = 0;
     uint32_t n_tex = 0;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
@@ -326,7 +326,7 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     sc.rank = s->wrank.as<uint32_t>();
     sc.leafbox = s->wleaf.as<float4>();
     sc.dfs_high = s->dfs_high;
-    sc.n_wnodes = uint32_t(s->wnodes.bytes / (8 * sizeof(float4)));
+    sc.n_wnodes = uint32_t(s->wnodes.bytes / (10 * sizeof(float4)));
 }
 
 int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
@@ -385,12 +385,18 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
     int depth = 0, depth4 = 0;
     const std::vector<float> bin = rtamd::sah_build(boxes.data(), n, &depth);
     std::vector<float> wide = rtamd::bvh4_collapse(bin, &depth4);
-    for (size_t w = 0; w < wide.size() / 32; w++)  // child links as int bits
+    // rtk::kInwNodeF4 = 10 float4 per node: lx ly lz hx hy hz lx ly lz, child links as int bits
+    const size_t nw = wide.size() / 32;
+    std::vector<float> wn(nw * 40);
+    for (size_t w = 0; w < nw; w++) {
+        std::memcpy(&wn[w * 40], &wide[w * 32], 24 * sizeof(float));
+        std::memcpy(&wn[w * 40 + 24], &wide[w * 32], 12 * sizeof(float));
         for (int k = 0; k < 4; k++) {
             const int link = int(wide[w * 32 + 24 + size_t(k)]);
-            std::memcpy(&wide[w * 32 + 24 + size_t(k)], &link, sizeof(link));
+            std::memcpy(&wn[w * 40 + 36 + size_t(k)], &link, sizeof(link));
         }
-    HIP_OK(s->wnodes.upload(wide.data(), wide.size() * sizeof(float)));
+    }
+    HIP_OK(s->wnodes.upload(wn.data(), wn.size() * sizeof(float)));
     HIP_OK(s->wrank.upload(rank.data(), rank.size() * sizeof(uint32_t)));
     std::vector<float> lbox(size_t(n) * 8);  // each object's LBVH leaf node, indexed by object
     for (uint32_t g = 0; g < n; g++) std::memcpy(&lbox[size_t(g) * 8], nodes + size_t(leaf[g]) * 8, 8 * sizeof(float));
@@ -1018,7 +1024,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                      s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>(),
                      s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
     set_wide(s, sc);
-    // cull4f (one fma per plane) while every ray origin -- the camera (+ lens and the unit step
+    // the fused cull (cull4nf<true>: one fma per plane) while every ray origin -- the camera (+ lens and the unit step
     // of the primary ray), hit points inside the scene's boxes -- lies within 1000 of the origin
     // (DESIGN.md §2); not with the MULTIFOCUS lens chain, whose lens points are farther out
     {

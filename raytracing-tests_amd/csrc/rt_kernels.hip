@@ -171,7 +171,8 @@ __device__ __forceinline__ IowObj iow_obj(const float *__restrict__ h) {
 // Culling-only slab test for the IOW BVH (never decides a hit: the exact object test does).
 // Boxes are inflated on the host and the limit carries relative slack, so an object whose
 // exact t can win is never culled.  (plane - o) * (1/d) keeps a small relative error in t;
-// the fused form plane*(1/d) - o*(1/d) would cancel catastrophically for large o/d.
+// the fused form plane*(1/d) - o*(1/d) would cancel catastrophically for large o/d (INW uses it
+// only under the bound of cull4nf below).
 __device__ __forceinline__ bool cull_slab(float4 n0, float4 n1, f3 o, f3 id, float lim, float &te) {
     const float x0 = (n0.x - o.x) * id.x, x1 = (n0.w - o.x) * id.x;
     const float y0 = (n0.y - o.y) * id.y, y1 = (n1.x - o.y) * id.y;
@@ -209,33 +210,6 @@ __device__ __forceinline__ void cull4(const float4 lx, const float4 ly, const fl
     const pf2 ax23 = (pk(lx.z, lx.w) - ox) * ix, bx23 = (pk(hx.z, hx.w) - ox) * ix;
     const pf2 ay23 = (pk(ly.z, ly.w) - oy) * iy, by23 = (pk(hy.z, hy.w) - oy) * iy;
     const pf2 az23 = (pk(lz.z, lz.w) - oz) * iz, bz23 = (pk(hz.z, hz.w) - oz) * iz;
-    auto one = [&](float x0, float x1, float y0, float y1, float z0, float z1) {
-        const float te = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-        const float tx = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-        return (te <= tx && tx >= -1e-3f && te <= lim) ? te : kMiss;
-    };
-    t0 = one(ax01.x, bx01.x, ay01.x, by01.x, az01.x, bz01.x);
-    t1 = one(ax01.y, bx01.y, ay01.y, by01.y, az01.y, bz01.y);
-    t2 = one(ax23.x, bx23.x, ay23.x, by23.x, az23.x, bz23.x);
-    t3 = one(ax23.y, bx23.y, ay23.y, by23.y, az23.y, bz23.y);
-}
-// The same test with one fused multiply-add per plane: plane * (1/d) + (-o * (1/d)), the second
-// term computed once per ray (noid).  Its rounding error in t is at most |o| * 2^-23 * |1/d| per
-// axis, against a culling-box inflation of e >= 1e-3 (x |1/d| in t), so it stays conservative
-// while |o| * 2^-23 < e: the host enables it (InwScene::fused) only when every ray origin (the
-// camera, the scene's boxes) lies within 1000 of the origin.  INW only: its wide walk runs with
-// finite reciprocals (an infinite one would make every plane's fma NaN).
-__device__ __forceinline__ void cull4f(const float4 lx, const float4 ly, const float4 lz, const float4 hx,
-                                       const float4 hy, const float4 hz, f3 id, f3 noid, float lim, float &t0,
-                                       float &t1, float &t2, float &t3) {
-    const pf2 ix = pk(id.x, id.x), iy = pk(id.y, id.y), iz = pk(id.z, id.z);
-    const pf2 nx = pk(noid.x, noid.x), ny = pk(noid.y, noid.y), nz = pk(noid.z, noid.z);
-    const pf2 ax01 = __builtin_elementwise_fma(pk(lx.x, lx.y), ix, nx), bx01 = __builtin_elementwise_fma(pk(hx.x, hx.y), ix, nx);
-    const pf2 ay01 = __builtin_elementwise_fma(pk(ly.x, ly.y), iy, ny), by01 = __builtin_elementwise_fma(pk(hy.x, hy.y), iy, ny);
-    const pf2 az01 = __builtin_elementwise_fma(pk(lz.x, lz.y), iz, nz), bz01 = __builtin_elementwise_fma(pk(hz.x, hz.y), iz, nz);
-    const pf2 ax23 = __builtin_elementwise_fma(pk(lx.z, lx.w), ix, nx), bx23 = __builtin_elementwise_fma(pk(hx.z, hx.w), ix, nx);
-    const pf2 ay23 = __builtin_elementwise_fma(pk(ly.z, ly.w), iy, ny), by23 = __builtin_elementwise_fma(pk(hy.z, hy.w), iy, ny);
-    const pf2 az23 = __builtin_elementwise_fma(pk(lz.z, lz.w), iz, nz), bz23 = __builtin_elementwise_fma(pk(hz.z, hz.w), iz, nz);
     auto one = [&](float x0, float x1, float y0, float y1, float z0, float z1) {
         const float te = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
         const float tx = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
@@ -1817,18 +1791,85 @@ __device__ float inw_surrounding_ri(const InwScene &S, FStack &K, f3 hp, float r
 // (measured in DESIGN.md §5): kernels instantiated with LN copy the first n_lnodes wide
 // nodes -- the top levels, as bvh4_collapse numbers them breadth first -- into LDS and read them
 // there; deeper nodes come from global memory.
-constexpr int kInwLdsNodes = 320;  // 40 KB: what 3 x 256-lane stacks (120 KB) leave of 160 KB
-__shared__ float4 g_inw_lnodes[kInwLdsNodes * 8];
+// INW wide node: 10 float4, SoA over the 4 children: planes lx ly lz hx hy hz, then lx ly lz again,
+// then the child links.  The repeat lets a ray read its near and far planes of axis a at
+// a + 3*s_a and a + 3 + 3*s_a (s_a = 1 when d_a < 0): one per-lane offset per axis (inw_wnode_nf).
+constexpr int kInwNodeF4 = 10;
+constexpr int kInwLdsNodes = 256;  // 40 KB: what 3 x 256-lane stacks (120 KB) leave of 160 KB
+__shared__ float4 g_inw_lnodes[kInwLdsNodes * kInwNodeF4];
+template <bool LN>
+__device__ __forceinline__ const float4 *inw_node_ptr(const InwScene &S, int cur) {
+    if (LN && (uint32_t)(cur - 1) < S.n_lnodes) return g_inw_lnodes + kInwNodeF4 * (cur - 1);
+    return S.wnodes + kInwNodeF4 * (cur - 1);
+}
 template <bool LN>
 __device__ __forceinline__ void inw_wnode(const InwScene &S, int cur, float4 &lx, float4 &ly, float4 &lz, float4 &hx,
                                           float4 &hy, float4 &hz, float4 &lk) {
-    if (LN && (uint32_t)(cur - 1) < S.n_lnodes) {
-        const float4 *nd = g_inw_lnodes + 8 * (cur - 1);
-        lx = nd[0]; ly = nd[1]; lz = nd[2]; hx = nd[3]; hy = nd[4]; hz = nd[5]; lk = nd[6];
-    } else {
-        const float4 *nd = S.wnodes + 8 * (cur - 1);
-        lx = nd[0]; ly = nd[1]; lz = nd[2]; hx = nd[3]; hy = nd[4]; hz = nd[5]; lk = nd[6];
+    const float4 *nd = inw_node_ptr<LN>(S, cur);
+    lx = nd[0]; ly = nd[1]; lz = nd[2]; hx = nd[3]; hy = nd[4]; hz = nd[5]; lk = nd[9];
+}
+// The near and far planes of the four children for this ray's octant (oa = a + 3*s_a).
+template <bool LN>
+__device__ __forceinline__ void inw_wnode_nf(const InwScene &S, int cur, uint32_t ox, uint32_t oy, uint32_t oz,
+                                             float4 &nx, float4 &ny, float4 &nz, float4 &fx, float4 &fy, float4 &fz,
+                                             float4 &lk) {
+#ifndef RT_INW_FLAT
+    if (LN && (uint32_t)(cur - 1) < S.n_lnodes) {  // ds_read_b128 (a generic pointer would make flat loads)
+        const float4 *nd = g_inw_lnodes + kInwNodeF4 * (cur - 1);
+        const float4 *px = nd + ox, *py = nd + oy, *pz = nd + oz;
+        nx = px[0]; fx = px[3]; ny = py[0]; fy = py[3]; nz = pz[0]; fz = pz[3]; lk = nd[9];
+        return;
     }
+    const float4 *nd = S.wnodes + kInwNodeF4 * (cur - 1);
+#else
+    const float4 *nd = inw_node_ptr<LN>(S, cur);
+#endif
+    const float4 *px = nd + ox, *py = nd + oy, *pz = nd + oz;
+    nx = px[0]; fx = px[3]; ny = py[0]; fy = py[3]; nz = pz[0]; fz = pz[3]; lk = nd[9];
+}
+// FU: one fused multiply-add per plane, plane * (1/d) + (-o * (1/d)), the second term computed
+// once per ray (noid).  Its rounding error in t is at most |o| * 2^-23 * |1/d| per axis, against a
+// culling-box inflation of e >= 1e-3 (x |1/d| in t), so it stays conservative while
+// |o| * 2^-23 < e: the host enables it (InwScene::fused) only when every ray origin (the camera,
+// the scene's boxes) lies within 1000 of the origin.  The wide walk runs with finite reciprocals
+// only (an infinite one would make every plane's fma NaN).
+// The culling test with the planes already split into near and far by the ray's octant.  With a
+// finite, nonzero reciprocal, the slab value of a plane is monotone in the plane (each step is a
+// correctly rounded monotone function), so the near plane's value is the min of the pair and the
+// far plane's the max: the same te and tx bits as min / max of the pair, without the 6 min/max per child.
+// The test te <= tx && tx >= -1e-3 && te <= lim is max(te, -1e-3) <= min(tx, lim) (lim > 0).
+template <bool FU>
+__device__ __forceinline__ void cull4nf(const float4 nx, const float4 ny, const float4 nz, const float4 fx,
+                                        const float4 fy, const float4 fz, f3 o, f3 id, f3 noid, float lim, float &t0,
+                                        float &t1, float &t2, float &t3) {
+    const pf2 ix = pk(id.x, id.x), iy = pk(id.y, id.y), iz = pk(id.z, id.z);
+    pf2 a[12];
+    const float4 *pl[6] = {&nx, &ny, &nz, &fx, &fy, &fz};
+    const pf2 iv[3] = {ix, iy, iz};
+    if constexpr (FU) {
+        const pf2 nv[3] = {pk(noid.x, noid.x), pk(noid.y, noid.y), pk(noid.z, noid.z)};
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            a[2 * k] = __builtin_elementwise_fma(pk(pl[k]->x, pl[k]->y), iv[k % 3], nv[k % 3]);
+            a[2 * k + 1] = __builtin_elementwise_fma(pk(pl[k]->z, pl[k]->w), iv[k % 3], nv[k % 3]);
+        }
+    } else {
+        const pf2 ov[3] = {pk(o.x, o.x), pk(o.y, o.y), pk(o.z, o.z)};
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            a[2 * k] = (pk(pl[k]->x, pl[k]->y) - ov[k % 3]) * iv[k % 3];
+            a[2 * k + 1] = (pk(pl[k]->z, pl[k]->w) - ov[k % 3]) * iv[k % 3];
+        }
+    }
+    // a[2k + h]: plane k (near x, y, z, far x, y, z) of children 2h, 2h + 1
+    auto one = [&](float n0, float n1, float n2, float f0, float f1, float f2) {
+        const float te = fmaxf(fmaxf(n0, n1), n2), tx = fminf(fminf(f0, f1), f2);
+        return fmaxf(te, -1e-3f) <= fminf(tx, lim) ? te : kMiss;
+    };
+    t0 = one(a[0].x, a[2].x, a[4].x, a[6].x, a[8].x, a[10].x);
+    t1 = one(a[0].y, a[2].y, a[4].y, a[6].y, a[8].y, a[10].y);
+    t2 = one(a[1].x, a[3].x, a[5].x, a[7].x, a[9].x, a[11].x);
+    t3 = one(a[1].y, a[3].y, a[5].y, a[7].y, a[9].y, a[11].y);
 }
 
 // ---------------------------------------------------------------- INW wide walk
@@ -1861,8 +1902,9 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
     uint32_t br = 0xffffffffu;
     const uint32_t *rank = S.rank + (invert ? S.n : 0u);
     const f3 fid = f3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
-    const f3 noid = f3{-(o.x * fid.x), -(o.y * fid.y), -(o.z * fid.z)};  // cull4f's per-ray term (FU)
+    const f3 noid = f3{-(o.x * fid.x), -(o.y * fid.y), -(o.z * fid.z)};  // the fused cull's per-ray term (FU)
     const int base = (int)K.size, cap = kFStack - 3 - base;  // 3 spare slots for branch-free pushes
+    const uint32_t ox = d.x < 0.0f ? 3u : 0u, oy = d.y < 0.0f ? 4u : 1u, oz = d.z < 0.0f ? 5u : 2u;
     int sp = 0, pend = -1, cur = S.wroot;
     bool walking = ok, ovf = false;
     float lim = bt * 1.0001f + 1e-3f;
@@ -1887,12 +1929,11 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
         if (walking) {
             bool pop;
             if (cur > 0) {
-                float4 lx, ly, lz, hx, hy, hz, lk;
-                inw_wnode<LN>(S, cur, lx, ly, lz, hx, hy, hz, lk);
+                float4 nx, ny, nz, fx, fy, fz, lk;
+                inw_wnode_nf<LN>(S, cur, ox, oy, oz, nx, ny, nz, fx, fy, fz, lk);
                 c.nodes += 4;
                 float t0, t1, t2, t3;
-                if constexpr (FU) cull4f(lx, ly, lz, hx, hy, hz, fid, noid, lim, t0, t1, t2, t3);
-                else cull4(lx, ly, lz, hx, hy, hz, o, fid, lim, t0, t1, t2, t3);
+                cull4nf<FU>(nx, ny, nz, fx, fy, fz, o, fid, noid, lim, t0, t1, t2, t3);
                 int k0 = __float_as_int(lk.x), k1 = __float_as_int(lk.y), k2 = __float_as_int(lk.z),
                     k3 = __float_as_int(lk.w);
                 cswap(t0, k0, t1, k1); cswap(t2, k2, t3, k3);
@@ -2498,7 +2539,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     InwScene S = S0;
     if constexpr (LN) {
         const uint32_t n = S.wnodes ? (S.n_wnodes < (uint32_t)kInwLdsNodes ? S.n_wnodes : (uint32_t)kInwLdsNodes) : 0u;
-        for (uint32_t i = threadIdx.x; i < n * 8u; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
+        for (uint32_t i = threadIdx.x; i < n * (uint32_t)kInwNodeF4; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
         __syncthreads();
         S.n_lnodes = n;
     }
@@ -2664,7 +2705,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     InwScene S = S0;
     if constexpr (LN) {
         const uint32_t n = S.wnodes ? (S.n_wnodes < (uint32_t)kInwLdsNodes ? S.n_wnodes : (uint32_t)kInwLdsNodes) : 0u;
-        for (uint32_t i = threadIdx.x; i < n * 8u; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
+        for (uint32_t i = threadIdx.x; i < n * (uint32_t)kInwNodeF4; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
         __syncthreads();
         S.n_lnodes = n;
     }

@@ -79,7 +79,7 @@ struct InwScene {
     uint32_t dfs_high = 0;
     uint32_t n_wnodes = 0;  // wide nodes
     uint32_t n_lnodes = 0;  // the first n_lnodes wide nodes are staged in LDS (LN kernels only)
-    int fused = 0;          // the wide walk culls with one fma per plane (cull4f; set per frame)
+    int fused = 0;          // the wide walk culls with one fma per plane (cull4nf<true>; set per frame)
 };
 
 // One launch of a chunked render: samples [s_begin, s_end) of every pixel unit.  A pixel's
