@@ -413,6 +413,24 @@ def main():
                             "source": prof_src + " (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU)"}
             except Exception:  # noqa: BLE001
                 traffic, valu, lane_issue, prof_src = None, None, None, None
+        # the same roofline over the reference's own walk: F_alg with the node visits and object
+        # tests of the reference's LBVH walk of this frame (RT_INW_FAST=0, the oracle's counts;
+        # profiles/refwalk_<cfg>.json), a fixed amount of work per frame whatever walk runs
+        ref_walk = None
+        rw = os.path.join(ROOT, "profiles", f"refwalk_{cfg}.json")
+        if inw and world == 1 and os.path.exists(rw):
+            try:
+                rj = json.load(open(rw))
+                rc = rj["counters_per_step"]
+                if ([rj["config"]["width"], rj["config"]["height"], rj["config"]["spp"]] == [W, H, spp]
+                        and rc["segments"] == int(per_step["segments"])):
+                    fr = algorithmic_flops(rc) / launches
+                    ref_walk = {"flops_per_launch": fr, "achieved": round(fr / avg_s / 1e12, 3),
+                                "frac": round(fr / avg_s / 1e12 / FP32_PEAK_TFLOPS, 4),
+                                "node_visits": rc["node_visits"], "prim_tests": rc["prim_tests"],
+                                "source": "profiles/" + os.path.basename(rw)}
+            except Exception:  # noqa: BLE001
+                ref_walk = None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cores = args.cpu_threads or host_cores()
@@ -446,10 +464,12 @@ def main():
                          "render_ms_per_frame": round(kernel_ms, 3),
                          "flops_per_launch": flops / launches,
                          "source": prof_src,
+                         "ref_walk": ref_walk,
                          "note": "fp32 VALU kernel (no MFMA on this path); peak = FP32 vector peak; "
                                  "achieved = SURVEY 8d F_alg per launch / average launch time (HIP events "
                                  "on the launch stream); F_alg counts this build's own node visits and object "
-                                 "tests (4-wide culling walk), so it shrinks as the walk improves; "
+                                 "tests (4-wide culling walk, pixel beams), so it shrinks as the walk improves; "
+                                 "ref_walk = the same with the reference LBVH walk's counts of this frame; "
                                  "lane_issue_frac = VALU busy x lane utilisation (PMC); traffic = PMC HBM "
                                  "bytes per launch"},
             "valu": valu,

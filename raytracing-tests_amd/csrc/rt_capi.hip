@@ -152,6 +152,8 @@ struct rt_dev_scene {
     DevBuf inw_ring;             // k_inw_pm / k_inw_sm: the waves' fold rings
     DevBuf inw_mode;             // k_inw_probe's verdict (2 uints)
     DevBuf inw_cost;             // claim order: block cost keys, the order, 256 bucket offsets
+    DevBuf inw_beam, inw_beam_n;  // pixel beams: beam_cap (id, entry t) per unit; count + cut per unit
+    float sf_max = 0.0f;          // largest |x| + |y| of the sunflower lens table
     DevBuf sp_dbg_t;             // RT_DEBUG_TIMES diagnostics: per unit start / end launch
     size_t sp_dbg_n = 0;         // units (P * S) of the render that last wrote sp_dbg_t
     uint32_t launch_seq = 0;
@@ -195,6 +197,9 @@ int build_tables(rt_dev_scene *s, int spp) {
     for (int i = 0; i < spp; i++)
         for (int k = 0; k < 3; k++) fib4[size_t(i) * 4 + k] = fib3[size_t(i) * 3 + k];
     HIP_OK(s->sunflower.upload(sf.data(), sf.size() * sizeof(float)));
+    s->sf_max = 0.0f;
+    for (int i = 0; i < spp; i++)
+        s->sf_max = std::fmax(s->sf_max, std::fabs(sf[size_t(i) * 2]) + std::fabs(sf[size_t(i) * 2 + 1]));
     HIP_OK(s->fib.upload(fib4.data(), fib4.size() * sizeof(float)));
     HIP_OK(s->ring.upload(ring.data(), ring.size() * sizeof(int)));
     s->spp = spp;
@@ -997,6 +1002,52 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     return RT_OK;
 }
 
+// Pixel beams (DESIGN.md §5 "Pixel beams"; RT_INW_BEAM=0 turns them off).  Sample s of a pixel
+// starts its primary ray one unit behind tip = C0 + rr * ox + ru * oy (C0 = co + cd, |rr|, |ru|
+// <= 1, |ox| + |oy| <= aperture / 2 * sf_max) and aims it at F = co + cd * focus.  With
+// L = |F - C0| = focus - 1, the point of that ray at fraction u of the way from tip to F is
+// within delta0 * |1 - u| of the point C0 + u * L * cd of the central ray, so over the central
+// parameter range [tmin, tfar] that covers the scene, every primary ray lies within
+// R = delta0 * max |1 - t / L| (+ rounding slack) of the central ray.  A sample ray's hit at t
+// has central parameter <= t * kappa, kappa = L / (L - delta0).
+int set_beam(rt_dev_scene *s, const rtk::Frame &f, rtk::InwScene &sc) {
+    const uint32_t cap = 32;
+    const double units = double(rtk::units_of(f));
+    const double ap = std::fabs(double(f.aperture)), L = double(f.focus) - 1.0;
+    const double d0 = 0.5 * ap * double(s->sf_max) * (1.0 + 1e-4) + 1e-6;
+    if (env_int("RT_INW_BEAM", 1) == 0 || !sc.wnodes || f.n_focus > 0 || !(L > 8.0 * d0 + 1e-3) ||
+        units * cap * 8.0 > 2.0e9)
+        return RT_OK;
+    const double cam = std::sqrt(double(f.pos[0]) * f.pos[0] + double(f.pos[1]) * f.pos[1] + double(f.pos[2]) * f.pos[2]);
+    const double Lh = L + 1e-3 * (1.0 + cam), Ll = L - 1e-3 * (1.0 + cam);
+    if (!(Ll > 4.0 * d0)) return RT_OK;
+    // every point of a culling box lies within sqrt(3) * wbound of the origin
+    const double tfar = (cam + 1.0 + std::sqrt(3.0) * double(s->wbound) + 2.0) / (1.0 - d0 / Ll) * 1.001;
+    const double tmin = -Lh / (Ll - d0) - 0.01;
+    const double r = d0 * std::fmax(1.0 - tmin / Ll, std::fabs(1.0 - tfar / Ll));
+    const double R = r + 2e-3 + 1e-5 * (cam + tfar);
+    const size_t need = size_t(units) * cap * sizeof(uint2), need_n = size_t(units) * 2 * sizeof(uint32_t);
+    if (s->inw_beam.bytes < need) {
+        s->inw_beam.~DevBuf();
+        new (&s->inw_beam) DevBuf();
+        if (s->inw_beam.alloc(need) != hipSuccess) return RT_E_HIP;
+    }
+    if (s->inw_beam_n.bytes < need_n) {
+        s->inw_beam_n.~DevBuf();
+        new (&s->inw_beam_n) DevBuf();
+        if (s->inw_beam_n.alloc(need_n) != hipSuccess) return RT_E_HIP;
+    }
+    sc.beam = s->inw_beam.as<uint2>();
+    sc.beam_n = s->inw_beam_n.as<uint32_t>();
+    sc.beam_cut = reinterpret_cast<const float *>(s->inw_beam_n.as<uint32_t>() + size_t(units));
+    sc.beam_cap = cap;
+    sc.beam_R = float(R);
+    sc.beam_tmin = float(tmin);
+    sc.beam_tfar = float(tfar);
+    sc.beam_kappa = float(Lh / (Ll - d0) * (1.0 + 1e-5));
+    return RT_OK;
+}
+
 // INW with on-chip End() folds (DESIGN.md §5 "INW: on-chip End() folds"): the probe, then
 // k_inw_pm and k_inw_sm (one of them exits at once), persistent launches of one frame.  The
 // launches are bracketed by HIP events on their stream when kernel timing is on
@@ -1063,6 +1114,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         }
         cost = s->inw_cost.as<uint32_t>();
     }
+    if (int rc = set_beam(s, f, sc); rc != RT_OK) return rc;
     e = hipMemsetAsync(s->inw_ring.p, 0xff, ring_bytes, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->first, st);
     if (e == hipSuccess)

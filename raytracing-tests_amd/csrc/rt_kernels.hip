@@ -1980,6 +1980,81 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
     return (float)bg;
 }
 
+// Closest hit of a primary ray from its pixel's beam list (DESIGN.md §5 "Pixel beams").  The list
+// holds every object whose culling box the beam of the pixel's primary rays can cross, in the
+// order of the central ray's entry t into the box inflated by beam_R; a sample ray hitting object
+// j at t has entry(j) <= t * beam_kappa, so the candidates past bt * kappa (+ slack) cannot win.
+// Each candidate gets the wide walk's leaf test (the reference's leaf box with the initial limit,
+// the exact test, the leaf-entry guard, the (t, depth-first rank) rule), so the winner is the
+// wide walk's and the reference walk's.  ok = false: the list does not decide this ray (no list,
+// the wide walk's conditions fail, or candidates beyond the stored ones could still win).
+template <bool WANT_NORMAL>
+__device__ float inw_closest_beam(const InwScene &S, const FStack &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
+                                  f3 &normal, float &extra, float init_geom, Ctr &c, uint32_t unit, bool &ok,
+                                  float &blim) {
+    const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};  // the reference's reciprocals (test_aabb)
+    const uint32_t n = S.beam_n[unit];
+    ok = n != kBeamOff && K.size + S.dfs_high <= (uint32_t)kFStack && __builtin_isfinite(id.x) &&
+         __builtin_isfinite(id.y) && __builtin_isfinite(id.z) && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
+    const float tlim0 = tlim;
+    float bt = tlim0;
+    int bg = -1;
+    uint32_t br = 0xffffffffu;
+    const uint32_t *rank = S.rank + (invert ? S.n : 0u);
+    const uint2 *list = S.beam + (size_t)unit * S.beam_cap;
+    const float kap = S.beam_kappa;
+    float lim = bt * kap + 0.01f;
+    bool ovf = false;
+    uint32_t k = 0;
+    for (;;) {
+        bool act = ok && k < n;
+        uint2 e = make_uint2(0u, 0u);
+        if (act) {
+            e = list[k];
+            act = __uint_as_float(e.y) <= lim;
+        }
+        if (!__any(act)) break;
+        if (act) {
+            const int g = (int)e.x;
+            c.prims++;
+            const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
+            const Xf x = load_xf(S, g);
+            float te;
+            if (test_aabb_te(n0, n1, o, id, tlim0, te)) {
+                f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+                f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+                float t = -1.0f;
+                if (x.type == 1) t = t_ellipsoid(to, td, x.is);
+                else if (x.type == 2) t = t_cuboid(to, td, x.scale);
+                if (t > 0.0f && t < tlim0) {
+                    if (t < te) ovf = true;  // the leaf-entry guard (inw_traverse_wide)
+                    const uint32_t r = rank[g];
+                    if (t < bt || (t == bt && r < br)) { bt = t; bg = g; br = r; lim = bt * kap * 1.00001f + 0.01f; }
+                }
+            }
+            k++;
+        }
+    }
+    // candidates not stored (entry >= cut) could still be reached below lim
+    if (ok && (ovf || !(lim < S.beam_cut[unit]))) ok = false;
+    blim = lim;
+    if (!ok) return init_geom;
+    if (bg < 0) return init_geom;
+    tlim = bt;
+    if (WANT_NORMAL) {
+        const Xf x = load_xf(S, bg);
+        f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+        f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+        f3 h = to + td * bt, nl;
+        if (x.type == 1) nl = normalize(f3{h.x * x.is2.x, h.y * x.is2.y, h.z * x.is2.z});
+        else if (x.type == 2) nl = cuboid_normal(h, x.scale);
+        else nl = f3{0, 0, 0};
+        normal = mul(x.R, nl);
+        extra = x.extra;
+    }
+    return (float)bg;
+}
+
 // The surrounding-RI walk (01_BVH...glsl:486-502) sums the RI of every object holding the point,
 // in its depth-first order (right child first).  Same conditions as above: the objects are those
 // whose leaf box holds the point (inclusive, as the reference compares) and whose inside test
@@ -2049,6 +2124,51 @@ __device__ float inw_surrounding_ri_wide(const InwScene &S, FStack &K, f3 hp, fl
     return acc;
 }
 
+// The surrounding-RI walk (inw_surrounding_ri_wide) for the hit of a primary ray decided by its
+// beam list: the query point lies within 0.0011 of the hit, so an object holding it has its
+// culling box within beam_R of the central ray before the hit's bound blim, and it is listed.
+__device__ float inw_ri_beam(const InwScene &S, f3 hp, float ratio, Ctr &c, uint32_t unit, float blim, bool &ok) {
+    const uint32_t n = S.beam_n[unit];
+    const uint2 *list = S.beam + (size_t)unit * S.beam_cap;
+    uint32_t rk[kRiMax];
+    float rv[kRiMax];
+    int nin = 0;
+    ok = true;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint2 e = list[k];
+        if (!(__uint_as_float(e.y) <= blim)) break;
+        const int g = (int)e.x;
+        c.prims++;
+        const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
+        const Xf x = load_xf(S, g);
+        if (hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z) {
+            f3 v = (hp - x.pos) + x.delta * (1.0f - ratio);
+            v = tmul(x.R, v);
+            v.x *= x.is.x; v.y *= x.is.y; v.z *= x.is.z;
+            bool inside;
+            if (x.type == 1) inside = dot(v, v) <= 1.0f;
+            else if (x.type == 2) inside = fabsf(v.x) <= 0.5f && fabsf(v.y) <= 0.5f && fabsf(v.z) <= 0.5f;
+            else inside = false;
+            if (inside) {
+                if (nin == kRiMax) { ok = false; return 1.0f; }
+                rk[nin] = S.rank[g];
+                rv[nin] = x.ri_acc;
+                nin++;
+            }
+        }
+    }
+    for (int i = 1; i < nin; i++)
+        for (int j = i; j > 0 && rk[j] < rk[j - 1]; j--) {
+            const uint32_t tr = rk[j]; rk[j] = rk[j - 1]; rk[j - 1] = tr;
+            const float tv = rv[j]; rv[j] = rv[j - 1]; rv[j - 1] = tv;
+        }
+    float acc = 0.0f;
+    for (int i = 0; i < nin; i++) acc += rv[i];
+    if (acc > 1.0f) acc *= rcp((float)nin);
+    else acc = 1.0f;
+    return acc;
+}
+
 template <bool WANT_NORMAL, bool LN = false, bool FU = false>
 __device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
                                              float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c) {
@@ -2082,9 +2202,8 @@ __device__ __forceinline__ f3 deviate(const InwScene &S, f3 dir, float tan_theta
 }
 
 // Camera ray of sample s (out_Pixel prologue, 01_BVH...glsl:366-410): push it, reset the sample.
-__device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame &F, FStack &K, int px, int py, int s,
-                                                 Ctr &c) {
-    K.size = 0;
+// the pixel's camera direction (01_BVH...glsl:366-386)
+__device__ __forceinline__ f3 inw_pixel_dir(const Frame &F, int px, int py) {
     const f3 D = mk(F.dir[0], F.dir[1], F.dir[2]);
     float aspect = (float)F.W * rcp((float)F.H);
     float srx = (float)px * rcp((float)F.W) - 0.5f;
@@ -2092,8 +2211,14 @@ __device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame 
     srx *= aspect;
     const f3 up = f3{0, 1, 0};
     f3 cr = cross(D, up), cu = cross(cr, D);
+    return normalize((D * F.screen_dist + cr * srx) + cu * sry);
+}
+__device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame &F, FStack &K, int px, int py, int s,
+                                                 Ctr &c) {
+    K.size = 0;
+    const f3 up = f3{0, 1, 0};
     f3 co = mk(F.pos[0], F.pos[1], F.pos[2]);
-    f3 cd = normalize((D * F.screen_dist + cr * srx) + cu * sry);
+    f3 cd = inw_pixel_dir(F, px, py);
     float ox = S.sunflower[2 * s] * (F.aperture * 0.5f), oy = S.sunflower[2 * s + 1] * (F.aperture * 0.5f);
     f3 rr = cross(cd, up), ru = cross(rr, cd);
     if (F.n_focus > 0) {  // MULTIFOCUS lens record (01_BVH...glsl:388-400): stack floats 0..5
@@ -2157,8 +2282,10 @@ __device__ f3 inw_tex_color(const InwScene &S, uint32_t k, f3 lp) {
 
 // One iteration of out_Pixel's ray loop (01_BVH...glsl:414-597 / 04...glsl:510-713):
 // pop a ray, closest hit, surrounding RI, shadow rays, push reflect/refract, accumulate.
+// bunit: the lane's pixel unit when its primary ray may use the pixel's beam list (k_inw_pm), else kBeamOff
 template <bool LIGHTS, bool LN = false, bool FU = false>
-__device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s, f3 &color, float &depth, Ctr &c) {
+__device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s, f3 &color, float &depth, Ctr &c,
+                            uint32_t bunit = kBeamOff) {
     const f3 D = mk(F.dir[0], F.dir[1], F.dir[2]);
     const float ratio = (float)s * F.inv_spp;
     const bool invert = dot(D, f3{1, 1, 1}) > 0.0f;
@@ -2174,7 +2301,13 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         float tlim = tlim0, extra = 0.0f;
         f3 normal = f3{0, 0, 0};
         INW_T0(t_ch);
-        float fg = inw_closest<true, LN, FU>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
+        float fg, blim = 0.0f;
+        bool beam_ok = false;
+        if (bunit != kBeamOff && (int)(bounced + 0.1f) == 0 && !mf0)  // a primary ray (pushed rays have bounced >= 1)
+            fg = inw_closest_beam<true>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c, bunit,
+                                        beam_ok, blim);
+        if (!beam_ok)
+            fg = inw_closest<true, LN, FU>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
         INW_CYC(c, 0, t_ch);
         const f3 hitpoint = co + cd * tlim;
         if (!(tlim < tlim0)) {
@@ -2222,7 +2355,9 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         if (!LIGHTS && (ri_forced || (ri_read && contribution > 0.01f && bounced + 1.0f < (float)F.max_bounces)))
         {
             INW_T0(t_ri);
-            surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
+            bool rok = false;
+            if (beam_ok && !ri_forced) surr = inw_ri_beam(S, hitpoint + normal * 0.001f, ratio, c, bunit, blim, rok);
+            if (!rok) surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
             INW_CYC(c, 1, t_ri);
         }
         if (mf0) K.size = 0;  // 01_BVH...glsl:544-549: the lens record goes after a primary hit
@@ -2242,8 +2377,11 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
                 }
                 const uint32_t nl = S.n_lights > 1 ? S.n_lights : 1u;
                 contribution *= (float)is_lit * rcp((float)nl);
-                if (ri_forced || (ri_read && contribution > 0.01f && bounced < (float)F.max_bounces))
-                    surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
+                if (ri_forced || (ri_read && contribution > 0.01f && bounced < (float)F.max_bounces)) {
+                    bool rok = false;
+                    if (beam_ok && !ri_forced) surr = inw_ri_beam(S, hitpoint + normal * 0.001f, ratio, c, bunit, blim, rok);
+                    if (!rok) surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
+                }
             } else {
                 if (ri_forced) (void)inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
                 color = f3{1, 1, 1};
@@ -2421,6 +2559,85 @@ __device__ __forceinline__ bool inw_sample_major(const uint32_t *mode, uint32_t 
     const uint32_t hit = uni(mode[0]), same = uni(mode[1]);
     return 2u * same >= hit && hit > 0u;
 }
+// Pixel beams (DESIGN.md §5 "Pixel beams").  A pixel's primary rays all pass through its focal
+// point F = co + cd * focus and leave the lens disk around C0 = co + cd (radius <= delta0), so they
+// lie within beam_R of the central ray C0 + t * cd over t in [beam_tmin, beam_tfar] (host bounds).
+// One lane per pixel unit walks the culling BVH with that ray against the boxes inflated by
+// beam_R and keeps the beam_cap leaves of smallest entry t, sorted; beam_cut is the smallest
+// entry t of a leaf it could not keep.
+constexpr int kBeamBlock = 128, kBeamStack = 48, kBeamCapMax = 32;
+__global__ __launch_bounds__(kBeamBlock) void k_inw_beam(Frame f, InwScene S, const uint32_t *mode, uint32_t force) {
+    if (inw_sample_major(mode, force)) return;
+    __shared__ int st[kBeamStack * kBeamBlock];
+    __shared__ uint2 lst[kBeamCapMax * kBeamBlock];
+    const uint32_t u = blockIdx.x * kBeamBlock + threadIdx.x;
+    if (u >= units_total(f)) return;
+    const UnitPix px = unit_pixel(f, u);
+    uint32_t *nout = const_cast<uint32_t *>(S.beam_n);
+    float *cout = const_cast<float *>(S.beam_cut);
+    if (!px.in_image) { nout[u] = 0u; cout[u] = kMiss; return; }
+    const f3 cd = inw_pixel_dir(f, px.x, px.y);
+    const f3 o = mk(f.pos[0], f.pos[1], f.pos[2]) + cd;
+    const f3 id = f3{rcp(cd.x), rcp(cd.y), rcp(cd.z)};
+    if (!(__builtin_isfinite(id.x) && __builtin_isfinite(id.y) && __builtin_isfinite(id.z))) { nout[u] = kBeamOff; return; }
+    const float R = S.beam_R, t0 = S.beam_tmin, t1 = S.beam_tfar;
+    const uint32_t cap = S.beam_cap;
+    // near / far planes of each axis for this direction, inflated outward by R
+    const uint32_t ox = cd.x < 0.0f ? 3u : 0u, oy = cd.y < 0.0f ? 4u : 1u, oz = cd.z < 0.0f ? 5u : 2u;
+    const f3 rn = f3{cd.x < 0.0f ? R : -R, cd.y < 0.0f ? R : -R, cd.z < 0.0f ? R : -R};
+    int *stk = st + threadIdx.x;
+    uint2 *L = lst + threadIdx.x;
+    int sp = 0, cur = S.wroot;
+    uint32_t nl = 0;
+    float cut = kMiss;
+    bool bad = false;
+    for (;;) {
+        const float4 *nd = S.wnodes + kInwNodeF4 * (cur - 1);
+        const float4 nx = nd[ox], fx = nd[ox + 3], ny = nd[oy], fy = nd[oy + 3], nz = nd[oz], fz = nd[oz + 3];
+        const float4 lk = nd[9];
+        const float nxa[4] = {nx.x, nx.y, nx.z, nx.w}, fxa[4] = {fx.x, fx.y, fx.z, fx.w};
+        const float nya[4] = {ny.x, ny.y, ny.z, ny.w}, fya[4] = {fy.x, fy.y, fy.z, fy.w};
+        const float nza[4] = {nz.x, nz.y, nz.z, nz.w}, fza[4] = {fz.x, fz.y, fz.z, fz.w};
+        const int lka[4] = {__float_as_int(lk.x), __float_as_int(lk.y), __float_as_int(lk.z), __float_as_int(lk.w)};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const float te = fmaxf(fmaxf(((nxa[k] + rn.x) - o.x) * id.x, ((nya[k] + rn.y) - o.y) * id.y),
+                                   ((nza[k] + rn.z) - o.z) * id.z);
+            const float tx = fminf(fminf(((fxa[k] - rn.x) - o.x) * id.x, ((fya[k] - rn.y) - o.y) * id.y),
+                                   ((fza[k] - rn.z) - o.z) * id.z);
+            if (!(fmaxf(te, t0) <= fminf(tx, t1))) continue;
+            const int l = lka[k];
+            if (l > 0) {
+                if (sp == kBeamStack) bad = true;
+                else stk[(sp++) * kBeamBlock] = l;
+            } else {  // keep the cap smallest entries, sorted (insertion)
+                float tv = te;
+                uint32_t gv = (uint32_t)(-l);
+                if (nl == cap) {
+                    const float last = __uint_as_float(L[(cap - 1) * kBeamBlock].y);
+                    if (!(tv < last)) { cut = fminf(cut, tv); continue; }
+                    cut = fminf(cut, last);
+                    nl--;
+                }
+                uint32_t j = nl;
+                while (j > 0 && __uint_as_float(L[(j - 1) * kBeamBlock].y) > tv) {
+                    L[j * kBeamBlock] = L[(j - 1) * kBeamBlock];
+                    j--;
+                }
+                L[j * kBeamBlock] = make_uint2(gv, __float_as_uint(tv));
+                nl++;
+            }
+        }
+        if (bad || sp == 0) break;
+        cur = stk[(--sp) * kBeamBlock];
+    }
+    if (bad) { nout[u] = kBeamOff; return; }
+    uint2 *dst = const_cast<uint2 *>(S.beam) + (size_t)u * cap;
+    for (uint32_t j = 0; j < nl; j++) dst[j] = L[j * kBeamBlock];
+    nout[u] = nl;
+    cout[u] = cut;
+}
+
 template <bool LIGHTS>
 __global__ __launch_bounds__(kBlock) void k_inw_probe(Frame f, InwScene S, uint32_t stride, uint32_t *mode) {
     __shared__ float lds[kFStack * kBlock];
@@ -2566,6 +2783,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     uint32_t g = 0;
     int s = 0;
     UnitPix px{};
+    uint32_t bu = kBeamOff;  // the lane's pixel unit for its beam list (S.beam)
     f3 col = f3{0, 0, 0};
     float dep = 0.0f;
     K.size = 0;
@@ -2583,10 +2801,15 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             }
             const unsigned long long m = __ballot(fin);
             const uint32_t n = ~m == 0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
-            for (uint32_t i = 0; i < n; i++) {
-                const f3 gv = f3{rdl(v.x, i), rdl(v.y, i), rdl(v.z, i)};
-                acc = sf == 0 ? gv : acc + gv;
-                if (++sf == spp) {  // pixel jf complete: End()'s imageStore (01_BVH...glsl:652)
+            // the run splits at pixel ends: per pixel, its entries are added with no test between them
+            for (uint32_t i = 0; i < n;) {
+                const uint32_t e = i + (n - i < spp - sf ? n - i : spp - sf);
+                uint32_t j = i;
+                if (sf == 0) { acc = f3{rdl(v.x, j), rdl(v.y, j), rdl(v.z, j)}; j++; }
+                for (; j < e; j++) acc = acc + f3{rdl(v.x, j), rdl(v.y, j), rdl(v.z, j)};
+                sf += e - i;
+                i = e;
+                if (sf == spp) {  // pixel jf complete: End()'s imageStore (01_BVH...glsl:652)
                     const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
                     if (lane == 0) {
                         const UnitPix p = unit_pixel(f, unit);
@@ -2647,6 +2870,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                     g = gi + rank;
                     s = (int)(adv - q * spp);
                     px = unit_pixel(f, unit);
+                    bu = S.beam ? unit : kBeamOff;
                     col = f3{0, 0, 0};
                     dep = 0.0f;
                     if (px.in_image) {
@@ -2667,7 +2891,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         if (qdone && ji == nclaimed && gf == gi && __ballot(busy) == 0) break;
         // ---- one ray segment per busy lane (samples are independent invocations)
         INW_T0(t_seg);
-        if (busy) inw_segment<LIGHTS, LN, FU>(S, f, K, s, col, dep, c);
+        if (busy) inw_segment<LIGHTS, LN, FU>(S, f, K, s, col, dep, c, bu);
         INW_CYC(c, 4, t_seg);
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
@@ -3102,6 +3326,11 @@ hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pa
     hipLaunchKernelGGL(k_iow03_resolve, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, f, R, final_pass ? 1 : 0, state);
     return hipGetLastError();
 }
+hipError_t launch_inw_beam(const Frame &f, const InwScene &sc, const uint32_t *mode, uint32_t force, hipStream_t s) {
+    const uint32_t n = units_of(f);
+    hipLaunchKernelGGL(k_inw_beam, dim3((n + kBeamBlock - 1) / kBeamBlock), dim3(kBeamBlock), 0, s, f, sc, mode, force);
+    return hipGetLastError();
+}
 // One frame of the on-chip-fold INW kernels: the probe (unless forced), then k_inw_pm and
 // k_inw_sm, of which the one the probe did not pick exits at once.  ring: blocks * 4 waves *
 // max(ring_pm, ring_sm) float4; mode: 2 uints (zeroed here).  force: 0 = probe, 1 = pm, 2 = sm.
@@ -3135,6 +3364,7 @@ hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uin
         else hipLaunchKernelGGL(k_inw_probe<false>, g, dim3(kBlock), 0, s, f, sc, stride, mode);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    if (sc.beam && (e = launch_inw_beam(f, sc, mode, force, s)) != hipSuccess) return e;
     for (int k = 0; k < 2; k++) {  // (pm, then sm) each with its own queue counter
         if ((e = hipMemsetAsync(counter + 16 * k, 0, sizeof(unsigned), s)) != hipSuccess) return e;
         const uint32_t rm = (k == 0 ? ring_pm : ring_sm) - 1u;

@@ -80,7 +80,17 @@ struct InwScene {
     uint32_t n_wnodes = 0;  // wide nodes
     uint32_t n_lnodes = 0;  // the first n_lnodes wide nodes are staged in LDS (LN kernels only)
     int fused = 0;          // the wide walk culls with one fma per plane (cull4nf<true>; set per frame)
+    // Pixel beams (DESIGN.md §5 "Pixel beams"; null beam = off): for each pixel unit, the objects
+    // whose culling box the beam of its primary rays can cross, sorted by the entry t of the
+    // central ray into the box inflated by beam_R (k_inw_beam).  beam_n[u] = count (kBeamOff: use
+    // the wide walk), beam_cut[u] = every object with an entry below it is listed.
+    const uint2 *beam = nullptr;  // beam_cap entries per unit: object id, entry t (float bits)
+    const uint32_t *beam_n = nullptr;
+    const float *beam_cut = nullptr;
+    uint32_t beam_cap = 0;
+    float beam_R = 0.0f, beam_tmin = 0.0f, beam_tfar = 0.0f, beam_kappa = 0.0f;
 };
+constexpr uint32_t kBeamOff = 0xffffffffu;
 
 // One launch of a chunked render: samples [s_begin, s_end) of every pixel unit.  A pixel's
 // samples must run in order (IOW-03 reads stale stack slots of earlier samples), so the
@@ -268,6 +278,8 @@ hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pa
 hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uint32_t ring_pm, uint32_t ring_sm,
                            unsigned *counter, uint32_t *mode, uint32_t force, int blocks, int blocks_ln,
                            uint32_t *cost, hipStream_t s);
+// the pixel beams of a pixel-major frame (sc.beam*; exits when the probe picks sample-major)
+hipError_t launch_inw_beam(const Frame &f, const InwScene &sc, const uint32_t *mode, uint32_t force, hipStream_t s);
 // resident blocks per CU of the render kernel for `kind` (3 = IOW-03 wide, 4 = IOW-03 narrow,
 // 11/14 = INW layout 1/4)
 int resident_blocks_per_cu(int kind);  // 5 = sample-parallel IOW-03, 6/7 = sample-parallel INW 1/4,
