@@ -130,6 +130,9 @@ struct rt_dev_scene {
     DevBuf obox;  // IOW-03: per-object culling boxes (2 float4 each) for wave-cooperative queries
     DevBuf tex, tex_info;  // INW-04 material textures (float4 texels, (first, w, h, 0) per texture)
     DevBuf wnodes, wrank, wleaf;  // INW wide walk: culling BVH, depth-first ranks, LBVH leaf boxes
+    DevBuf ri_cells, ri_ids;      // INW surrounding-RI grid (cell offsets, object ids)
+    float ri_lo[3] = {}, ri_hi[3] = {}, ri_inv[3] = {};
+    int ri_dim[3] = {};
     int wdepth = 0;               // levels of the 4-wide culling BVH
     bool last_ln = false;         // the last INW fold launch used the LDS-staged kernels
     bool last_fu = false;         // ... their fused-fma cull instances
@@ -332,6 +335,80 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     sc.leafbox = s->wleaf.as<float4>();
     sc.dfs_high = s->dfs_high;
     sc.n_wnodes = uint32_t(s->wnodes.bytes / (10 * sizeof(float4)));
+    if (s->ri_cells.p && !(std::getenv("RT_INW_RIGRID") && std::getenv("RT_INW_RIGRID")[0] == '0')) {
+        sc.ri_cells = s->ri_cells.as<uint32_t>();
+        sc.ri_ids = s->ri_ids.as<uint32_t>();
+        for (int a = 0; a < 3; a++) {
+            sc.ri_lo[a] = s->ri_lo[a]; sc.ri_hi[a] = s->ri_hi[a]; sc.ri_inv[a] = s->ri_inv[a]; sc.ri_dim[a] = s->ri_dim[a];
+        }
+    }
+}
+
+// The surrounding-RI grid (DESIGN.md §5 "RI grid"): about two cells per object over the union of
+// the LBVH leaf boxes; each object is entered in every cell its leaf box overlaps once widened by
+// a thousandth of a cell (far above the rounding of a float cell index), so the cell a point
+// falls in lists every object whose leaf box holds the point.  No grid when a cell would list
+// more than 64 objects.
+int make_ri_grid(rt_dev_scene *s, const std::vector<float> &lbox, uint32_t n) {
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (uint32_t g = 0; g < n; g++)
+        for (int a = 0; a < 3; a++) {
+            lo[a] = std::fmin(lo[a], double(lbox[size_t(g) * 8 + a]));
+            hi[a] = std::fmax(hi[a], double(lbox[size_t(g) * 8 + 3 + a]));
+        }
+    double ext[3], vol = 1.0;
+    for (int a = 0; a < 3; a++) {
+        if (!(hi[a] >= lo[a]) || !std::isfinite(lo[a]) || !std::isfinite(hi[a])) return RT_OK;
+        ext[a] = std::fmax(hi[a] - lo[a], 1e-6 * (1.0 + std::fabs(lo[a])));
+        vol *= ext[a];
+    }
+    const double cell = std::cbrt(vol / (2.0 * n));
+    int dim[3];
+    double inv[3];
+    for (int a = 0; a < 3; a++) {
+        dim[a] = int(std::fmin(512.0, std::fmax(1.0, std::ceil(ext[a] / cell))));
+        inv[a] = double(dim[a]) / ext[a];
+    }
+    const size_t nc = size_t(dim[0]) * dim[1] * dim[2];
+    std::vector<uint32_t> cnt(nc + 1, 0);
+    auto range = [&](uint32_t g, int a, int &c0, int &c1) {
+        const double m = 1e-3 / inv[a];
+        c0 = std::max(0, std::min(dim[a] - 1, int(std::floor((double(lbox[size_t(g) * 8 + a]) - m - lo[a]) * inv[a]))));
+        c1 = std::max(0, std::min(dim[a] - 1, int(std::floor((double(lbox[size_t(g) * 8 + 3 + a]) + m - lo[a]) * inv[a]))));
+    };
+    for (int pass = 0; pass < 2; pass++) {
+        std::vector<uint32_t> fill;
+        std::vector<uint32_t> ids;
+        if (pass == 1) {
+            for (size_t c = 0; c < nc; c++) cnt[c + 1] += cnt[c];
+            fill.assign(cnt.begin(), cnt.end() - 1);
+            ids.resize(cnt[nc]);
+        }
+        for (uint32_t g = 0; g < n; g++) {
+            int r0[3], r1[3];
+            for (int a = 0; a < 3; a++) range(g, a, r0[a], r1[a]);
+            for (int z = r0[2]; z <= r1[2]; z++)
+                for (int y = r0[1]; y <= r1[1]; y++)
+                    for (int x = r0[0]; x <= r1[0]; x++) {
+                        const size_t c = (size_t(z) * dim[1] + y) * dim[0] + x;
+                        if (pass == 0) {
+                            if (++cnt[c + 1] > 64) return RT_OK;
+                        } else ids[fill[c]++] = g;
+                    }
+        }
+        if (pass == 1) {
+            HIP_OK(s->ri_cells.upload(cnt.data(), cnt.size() * sizeof(uint32_t)));
+            HIP_OK(s->ri_ids.upload(ids.data(), std::max<size_t>(1, ids.size()) * sizeof(uint32_t)));
+        }
+    }
+    for (int a = 0; a < 3; a++) {
+        // float bounds: a point outside them is outside every leaf box
+        s->ri_lo[a] = float(lo[a]);
+        s->ri_hi[a] = float(hi[a]);
+        s->ri_inv[a] = float(inv[a]);
+        s->ri_dim[a] = dim[a];
+    }
+    return RT_OK;
 }
 
 int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
@@ -406,6 +483,7 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
     std::vector<float> lbox(size_t(n) * 8);  // each object's LBVH leaf node, indexed by object
     for (uint32_t g = 0; g < n; g++) std::memcpy(&lbox[size_t(g) * 8], nodes + size_t(leaf[g]) * 8, 8 * sizeof(float));
     HIP_OK(s->wleaf.upload(lbox.data(), lbox.size() * sizeof(float)));
+    if (int rc = make_ri_grid(s, lbox, n); rc != RT_OK) return rc;
     s->dfs_high = high;
     s->wdepth = depth4;
     s->wbound = wbound;

@@ -1990,8 +1990,7 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
 // the wide walk's conditions fail, or candidates beyond the stored ones could still win).
 template <bool WANT_NORMAL>
 __device__ float inw_closest_beam(const InwScene &S, const FStack &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
-                                  f3 &normal, float &extra, float init_geom, Ctr &c, uint32_t unit, bool &ok,
-                                  float &blim) {
+                                  f3 &normal, float &extra, float init_geom, Ctr &c, uint32_t unit, bool &ok) {
     const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};  // the reference's reciprocals (test_aabb)
     const uint32_t n = S.beam_n[unit];
     ok = n != kBeamOff && K.size + S.dfs_high <= (uint32_t)kFStack && __builtin_isfinite(id.x) &&
@@ -2037,7 +2036,6 @@ __device__ float inw_closest_beam(const InwScene &S, const FStack &K, f3 o, f3 d
     }
     // candidates not stored (entry >= cut) could still be reached below lim
     if (ok && (ovf || !(lim < S.beam_cut[unit]))) ok = false;
-    blim = lim;
     if (!ok) return init_geom;
     if (bg < 0) return init_geom;
     tlim = bt;
@@ -2124,37 +2122,41 @@ __device__ float inw_surrounding_ri_wide(const InwScene &S, FStack &K, f3 hp, fl
     return acc;
 }
 
-// The surrounding-RI walk (inw_surrounding_ri_wide) for the hit of a primary ray decided by its
-// beam list: the query point lies within 0.0011 of the hit, so an object holding it has its
-// culling box within beam_R of the central ray before the hit's bound blim, and it is listed.
-__device__ float inw_ri_beam(const InwScene &S, f3 hp, float ratio, Ctr &c, uint32_t unit, float blim, bool &ok) {
-    const uint32_t n = S.beam_n[unit];
-    const uint2 *list = S.beam + (size_t)unit * S.beam_cap;
+// The surrounding-RI walk (inw_surrounding_ri_wide) through the RI grid: the objects whose
+// leaf box holds the point are all listed in the point's cell (their boxes were entered with a
+// margin wider than the rounding of the cell index), so testing that cell's objects with the
+// walk's comparisons finds the same objects; they are summed in depth-first rank order.
+__device__ float inw_ri_grid(const InwScene &S, f3 hp, float ratio, Ctr &c, bool &ok) {
+    ok = true;
+    if (!(hp.x >= S.ri_lo[0] && hp.y >= S.ri_lo[1] && hp.z >= S.ri_lo[2] && hp.x <= S.ri_hi[0] &&
+          hp.y <= S.ri_hi[1] && hp.z <= S.ri_hi[2]))
+        return 1.0f;  // outside every leaf box (or NaN: no comparison holds, as in the walk)
+    const int cx = min(max((int)((hp.x - S.ri_lo[0]) * S.ri_inv[0]), 0), S.ri_dim[0] - 1);
+    const int cy = min(max((int)((hp.y - S.ri_lo[1]) * S.ri_inv[1]), 0), S.ri_dim[1] - 1);
+    const int cz = min(max((int)((hp.z - S.ri_lo[2]) * S.ri_inv[2]), 0), S.ri_dim[2] - 1);
+    const uint32_t cell = ((uint32_t)cz * (uint32_t)S.ri_dim[1] + (uint32_t)cy) * (uint32_t)S.ri_dim[0] + (uint32_t)cx;
+    const uint32_t b = S.ri_cells[cell], e = S.ri_cells[cell + 1];
     uint32_t rk[kRiMax];
     float rv[kRiMax];
     int nin = 0;
-    ok = true;
-    for (uint32_t k = 0; k < n; k++) {
-        const uint2 e = list[k];
-        if (!(__uint_as_float(e.y) <= blim)) break;
-        const int g = (int)e.x;
+    for (uint32_t k = b; k < e; k++) {
+        const int g = (int)S.ri_ids[k];
         c.prims++;
         const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
+        if (!(hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z)) continue;
         const Xf x = load_xf(S, g);
-        if (hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z) {
-            f3 v = (hp - x.pos) + x.delta * (1.0f - ratio);
-            v = tmul(x.R, v);
-            v.x *= x.is.x; v.y *= x.is.y; v.z *= x.is.z;
-            bool inside;
-            if (x.type == 1) inside = dot(v, v) <= 1.0f;
-            else if (x.type == 2) inside = fabsf(v.x) <= 0.5f && fabsf(v.y) <= 0.5f && fabsf(v.z) <= 0.5f;
-            else inside = false;
-            if (inside) {
-                if (nin == kRiMax) { ok = false; return 1.0f; }
-                rk[nin] = S.rank[g];
-                rv[nin] = x.ri_acc;
-                nin++;
-            }
+        f3 v = (hp - x.pos) + x.delta * (1.0f - ratio);
+        v = tmul(x.R, v);
+        v.x *= x.is.x; v.y *= x.is.y; v.z *= x.is.z;
+        bool inside;
+        if (x.type == 1) inside = dot(v, v) <= 1.0f;
+        else if (x.type == 2) inside = fabsf(v.x) <= 0.5f && fabsf(v.y) <= 0.5f && fabsf(v.z) <= 0.5f;
+        else inside = false;
+        if (inside) {
+            if (nin == kRiMax) { ok = false; return 1.0f; }
+            rk[nin] = S.rank[g];
+            rv[nin] = x.ri_acc;
+            nin++;
         }
     }
     for (int i = 1; i < nin; i++)
@@ -2180,6 +2182,10 @@ __device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o,
 template <bool LN = false>
 __device__ __forceinline__ float inw_ri(const InwScene &S, FStack &K, f3 hp, float ratio, Ctr &c) {
     bool ok = false;
+    if (S.ri_cells && K.size + S.dfs_high <= (uint32_t)kFStack) {  // no push of the walk could drop
+        const float g = inw_ri_grid(S, hp, ratio, c, ok);
+        if (ok) return g;
+    }
     const float r = inw_surrounding_ri_wide<LN>(S, K, hp, ratio, c, ok);
     if (ok) return r;
     return inw_surrounding_ri(S, K, hp, ratio, c);
@@ -2301,11 +2307,11 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         float tlim = tlim0, extra = 0.0f;
         f3 normal = f3{0, 0, 0};
         INW_T0(t_ch);
-        float fg, blim = 0.0f;
+        float fg;
         bool beam_ok = false;
         if (bunit != kBeamOff && (int)(bounced + 0.1f) == 0 && !mf0)  // a primary ray (pushed rays have bounced >= 1)
             fg = inw_closest_beam<true>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c, bunit,
-                                        beam_ok, blim);
+                                        beam_ok);
         if (!beam_ok)
             fg = inw_closest<true, LN, FU>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
         INW_CYC(c, 0, t_ch);
@@ -2355,9 +2361,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         if (!LIGHTS && (ri_forced || (ri_read && contribution > 0.01f && bounced + 1.0f < (float)F.max_bounces)))
         {
             INW_T0(t_ri);
-            bool rok = false;
-            if (beam_ok && !ri_forced) surr = inw_ri_beam(S, hitpoint + normal * 0.001f, ratio, c, bunit, blim, rok);
-            if (!rok) surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
+            surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
             INW_CYC(c, 1, t_ri);
         }
         if (mf0) K.size = 0;  // 01_BVH...glsl:544-549: the lens record goes after a primary hit
@@ -2377,11 +2381,8 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
                 }
                 const uint32_t nl = S.n_lights > 1 ? S.n_lights : 1u;
                 contribution *= (float)is_lit * rcp((float)nl);
-                if (ri_forced || (ri_read && contribution > 0.01f && bounced < (float)F.max_bounces)) {
-                    bool rok = false;
-                    if (beam_ok && !ri_forced) surr = inw_ri_beam(S, hitpoint + normal * 0.001f, ratio, c, bunit, blim, rok);
-                    if (!rok) surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
-                }
+                if (ri_forced || (ri_read && contribution > 0.01f && bounced < (float)F.max_bounces))
+                    surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
             } else {
                 if (ri_forced) (void)inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
                 color = f3{1, 1, 1};

@@ -89,6 +89,12 @@ struct InwScene {
     const float *beam_cut = nullptr;
     uint32_t beam_cap = 0;
     float beam_R = 0.0f, beam_tmin = 0.0f, beam_tfar = 0.0f, beam_kappa = 0.0f;
+    // Surrounding-RI grid (DESIGN.md §5 "RI grid"; null ri_cells = off): a uniform grid over the
+    // LBVH leaf boxes; cell c lists (ri_ids[ri_cells[c] .. ri_cells[c + 1]]) every object whose
+    // leaf box, widened by a margin above the rounding of the cell index, overlaps the cell.
+    const uint32_t *ri_cells = nullptr, *ri_ids = nullptr;
+    float ri_lo[3] = {0, 0, 0}, ri_hi[3] = {0, 0, 0}, ri_inv[3] = {0, 0, 0};
+    int ri_dim[3] = {0, 0, 0};
 };
 constexpr uint32_t kBeamOff = 0xffffffffu;
 
