@@ -2219,12 +2219,11 @@ __device__ __forceinline__ f3 inw_pixel_dir(const Frame &F, int px, int py) {
     f3 cr = cross(D, up), cu = cross(cr, D);
     return normalize((D * F.screen_dist + cr * srx) + cu * sry);
 }
-__device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame &F, FStack &K, int px, int py, int s,
-                                                 Ctr &c) {
+// cd: the pixel's direction (inw_pixel_dir), which callers that keep it per pixel pass in
+__device__ __forceinline__ void inw_start_sample_cd(const InwScene &S, const Frame &F, FStack &K, f3 cd, int s, Ctr &c) {
     K.size = 0;
     const f3 up = f3{0, 1, 0};
     f3 co = mk(F.pos[0], F.pos[1], F.pos[2]);
-    f3 cd = inw_pixel_dir(F, px, py);
     float ox = S.sunflower[2 * s] * (F.aperture * 0.5f), oy = S.sunflower[2 * s + 1] * (F.aperture * 0.5f);
     f3 rr = cross(cd, up), ru = cross(rr, cd);
     if (F.n_focus > 0) {  // MULTIFOCUS lens record (01_BVH...glsl:388-400): stack floats 0..5
@@ -2240,6 +2239,10 @@ __device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame 
     f3 tip = ((co + cd) + rr * ox) + ru * oy;
     f3 la = normalize((co + cd * F.focus) - tip);
     K.push_ray(tip - la, la, 1.0f, 0.0f, c);
+}
+__device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame &F, FStack &K, int px, int py, int s,
+                                                 Ctr &c) {
+    inw_start_sample_cd(S, F, K, inw_pixel_dir(F, px, py), s, c);
 }
 
 // texture(u_MaterialTextures[k], st) in a compute shader: lambda = 0, so the magnification
@@ -2785,6 +2788,8 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     int s = 0;
     UnitPix px{};
     uint32_t bu = kBeamOff;  // the lane's pixel unit for its beam list (S.beam)
+    uint32_t pu = 0xffffffffu;  // the unit px and pcd belong to: a lane's next sample is mostly the same pixel's
+    f3 pcd = f3{0, 0, 0};
     f3 col = f3{0, 0, 0};
     float dep = 0.0f;
     K.size = 0;
@@ -2870,13 +2875,17 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 if (!busy && rank < take) {
                     g = gi + rank;
                     s = (int)(adv - q * spp);
-                    px = unit_pixel(f, unit);
+                    if (unit != pu) {
+                        pu = unit;
+                        px = unit_pixel(f, unit);
+                        if (px.in_image) pcd = inw_pixel_dir(f, px.x, px.y);
+                    }
                     bu = S.beam ? unit : kBeamOff;
                     col = f3{0, 0, 0};
                     dep = 0.0f;
                     if (px.in_image) {
                         busy = true;
-                        inw_start_sample(S, f, K, px.x, px.y, s, c);
+                        inw_start_sample_cd(S, f, K, pcd, s, c);
                     } else {  // a padding slot: an empty sample, folded as zero
                         if ((uint32_t)s == mid && f.out_depth && px.out != (size_t)-1) f.out_depth[px.out] = 0.0f;
                         wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));

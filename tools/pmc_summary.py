@@ -61,6 +61,11 @@ def main():
         res["issue_stall_fraction"] = agg["SQ_WAIT_INST_ANY"] / agg["SQ_WAVE_CYCLES"]
     if "SQ_INSTS_VALU" in agg and "SQ_WAVES" in agg:
         res["valu_insts_per_wave"] = agg["SQ_INSTS_VALU"] / agg["SQ_WAVES"]
+    if "TA_TA_BUSY_sum" in agg and "GRBM_GUI_ACTIVE" in agg:
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md); one TA per CU (256)
+        res["ta_busy_fraction"] = agg["TA_TA_BUSY_sum"] / (256.0 * agg["GRBM_GUI_ACTIVE"] / 8.0)
+    if "TCP_TOTAL_CACHE_ACCESSES_sum" in agg and "TCP_TCC_READ_REQ_sum" in agg:
+        res["l1_read_miss_per_access"] = agg["TCP_TCC_READ_REQ_sum"] / max(1.0, agg["TCP_TOTAL_CACHE_ACCESSES_sum"])
     if "TCC_HIT_sum" in agg and "TCC_MISS_sum" in agg:
         res["l2_hit_rate"] = agg["TCC_HIT_sum"] / max(1.0, agg["TCC_HIT_sum"] + agg["TCC_MISS_sum"])
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
