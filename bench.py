@@ -178,7 +178,7 @@ def cpu_baseline(sc, threads: int, spp: int, bw: int = 64, rows_per_core: int = 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--spp", type=int, default=0, help="override spp (default: the config's 100)")
     ap.add_argument("--width", type=int, default=0)
