@@ -46,6 +46,45 @@ def _touching_cuboids(n=25, **over):
     return sc
 
 
+def _scene_cam(preset, seed, n_hint, cam_over, **over):
+    """make_scene with camera-description overrides (aperture, focus_dist, position, ...)."""
+    stage = R.PRESET_STAGE[preset]
+    arr, n, cd, par = R.preset_desc(preset, seed, n_hint)
+    for k, v in over.items():
+        setattr(par, k, v)
+    for k, v in cam_over.items():
+        if k == "position":
+            for i in range(3):
+                cd.position[i] = v[i]
+        else:
+            setattr(cd, k, v)
+    sc = R.Scene(stage=stage, desc=arr, n=n, camera=R.camera_from_desc(cd, stage), params=par)
+    for k, v in R.pack(arr, n, stage).items():
+        setattr(sc, k, v)
+    return sc
+
+
+def _dense_glass(n=160, **over):
+    """INW-01 with n refractive spheres of radius 1.5 packed into a 6-unit cube: points lie inside
+    many objects at once (more than the 8 the RI grid / wide RI walk sum before handing the query to
+    the reference walk, and cells listing more objects than the grid keeps), and the pixel beam
+    lists overflow their 32 entries."""
+    sc = _scene_cam(R.PRESET_INW01_RANDOM, 99, n, {"position": (-7.0, 2.5, -7.0), "focus_dist": 8.0}, **over)
+    arr = sc.desc
+    rng = np.random.default_rng(7)
+    for i in range(sc.n):
+        d = arr[i]
+        p = rng.uniform(-3.0, 3.0, 3)
+        for k in range(3):
+            d.position[k] = float(p[k])
+            d.last_position[k] = float(p[k]) - 0.1
+            d.scale[k] = 1.5
+        d.refractivity, d.reflectivity, d.refractive_index = 0.65, 0.15, 1.3 + 0.05 * (i % 8)
+    for k, v in R.pack(arr, sc.n, sc.stage).items():
+        setattr(sc, k, v)
+    return sc
+
+
 CASES = {
     # name: callable -> Scene (IOW-01 handled separately)
     "iow03_ref3": lambda: _scene(R.PRESET_IOW03_REF3, spp=4),
@@ -69,6 +108,13 @@ CASES = {
     "inw01_random_two": lambda: _scene(R.PRESET_INW01_RANDOM, 5, 2, width=33, height=7, spp=4),
     "inw01_touching_cuboids": lambda: _touching_cuboids(25, width=64, height=64, spp=4, max_bounces=12),
     "inw04_cornell_odd": lambda: _scene(R.PRESET_INW04_CORNELL, 7, 0, width=13, height=11, spp=3, max_bounces=3),
+    # pixel beams (k_inw_beam): a wide lens makes the lists overflow (their cut decides), a focus
+    # distance near the lens turns them off; a dense glass cluster for the RI grid's fallbacks
+    "inw01_random_aperture": lambda: _scene_cam(R.PRESET_INW01_RANDOM, 1234, 3000, {"aperture": 4.0},
+                                                width=64, height=36, spp=12),
+    "inw01_random_focus1": lambda: _scene_cam(R.PRESET_INW01_RANDOM, 1234, 3000, {"focus_dist": 1.05},
+                                              width=48, height=27, spp=8),
+    "inw01_dense_glass": lambda: _dense_glass(160, width=48, height=48, spp=6, max_bounces=10),
 }
 
 GOLDEN_CASES = ["iow01_c1", "iow03_ref3", "iow03_ref3_normals", "iow03_final", "inw01_grid",
