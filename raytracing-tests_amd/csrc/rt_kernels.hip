@@ -2812,6 +2812,12 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 const uint32_t e = i + (n - i < spp - sf ? n - i : spp - sf);
                 uint32_t j = i;
                 if (sf == 0) { acc = f3{rdl(v.x, j), rdl(v.y, j), rdl(v.z, j)}; j++; }
+                for (; j + 4u <= e; j += 4u) {  // four adds in order, one loop test
+                    acc = acc + f3{rdl(v.x, j), rdl(v.y, j), rdl(v.z, j)};
+                    acc = acc + f3{rdl(v.x, j + 1u), rdl(v.y, j + 1u), rdl(v.z, j + 1u)};
+                    acc = acc + f3{rdl(v.x, j + 2u), rdl(v.y, j + 2u), rdl(v.z, j + 2u)};
+                    acc = acc + f3{rdl(v.x, j + 3u), rdl(v.y, j + 3u), rdl(v.z, j + 3u)};
+                }
                 for (; j < e; j++) acc = acc + f3{rdl(v.x, j), rdl(v.y, j), rdl(v.z, j)};
                 sf += e - i;
                 i = e;

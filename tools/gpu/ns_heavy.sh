@@ -1,7 +1,7 @@
 # North-star workload (IOW-03 final scene, 1920x1080, 500 spp): 8-way shares for heavy-first settings
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r8; rm -rf $O; mkdir -p $O
+O=gpurun_out/ns_heavy; rm -rf $O; mkdir -p $O
 for h in ${HEAVY:-default 48 96}; do
   if [ "$h" = "default" ]; then unset RT_SPEC_HEAVY; else export RT_SPEC_HEAVY=$h; fi
   timeout -k 10 900 bash tools/gpu/shares.sh ns 8 1 > $O/h_$h.txt 2>&1 || exit 1

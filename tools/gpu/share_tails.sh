@@ -2,7 +2,7 @@
 # estimate (16 pixels per block), every pixel of the block (RT_COST64 build) and unit order
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r9; rm -rf $O; mkdir -p $O
+O=gpurun_out/share_tails; rm -rf $O; mkdir -p $O
 L=$GRAFT_REPO_ROOT/raytracing-tests_amd
 for sh in 0/8 6/8; do
   t=$(echo $sh | tr '/' 'o')
