@@ -167,12 +167,37 @@ def cpu_baseline(sc, threads: int, spp: int, bw: int = 64, rows_per_core: int = 
     p.tile_x0, p.tile_y0 = sc.params.width // 2 - bw // 2, sc.params.height // 2 - bh // 2
     p.tile_w, p.tile_h = bw, bh
     t0 = time.perf_counter()
-    _, _, st = O.render(sc, p)
+    rgba, depth, st = O.render(sc, p)
     dt = time.perf_counter() - t0
+    rect = (p.tile_x0, p.tile_y0, bw, bh)
     return {"value": st["segments"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"central {bw}x{bh} pixel block of the same frame at {p.spp} spp / "
                       f"{sc.params.max_bounces} bounces, one OpenMP thread per core = nproc "
-                      f"({st['segments']} rays, {dt:.1f} s, oracle/librt_oracle.so)"}
+                      f"({st['segments']} rays, {dt:.1f} s, oracle/librt_oracle.so)"}, (rect, rgba, depth, p.spp)
+
+
+def block_parity(rect, ref_rgba, ref_depth, img, dep) -> dict:
+    """The GPU frame's pixels in `rect` against the oracle's render of that block (bit
+    comparison, NaN == NaN): max |delta| per channel, the fraction of bit-identical values, pixels."""
+    x0, y0, w, h = rect
+    a = np.ascontiguousarray(img[y0:y0 + h, x0:x0 + w], np.float32)
+    b = np.ascontiguousarray(ref_rgba[y0:y0 + h, x0:x0 + w], np.float32)
+    pairs = [(a, b)]
+    if dep is not None and ref_depth is not None:
+        pairs.append((np.ascontiguousarray(dep[y0:y0 + h, x0:x0 + w], np.float32),
+                      np.ascontiguousarray(ref_depth[y0:y0 + h, x0:x0 + w], np.float32)))
+    same, total, mx, nan_mis = 0, 0, 0.0, 0
+    for u, v in pairs:
+        nu, nv = np.isnan(u), np.isnan(v)
+        both = ~(nu | nv)
+        d = np.abs(u[both].astype(np.float64) - v[both].astype(np.float64))
+        mx = max(mx, float(d.max()) if d.size else 0.0)
+        same += int(((u.view(np.uint32) == v.view(np.uint32)) | (nu & nv)).sum())
+        total += u.size
+        nan_mis += int((nu != nv).sum())
+    return {"max_abs": mx, "exact_frac": same / max(total, 1), "nan_mismatch": nan_mis, "pixels": w * h,
+            "rect": list(rect), "depth": len(pairs) > 1, "tol": 1e-3,
+            "oracle": "oracle/librt_oracle.so render of the same block at the same spp (the cpu_baseline run)"}
 
 
 def main():
@@ -192,6 +217,8 @@ def main():
                          "(measured neutral on the 8-way frames: their time is set by long samples, not by rays)")
     ap.add_argument("--occupancy", action="store_true", help="report per-phase lane occupancy (diagnostic)")
     ap.add_argument("--save-image", default="", help="rank 0 saves the assembled frame (.npy) for checking")
+    ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
+                    help="set an rt_options field for this run (A/B of the exact strategies; recorded in the line)")
     ap.add_argument("--config", default="c3", choices=("c3", "c4", "c2", "ns"),
                     help="c3 (= c4): BASELINE configs[2] / configs[3], the headline; c2: configs[1]; "
                          "ns: the north star's IOW-03 workload")
@@ -217,6 +244,12 @@ def main():
     host_coll = world > 1 and backend != "nccl"
 
     lib = R.load()
+    if args.opt:
+        o = R.get_options()
+        for kv in args.opt:
+            k, v = kv.split("=", 1)
+            setattr(o, k, type(getattr(o, k))(float(v)) if k == "spec_max_gb" else int(v))
+        R.set_options(o)
     over = {}
     if args.spp:
         over["spp"] = args.spp
@@ -368,9 +401,9 @@ def main():
     st = dict(zip(("segments", "node_visits", "prim_tests", "shadow_queries", "stack_drops", "nan_drops"), c))
     per_step = {k: v / args.steps for k, v in st.items()}
 
-    kname = C.create_string_buffer(64)
-    launches = max(1, lib.rt_debug_launches(scene, kname, 64))  # main-kernel launches per frame (planned)
-    kname = kname.value.decode()
+    path = R.debug_path(scene)  # the kernel and the exact shortcuts the last frame ran (rt_debug_path)
+    launches = max(1, path["launches"])  # main-kernel launches per frame (planned)
+    kname = path["kernel"]
     # the main kernel's own launches in the last timed frame, each bracketed by HIP events on its
     # stream inside the library (rt_debug_time_kernels): what rocprofv3's per-kernel stats see
     kt_ms, kt_n = C.c_double(0.0), C.c_int(0)
@@ -414,7 +447,7 @@ def main():
             except Exception:  # noqa: BLE001
                 traffic, valu, lane_issue, prof_src = None, None, None, None
         # the same roofline over the reference's own walk: F_alg with the node visits and object
-        # tests of the reference's LBVH walk of this frame (RT_INW_FAST=0, the oracle's counts;
+        # tests of the reference's LBVH walk of this frame (inw_wide_walk=0, the oracle's counts;
         # profiles/refwalk_<cfg>.json), a fixed amount of work per frame whatever walk runs
         ref_walk = None
         rw = os.path.join(ROOT, "profiles", f"refwalk_{cfg}.json")
@@ -431,14 +464,21 @@ def main():
                                 "source": "profiles/" + os.path.basename(rw)}
             except Exception:  # noqa: BLE001
                 ref_walk = None
-        cpu = None
+        cpu, parity = None, None
         if world == 1 and not args.no_cpu_baseline:
             cores = args.cpu_threads or host_cores()
             # ~10-20 s of host work on the GPU box (C3: 3.2 Mrays/s on 16 cores for the central block)
             if cfg == "c3":
-                cpu = cpu_baseline(sc, cores, args.cpu_spp or sc.params.spp, bw=256, rows_per_core=4)
+                cpu, ref = cpu_baseline(sc, cores, args.cpu_spp or sc.params.spp, bw=256, rows_per_core=4)
             else:  # IOW-03: ~280 rays per sample; ns has 5x the samples per pixel of c2
-                cpu = cpu_baseline(sc, cores, args.cpu_spp or sc.params.spp, bw=16 if cfg == "ns" else 64)
+                cpu, ref = cpu_baseline(sc, cores, args.cpu_spp or sc.params.spp, bw=16 if cfg == "ns" else 64)
+            rect, ref_rgba, ref_depth, ref_spp = ref
+            if ref_spp == spp and not shard:  # the oracle rendered the same block at the frame's spp
+                dimg = None
+                if inw and buf["depth"] is not None:  # the last timed frame's depth tiles, assembled
+                    d = buf["depth"].unsqueeze(0).unsqueeze(-1).expand(-1, -1, -1, -1, 4).contiguous()
+                    dimg = assemble_lists(d, lists, nx, ny)[..., 0].cpu().numpy()
+                parity = block_parity(rect, ref_rgba, ref_depth, image.cpu().numpy(), dimg)
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -485,6 +525,14 @@ def main():
             "rays_per_step": int(per_step["segments"]),
             "counters_per_step": {k: int(v) for k, v in per_step.items()},
             "cpu_baseline": cpu,
+            "parity": parity,
+            "path": path,
+            "options": {k: v for k, v in R.get_options().as_dict().items()
+                        if v != R.default_options().as_dict()[k]} or "defaults",
+            "timed_region": "rt_render_tiles_async of one full frame per step (+ the RCCL gather and rank 0's "
+                            "frame assembly at N > 1) on a device scene built before timing: the host "
+                            "acceleration structures, the scene upload and the device allocations of the first "
+                            "frame are outside it (bench.py --rebuild times them per step)",
         }
         if args.occupancy:
             d = [int(v) for v in dbg.cpu().tolist()]

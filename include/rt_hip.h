@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* status codes */
 #define RT_OK            0
@@ -90,6 +90,61 @@ typedef struct rt_stats {
     uint64_t nan_drops;       /* secondary directions that came out NaN                      */
     double   ms;              /* device time of the render launch(es), milliseconds          */
 } rt_stats;
+
+/* ---- options ------------------------------------------------------------------------
+ * The strategy switches of the render path.  Every strategy is exact: the image, the depth
+ * and the ray-level counters are bit-identical whatever the options (tests/test_gpu_bvh_exact.py);
+ * only speed and the build's own node / primitive counts change.  The defaults (rt_options_default)
+ * are the measured-best settings; nothing else (no environment variable) changes what the
+ * library runs.  rt_options_set sets the library-wide options; a device scene copies them when
+ * it is created (rt_dev_scene_*) and rt_dev_scene_set_options replaces its copy.  The blocking
+ * entry points build a scene per call, so they use the options current at the call.
+ * Options marked [build] shape the scene's device structures and are read at scene creation only. */
+typedef struct rt_options {
+    uint32_t size;          /* sizeof(rt_options), set by rt_options_default; checked by the setters */
+    /* INW (In-Next-Week 01 / 04) */
+    int inw_wide_walk;      /* [build] 1: 4-wide culling walk with the reference's leaf tests; 0: the LBVH walk as the shader does it */
+    int inw_order;          /* fold kernel: 0 = the probe picks, 1 = pixel-major, 2 = sample-major, -1 = per-pixel k_inw */
+    int inw_beams;          /* per-pixel candidate lists for primary rays (pixel-major frames) */
+    int inw_ri_grid;        /* surrounding-RI queries through the uniform grid */
+    int inw_lds_nodes;      /* top of the wide BVH staged in LDS (768-lane blocks) */
+    int inw_fused_cull;     /* one fma per culling plane where the error bound holds */
+    int inw_claim_order;    /* pixel-major claims costliest 8x8 blocks first */
+    int inw_ring_pm;        /* fold window (entries per wave) of the pixel-major kernel, power of two >= 64 */
+    int inw_ring_sm;        /* ... of the sample-major kernel */
+    /* IOW-03 (In-One-Weekend 03) */
+    int iow_spec;           /* sample-parallel speculation (0: the sequential per-pixel kernel) */
+    int iow_linear;         /* [build] the shader's linear object loop instead of the culling BVH */
+    int iow_narrow;         /* byte bounce counts / 12-deep BVH stack variant (u_NumOfBounce <= 255) */
+    int iow_lds_bvh;        /* culling BVH staged in LDS when it fits */
+    int iow_leaf_batch;     /* test postponed leaves once this many lanes hold one (1..65) */
+    int iow_coop_max;       /* wave-cooperative closest hits when at most this many lanes trace (0 = off) */
+    int iow_chunks_lpt;     /* sequential kernel: a short first sample chunk, then longest-first */
+    int rounds_seq;         /* tail-compaction rounds per pass, sequential kernels (0..14) */
+    int rounds_spec;        /* ... sample-parallel passes (0..14) */
+    int park_min;           /* park lanes only while at least this many units remain (-1: resident lanes / 8) */
+    int spec_iters;         /* resolve + re-run passes */
+    int spec_probe;         /* heavy-first: every spec_probe-th pixel probes all sample indices */
+    int spec_heavy;         /* heavy-first: costliest sample indices run first (-1: (spp - 1) / 20) */
+    int spec_rounds;        /* checkpoint rounds of the speculative pass (0 = one launch) */
+    int spec_tail_rounds;   /* budgeted tail rounds */
+    int spec_tail_budget;   /* segments per unit and budgeted tail round */
+    int spec_scan;          /* anchored scan past the frontier, samples (0 = off) */
+    int spec_chain;         /* exact restarts follow their pixel's chain */
+    int spec_alt;           /* alternative runs for long samples that read one stale entry */
+    int spec_alt_cap;       /* alternative-run records */
+    int spec_alt_seg;       /* segments that make a sample long enough for alternatives */
+    int spec_alt_every;     /* also spawn alternatives after every k-th budgeted tail round (0 = once) */
+    int spec_spread;        /* the last round of a pass gives long samples a wave each */
+    int spec_prior_from;    /* first sample whose stale entries are guessed as the scene's RI prior */
+    int spec_sort;          /* run the first re-execution list longest first */
+    int spec_solo;          /* re-run pass: the longest samples take a wave each, up to this many */
+    int spec_validate;      /* the sequential leftover pass reuses still-exact records */
+    double spec_max_gb;     /* device memory cap of the speculation records, GB */
+} rt_options;
+void rt_options_default(rt_options *o);
+int  rt_options_set(const rt_options *o);   /* RT_E_ARG: null, wrong size or a value out of range */
+int  rt_options_get(rt_options *o);
 
 /* ---- version / device ------------------------------------------------------------ */
 int  rt_abi_version(void);
@@ -208,6 +263,24 @@ rt_dev_scene *rt_dev_scene_inw_tex(const float *geom, uint32_t n, int layout, co
                                    const float *lights, uint32_t n_lights, const rt_texture *tex, int n_tex,
                                    int spp, int device);
 void rt_dev_scene_free(rt_dev_scene *s);
+/* Replace the scene's options (the [build] ones keep the values the scene was built with). */
+int rt_dev_scene_set_options(rt_dev_scene *s, const rt_options *o);
+
+/* The path the scene's last render took (bench line): the main kernel as
+ * rocprofv3 names it and its launches per frame, the resolved fold order and which exact
+ * shortcuts were on for that frame (some are decided per frame: the probe's pick, the fused
+ * cull's error bound, the beam lists' memory and geometry conditions).  Synchronises when the
+ * fold order was left to the device probe. */
+typedef struct rt_path_info {
+    char kernel[64];
+    int launches;
+    int order;            /* INW: 1 pixel-major, 2 sample-major, 3 per-pixel k_inw; IOW-03: 4 sample-parallel, 5 sequential */
+    int order_forced;     /* 1 when rt_options.inw_order chose it, 0 when the probe did */
+    int wide_walk, beams, ri_grid, fused_cull, lds_nodes, claim_order;
+    int ring_entries;     /* fold window of the kernel that ran */
+    int iow_bvh;          /* IOW-03: 0 linear loop, 1 culling BVH, 2 culling BVH in LDS */
+} rt_path_info;
+int rt_debug_path(rt_dev_scene *s, rt_path_info *out);
 
 /* Render one tile list.  tiles: device int array of n_tiles (tx, ty) pairs of tile_size^2
  * tiles; out_packed: device float array n_tiles*tile_size*tile_size*4 (tile-major, row-major
@@ -252,7 +325,9 @@ int rt_display_rgba8_async(const float *d_rgba, const float *d_depth, int width,
 int rt_debug_counters(uint64_t *d_buf);
 /* d_buf: device array with one uint32 per work unit (or NULL to disable): the IOW-03 kernel
  * writes the rays each pixel cast when the pixel completes (unit = tile-major pixel index in
- * tile mode, 8x8-block-major in rect mode). */
+ * tile mode, 8x8-block-major in rect mode).  The INW fold kernels instead ADD the rays of each
+ * output pixel (index = the pixel's position in the output image: y * W + x, or the packed
+ * tile index), so the buffer must be zeroed before the render. */
 int rt_debug_pixel_rays(uint32_t *d_buf);
 /* Lanes parked by each tail-compaction round of the scene's last render (synchronises the
  * device).  Returns the number of rounds written to out (<= cap). */

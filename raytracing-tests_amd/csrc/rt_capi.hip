@@ -23,6 +23,35 @@
 namespace {
 
 unsigned long long *g_dbg = nullptr;  // rt_debug_counters(): lane-occupancy diagnostics
+
+// rt_options (include/rt_hip.h): the library-wide options; scenes copy them at creation
+rt_options default_options() {
+    rt_options o;
+    std::memset(&o, 0, sizeof(o));
+    o.size = sizeof(rt_options);
+    o.inw_wide_walk = 1; o.inw_order = 0; o.inw_beams = 1; o.inw_ri_grid = 1; o.inw_lds_nodes = 1;
+    o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 1024; o.inw_ring_sm = 256;
+    o.iow_spec = 1; o.iow_linear = 0; o.iow_narrow = 0; o.iow_lds_bvh = 1;
+    o.iow_leaf_batch = 32;  // 32 measured 2.5% faster on the bench frame than 65 (round 2)
+    o.iow_coop_max = 4; o.iow_chunks_lpt = 0;
+    o.rounds_seq = 6; o.rounds_spec = 1; o.park_min = -1;
+    o.spec_iters = 1; o.spec_probe = 64; o.spec_heavy = -1; o.spec_rounds = 24; o.spec_tail_rounds = 60;
+    o.spec_tail_budget = 3072; o.spec_scan = 128; o.spec_chain = 1; o.spec_alt = 1; o.spec_alt_cap = 1 << 17;
+    o.spec_alt_seg = 16384; o.spec_alt_every = 0; o.spec_spread = 1; o.spec_prior_from = 2; o.spec_sort = 1;
+    o.spec_solo = 4096; o.spec_validate = 1; o.spec_max_gb = 96.0;
+    return o;
+}
+bool options_ok(const rt_options *o) {
+    auto pow2 = [](int r) { return r >= 64 && r <= (1 << 16) && (r & (r - 1)) == 0; };
+    return o && o->size == sizeof(rt_options) && o->inw_order >= -1 && o->inw_order <= 2 && pow2(o->inw_ring_pm) &&
+           pow2(o->inw_ring_sm) && o->iow_leaf_batch >= 1 && o->iow_leaf_batch <= 65 && o->iow_coop_max >= 0 &&
+           o->rounds_seq >= 0 && o->rounds_seq <= 14 && o->rounds_spec >= 0 && o->rounds_spec <= 14 &&
+           o->park_min >= -1 && o->spec_iters >= 0 && o->spec_probe >= 1 && o->spec_heavy >= -1 &&
+           o->spec_rounds >= 0 && o->spec_tail_rounds >= 0 && o->spec_tail_budget >= 1 && o->spec_scan >= 0 &&
+           o->spec_alt_cap >= 1024 && o->spec_alt_cap <= (1 << 24) && o->spec_alt_seg >= 1 && o->spec_alt_every >= 0 &&
+           o->spec_prior_from >= 1 && o->spec_solo >= 0 && o->spec_max_gb > 0.0;
+}
+rt_options g_opt = default_options();
 unsigned *g_px_rays = nullptr;        // rt_debug_pixel_rays(): rays per work unit
 
 #define HIP_OK(expr)                                             \
@@ -88,14 +117,7 @@ rtk::Frame make_frame(const rt_camera *cam, const rt_params *p) {
     f.inv_spp = 1.0f / (float)p->spp;
     f.dbg = g_dbg;
     f.px_rays = g_px_rays;
-    // IOW-03 walk: test postponed leaves once this many lanes hold one (65 = only when no lane can
-    // advance); 32 measured 2.5% faster on the bench frame than 65 (round 2)
-    const char *lb = std::getenv("RT_LEAF_BATCH");
-    f.leaf_batch = (lb && *lb) ? std::max(1, std::atoi(lb)) : 32;
-    // IOW-03: wave-cooperative closest hits for waves with at most this many tracing lanes
-    // (0 = off; every mode is bit-identical, tests/test_gpu_bvh_exact.py)
-    const char *co = std::getenv("RT_COOP");
-    f.coop_max = (co && *co) ? std::max(0, std::atoi(co)) : 4;
+    // leaf_batch / coop_max / narrow come from the scene's options (launch_scene)
 #ifdef RT_DIAG  // diagnostic builds only (make variant VDEFS=-DRT_DIAG)
     const char *fs = std::getenv("RT_DEBUG_FIRST_STALE");
     f.dbg_first_stale = (fs && fs[0] == '1') ? 1 : 0;
@@ -107,6 +129,7 @@ rtk::Frame make_frame(const rt_camera *cam, const rt_params *p) {
 
 // A prepared scene: device-resident records, LBVH nodes, lights and sample tables.
 struct rt_dev_scene {
+    rt_options opt = g_opt;  // the options current when the scene was created (rt_dev_scene_set_options)
     int kind = 0;  // 3 = IOW-03, 11/14 = INW layout 1/4
     int device = 0;
     int spp = 0;
@@ -136,6 +159,9 @@ struct rt_dev_scene {
     int wdepth = 0;               // levels of the 4-wide culling BVH
     bool last_ln = false;         // the last INW fold launch used the LDS-staged kernels
     bool last_fu = false;         // ... their fused-fma cull instances
+    uint32_t last_force = 0;      // ... its forced order (0: the probe's pick, read back from inw_mode)
+    uint32_t last_ring[2] = {0, 0};  // ... its fold windows (pixel-major, sample-major)
+    rt_path_info last_path{};     // rt_debug_path: what the last render ran
     float wbound = 0.0f;          // largest |coordinate| of the INW culling boxes (the fused cull's condition)
     uint32_t dfs_high = 0;
     uint32_t n_tex = 0;
@@ -271,8 +297,7 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
     HIP_OK(s->cold.upload(cold.data(), cold.size() * sizeof(float)));
     // Culling BVH over the objects (the reference loops linearly; rtk::iow_launch_ray keeps its
     // exact result).  World box = |M^T| * local half extents, inflated so it is conservative.
-    const char *force_linear = std::getenv("RT_IOW_LINEAR");  // A/B switch: the reference's linear loop
-    if (n >= 2 && !(force_linear && force_linear[0] == '1')) {
+    if (n >= 2 && !s->opt.iow_linear) {  // iow_linear: the reference's linear loop (A/B)
         std::vector<float> boxes(size_t(n) * 6);
         for (uint32_t j = 0; j < n; j++) {
             const float *r = rec + size_t(j) * 24;
@@ -335,7 +360,7 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     sc.leafbox = s->wleaf.as<float4>();
     sc.dfs_high = s->dfs_high;
     sc.n_wnodes = uint32_t(s->wnodes.bytes / (10 * sizeof(float4)));
-    if (s->ri_cells.p && !(std::getenv("RT_INW_RIGRID") && std::getenv("RT_INW_RIGRID")[0] == '0')) {
+    if (s->ri_cells.p && s->opt.inw_ri_grid) {
         sc.ri_cells = s->ri_cells.as<uint32_t>();
         sc.ri_ids = s->ri_ids.as<uint32_t>();
         for (int a = 0; a < 3; a++) {
@@ -413,8 +438,7 @@ int make_ri_grid(rt_dev_scene *s, const std::vector<float> &lbox, uint32_t n) {
 
 int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
     s->dfs_high = 0;
-    const char *off = std::getenv("RT_INW_FAST");
-    if (n < 2 || (off && off[0] == '0')) return RT_OK;
+    if (n < 2 || !s->opt.inw_wide_walk) return RT_OK;
     const uint32_t nn = 2 * n - 1;
     std::vector<uint32_t> leaf(n, 0xffffffffu), rank(size_t(2) * n, 0);
     for (uint32_t i = 0; i < nn; i++) {
@@ -530,12 +554,11 @@ int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const f
 }
 
 // Sample ranges of the render.  Default: one range (tail compaction keeps the SIMDs full).
-// RT_CHUNKS=lpt: a short first chunk measures every pixel's cost and the rest run
+// rt_options.iow_chunks_lpt: a short first chunk measures every pixel's cost and the rest run
 // longest-first (LPT) -- kept as an A/B switch; with compaction it measured slower.
-std::vector<std::pair<int, int>> chunk_plan(int spp) {
+std::vector<std::pair<int, int>> chunk_plan(int spp, bool lpt) {
     std::vector<std::pair<int, int>> plan;
-    const char *env = std::getenv("RT_CHUNKS");
-    if (spp <= 2 || !(env && std::strcmp(env, "lpt") == 0)) { plan.push_back({0, spp}); return plan; }
+    if (spp <= 2 || !lpt) { plan.push_back({0, spp}); return plan; }
     const int first = std::max(1, spp / 20);
     const int step = std::max(1, (spp - first + 7) / 8);
     plan.push_back({0, first});
@@ -564,9 +587,15 @@ int ensure_workspace(rt_dev_scene *s, uint32_t units) {
     return RT_OK;
 }
 
+#ifdef RT_DIAG  // diagnostic builds only: switches of the diagnostics (never of the render path)
 int env_int(const char *name, int dflt) {
     const char *v = std::getenv(name);
     return (v && *v) ? std::atoi(v) : dflt;
+}
+#endif
+// park lanes only while at least this many units remain (rt_options.park_min; -1: cap / 8 waves)
+uint32_t park_min_of(const rt_dev_scene *s, int cap) {
+    return uint32_t(s->opt.park_min >= 0 ? s->opt.park_min : cap * rtk::kBlock / 8);
 }
 
 int ensure_cont(rt_dev_scene *s) {
@@ -609,8 +638,7 @@ int ensure_lanes(rt_dev_scene *s, int groups, size_t temp_bytes) {
 bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
     const size_t n = size_t(P) * S;
     const size_t bytes = n * (4 * sizeof(float4) + 4 * sizeof(uint32_t)) + size_t(P) * (4 + 32);
-    const double max_gb = std::atof(std::getenv("RT_SPEC_MAX_GB") ? std::getenv("RT_SPEC_MAX_GB") : "96");
-    if (double(bytes) > max_gb * 1e9) return false;
+    if (double(bytes) > s->opt.spec_max_gb * 1e9) return false;
     if (n <= s->spec_cap && P <= s->spec_units) return true;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || bytes > free_b / 2) return false;
@@ -648,16 +676,22 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st);
 int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     f.n_focus = (s->kind != 3 && s->layout == 1) ? s->n_focus : 0;
     std::memcpy(f.focus_list, s->focus, sizeof(f.focus_list));
-    if (s->kind == 3 && env_int("RT_IOW_SPEC", 1) != 0 && !rtk::iow_narrow(f) && s->s_stop > 0 &&
+    f.leaf_batch = s->opt.iow_leaf_batch;
+    f.coop_max = s->opt.iow_coop_max;
+    f.narrow = s->opt.iow_narrow;
+    s->last_path = rt_path_info{};
+    if (s->kind == 3 && s->opt.iow_spec && !rtk::iow_narrow(f) && s->s_stop > 0 &&
         ensure_spec(s, rtk::units_of(f), uint32_t(s->s_stop)))
         return launch_scene_spec(s, f, st);
-    // INW: the on-chip fold kernels; RT_INW_ORDER=-1 runs the per-pixel sequential kernel k_inw
+    // INW: the on-chip fold kernels; inw_order = -1 runs the per-pixel sequential kernel k_inw
     // (a second restatement of End()'s loop, kept for the strategy-exactness tests)
-    if (s->kind != 3 && env_int("RT_INW_ORDER", 0) >= 0) return launch_scene_inw_fold(s, f, st);
-    const std::vector<std::pair<int, int>> plan = chunk_plan(f.spp);
+    if (s->kind != 3 && s->opt.inw_order >= 0) return launch_scene_inw_fold(s, f, st);
+    const std::vector<std::pair<int, int>> plan = chunk_plan(f.spp, s->opt.iow_chunks_lpt != 0);
     const uint32_t units = rtk::units_of(f);
     s->last_kernel = s->kind == 3 ? (rtk::iow_narrow(f) ? "k_iow03n" : "k_iow03") : (s->layout == 4 ? "k_inw<true>" : "k_inw<false>");
-    s->last_launches = int(plan.size()) * (1 + std::min(14, std::max(0, env_int("RT_ROUNDS", 6))));
+    s->last_launches = int(plan.size()) * (1 + s->opt.rounds_seq);
+    s->last_path.order = s->kind == 3 ? 5 : 3;
+    s->last_path.wide_walk = s->kind != 3 && s->dfs_high != 0;
     s->last_chunks = int(plan.size());
     if (plan.size() > 1) {
         int rc = ensure_workspace(s, units);
@@ -667,19 +701,21 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // lanes the previous one parked.  Counts stay on the device (no host round trip): a resume
     // launch with nothing parked exits at once.  Parking stops below ~one wave per SIMD, where
     // compaction can no longer shorten the critical path; the last round never parks.
-    const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 6)));  // <= 14: one count slot per round
+    const int rounds = s->opt.rounds_seq;  // <= 14: one count slot per round
     // grid of this frame's kernel variant
     int cap = s->kind == 3 ? s->cus * rtk::resident_blocks_per_cu(rtk::iow_narrow(f) ? 4 : 3) : s->blocks_cap;
     if (s->kind == 3 && !rtk::iow_narrow(f)) {
         rtk::IowScene probe{};
         probe.nodes = s->nodes.as<float4>();
         probe.n_nodes = s->n_wide;
+        probe.lds_on = s->opt.iow_lds_bvh;
         if (rtk::iow_lds(probe)) {
             cap = s->cus * 3 * rtk::resident_blocks_per_cu(9);  // 256-lane slots of the 768-lane blocks
             s->last_kernel = "k_iow03L";
         }
+        s->last_path.iow_bvh = s->root_link ? (rtk::iow_lds(probe) ? 2 : 1) : 0;
     }
-    const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
+    const uint32_t park_min = park_min_of(s, cap);
     if (rounds > 0) {
         int rc = ensure_cont(s);
         if (rc != RT_OK) return rc;
@@ -712,7 +748,7 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             if (s->kind == 3) {
                 rtk::IowScene sc{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
                                  s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link,
-                                 s->obox.as<float4>(), s->n_wide};
+                                 s->obox.as<float4>(), s->n_wide, s->opt.iow_lds_bvh};
                 e = rtk::launch_iow03(f, sc, ch, ct, n_units, s->counter.as<unsigned>(), s->s_stop, cap, st);
             } else {
                 rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
@@ -766,8 +802,9 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     s->kt_used = 0;
     int rc = ensure_workspace(s, P);
     if (rc != RT_OK) return rc;
-    const int rounds = std::min(14, std::max(0, env_int("RT_ROUNDS", 1)));
-    const int iters = std::max(0, env_int("RT_SPEC_ITERS", 1));
+    const rt_options &o = s->opt;
+    const int rounds = o.rounds_spec;
+    const int iters = o.spec_iters;
     const int groups = 1;  // one pipeline (per-group streams measured slower: 8.8 s with 4 groups)
     const size_t gmax = size_t(P + groups - 1) / groups + 1;  // pixels in the largest group
     if ((rc = ensure_cont(s)) != RT_OK) return rc;
@@ -777,9 +814,9 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                           s->sp_assume.as<float4>(), P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(),
                           sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), ++s->epoch,
                           s->sp_front.as<uint4>(), s->sp_sorder.as<uint32_t>(),
-                          uint32_t(std::max(1, env_int("RT_SPEC_PROBE", 64))),
-                          S > 2 && groups == 1 ? uint32_t(std::min(int(S) - 2, std::max(0, env_int("RT_SPEC_HEAVY",
-                                                                                                  int(S - 1) / 20))))
+                          uint32_t(o.spec_probe),
+                          S > 2 && groups == 1 ? uint32_t(std::min(int(S) - 2, o.spec_heavy >= 0 ? o.spec_heavy
+                                                                                                : int(S - 1) / 20))
                                                : 0u};
     s->launch_seq = 0;
 #ifdef RT_DIAG
@@ -796,10 +833,10 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         s->sp_dbg_n = size_t(P) * S;
     }
 #endif
-    const bool alt_on = env_int("RT_SPEC_ALT", 1) != 0 && s->n_alt_vals > 1 && S > 1;
+    const bool alt_on = o.spec_alt != 0 && s->n_alt_vals > 1 && S > 1;
     if (alt_on) {  // alternative runs (DESIGN.md "Alternative runs")
         // slots pack as first | count << 24 in the hash (alt_find): the cap stays below 2^24
-        const uint32_t cap = uint32_t(std::min(1 << 24, std::max(1024, env_int("RT_SPEC_ALT_CAP", 1 << 17))));
+        const uint32_t cap = uint32_t(o.spec_alt_cap);
         if (s->alt_cap != cap) {
             for (DevBuf *b : {&s->sp_alt, &s->sp_alt_hash, &s->sp_alt_count}) { b->~DevBuf(); new (b) DevBuf(); }
             HIP_OK(s->sp_alt.alloc(size_t(cap) * sizeof(rtk::AltRec)));
@@ -814,15 +851,15 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         R.alt_count = s->sp_alt_count.as<unsigned>();
         R.alt_cap = cap;
         R.alt_hcap = cap * 2;
-        R.alt_min_seg = uint32_t(std::max(1, env_int("RT_SPEC_ALT_SEG", 16384)));
+        R.alt_min_seg = uint32_t(o.spec_alt_seg);
         for (int v = 0; v < 8; v++) R.alt_vals[v] = s->alt_vals[v];
         R.n_alt_vals = s->n_alt_vals;
     }
-    // alternatives are spawned after the checkpoint rounds and, with RT_SPEC_ALT_EVERY = k > 0,
+    // alternatives are spawned after the checkpoint rounds and, with spec_alt_every = k > 0,
     // after every k-th budgeted tail round too (measured: once is best on the bench frame)
-    const int alt_every = std::max(0, env_int("RT_SPEC_ALT_EVERY", 0));
+    const int alt_every = o.spec_alt_every;
     R.front2 = s->sp_front.as<uint4>() + P;  // the anchored scan's secondary frontier
-    R.scan_max = uint32_t(std::max(0, env_int("RT_SPEC_SCAN", 128)));
+    R.scan_max = uint32_t(o.spec_scan);
     if (R.scan_max == 0) R.front2 = nullptr;
 #ifdef RT_DIAG  // diagnostic builds only: copy one render's exact per-sample state into the next
     if (env_int("RT_SPEC_ORACLE", 0) != 0) {  // (see SpecRecs::exact)
@@ -841,7 +878,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
 #endif
     rtk::IowScene scene{s->hot.as<float>(), s->cold.as<float>(), s->n, s->nodes.as<float4>(),
                         s->sunflower.as<float>(), s->fib.as<float>(), s->ring.as<int>(), s->root_link,
-                                 s->obox.as<float4>(), s->n_wide};
+                        s->obox.as<float4>(), s->n_wide, o.iow_lds_bvh};
     // caps in 256-lane slots; the LDS-BVH kernels run 768-lane blocks
     const bool lds = rtk::iow_lds(scene);
     const int cap_s = s->cus * (lds ? 3 * rtk::resident_blocks_per_cu(10) : rtk::resident_blocks_per_cu(5));
@@ -850,11 +887,11 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // one compacted pass on a stream with its own queue counter and continuation buffers: the
     // first launch takes `n0` units, resume launches take the parked lanes
     struct Lane { hipStream_t st; unsigned *counter; const DevBuf *cont; unsigned *cnt; };
-    const bool spread_last = env_int("RT_SPEC_SPREAD", 1) != 0;
+    const bool spread_last = o.spec_spread != 0;
     // the first launch of the next pass takes its sorted head one unit per wave (Cont.solo_n)
     uint32_t solo_first = 0;
     auto pass = [&](const Lane &q, auto &&launch, uint32_t n0, int cap) {
-        const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap * rtk::kBlock / 8)));
+        const uint32_t park_min = park_min_of(s, cap);
         for (int r = 0; r <= rounds && e == hipSuccess; r++) {
             rtk::Cont ct{};
             uint32_t n_units = n0;
@@ -879,24 +916,23 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             return spec_launch(s, f, scene, RR, mode, ct, n, q.counter, cap_s, q.st);
         };
     };
-    // Checkpoint rounds (RT_SPEC_ROUNDS = k > 0): the speculative pass over samples 1.. runs as k
+    // Checkpoint rounds (spec_rounds = k > 0): the speculative pass over samples 1.. runs as k
     // launches, each taking the lanes the previous one parked plus the next slice of fresh units
     // and parking every lane once its queue drains; between launches the pixel frontiers advance
     // and mispredicted samples at a frontier are re-run at once (k_iow03_frontier,
     // k_iow03_fixf).  The tail then runs as before (compaction rounds).
-    const int ckpt = S > 1 ? std::max(0, std::min(kCountSlots - 16, env_int("RT_SPEC_ROUNDS", 24))) : 0;
+    const int ckpt = S > 1 ? std::min(kCountSlots - 16, o.spec_rounds) : 0;
     // Heavy-first (R.n_heavy = K > 0): round 0 runs every sample of every R.probe_stride-th pixel;
     // the measured cost per sample index orders the indices (k_sample_rank); the next rounds run
     // the K costliest indices for every pixel (sample-major, so the long samples start first);
     // the pixels are then re-sorted by the rays of those samples and the remaining indices run
     // pixel-major (so each heavy pixel's frontier reaches its long samples early).
-    // Budgeted tail rounds (RT_SPEC_TAIL_ROUNDS, RT_SPEC_TAIL_BUDGET segments each; DESIGN.md
+    // Budgeted tail rounds (spec_tail_rounds, spec_tail_budget segments each; DESIGN.md
     // "Budgeted tail"): the frontier advances between them, so mispredicted samples re-run while
     // the long ones still run instead of in a re-run pass after them.
-    // exact restarts go on down their pixel's chain of mispredicted samples (RT_SPEC_CHAIN)
-    const int chain = env_int("RT_SPEC_CHAIN", 1) != 0 ? 1 : 0;
-    const int tail_budgeted =
-        ckpt > 0 ? std::max(0, std::min(kCountSlots - 16 - ckpt - rounds, env_int("RT_SPEC_TAIL_ROUNDS", 60))) : 0;
+    // exact restarts go on down their pixel's chain of mispredicted samples (spec_chain)
+    const int chain = o.spec_chain != 0 ? 1 : 0;
+    const int tail_budgeted = ckpt > 0 ? std::max(0, std::min(kCountSlots - 16 - ckpt - rounds, o.spec_tail_rounds)) : 0;
     auto ckpt_pass = [&](const Lane &q, const rtk::SpecRecs &RG, uint32_t n_fresh) {
         const uint32_t slots = uint32_t(s->blocks_cap) * rtk::kBlock, cap_cont = 2 * slots;
         struct Rnd { int mode; uint32_t lo, hi; };
@@ -930,7 +966,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             ct.fresh_lo = plan[size_t(r)].lo;
             ct.fresh_hi = plan[size_t(r)].hi;
             if (r == ckpt - 1) ct.park_below = 0;  // the last round compacts as the tail rounds do
-            ct.park_min = r == ckpt - 1 ? uint32_t(std::max(0, env_int("RT_PARK_MIN", cap_s * rtk::kBlock / 8))) : 0u;
+            ct.park_min = r == ckpt - 1 ? park_min_of(s, cap_s) : 0u;
             e = hipMemsetAsync(ct.out_count, 0, sizeof(unsigned), q.st);
             if (e == hipSuccess) e = spec_launch(s, f, scene, RG, rtk::kSpecRest, ct, uint32_t(cap_s) * rtk::kBlock,
                                                  q.counter, cap_s, q.st);
@@ -953,12 +989,12 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             b = r & 1;
         }
         // tail: resume rounds with compaction; the first `tb` of them are budgeted (every unit
-        // parks after RT_SPEC_TAIL_BUDGET segments) and followed by the frontier, so a sample found
+        // parks after spec_tail_budget segments) and followed by the frontier, so a sample found
         // mispredicted re-runs while the long samples are still running; the last round runs to
         // completion
-        const uint32_t park_min = uint32_t(std::max(0, env_int("RT_PARK_MIN", cap_s * rtk::kBlock / 8)));
+        const uint32_t park_min = park_min_of(s, cap_s);
         const int tb = tail_budgeted;
-        const uint32_t budget = uint32_t(std::max(1, env_int("RT_SPEC_TAIL_BUDGET", 3072)));
+        const uint32_t budget = uint32_t(o.spec_tail_budget);
         const int n_tail = tb + rounds;
         const bool spread = spread_last;
         for (int t = 0; t <= n_tail && e == hipSuccess; t++) {
@@ -990,6 +1026,8 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         }
     };
     s->last_kernel = lds ? "k_iow03sL" : "k_iow03s";
+    s->last_path.order = 4;
+    s->last_path.iow_bvh = s->root_link ? (lds ? 2 : 1) : 0;
     s->last_launches = (1 + rounds) * (1 + groups * ((S > 1 ? 1 : 0) + iters)) +
                        (ckpt > 0 ? groups * (ckpt + tail_budgeted) : 0);
     s->last_chunks = 1;
@@ -1000,10 +1038,10 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     if (e == hipSuccess) pass(L0, spec(R, rtk::kSpecFirst), P, cap_s);
     if (S > 1) {
         // Sample 1 starts from sample 0's final stack (exact: its written entries, 0 elsewhere).
-        // From RT_SPEC_PRIOR_FROM (2) on every entry is guessed as the scene's most common RI
+        // From spec_prior_from (2) on every entry is guessed as the scene's most common RI
         // The prior misses far less often (the re-run pass re-traces ~1% of the rays instead of
         // ~20% with zeros); the dependent chains it forms are cheap for the validating pass.
-        const uint32_t prior_from = uint32_t(std::max(1, env_int("RT_SPEC_PRIOR_FROM", 2)));
+        const uint32_t prior_from = uint32_t(o.spec_prior_from);
         if (e == hipSuccess)
             e = rtk::launch_iow03_prep(f, R, s->ws_cost.as<unsigned>(), s->ri_prior, prior_from, st);
         if (e == hipSuccess)
@@ -1014,7 +1052,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // (2) one independent pipeline per pixel group, each on its own stream, so one group's long
     // samples overlap the other groups' work: speculative pass over samples 1.., resolve and
     // re-run passes (the first list longest first), final resolve, sequential leftovers
-    const bool sort_first = env_int("RT_SPEC_SORT", 1) != 0;
+    const bool sort_first = o.spec_sort != 0;
     for (int g = 0; g < groups && e == hipSuccess; g++) {
         auto &GL = *s->lanes[size_t(g)];
         const Lane L{GL.st, GL.counter.as<unsigned>(), GL.cont, GL.cont_count.as<unsigned>()};
@@ -1046,7 +1084,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                     e = rtk::sort_pairs_desc(k1, k2, RG.list, l2, nmax, GL.temp.p, GL.temp_bytes, 24, L.st);
                 rtk::SpecRecs R2 = RG;
                 R2.list = l2;
-                solo_first = uint32_t(std::max(0, env_int("RT_SOLO", 4096)));
+                solo_first = uint32_t(o.spec_solo);
                 if (e == hipSuccess) pass(L, spec(R2, rtk::kSpecList), uint32_t(nmax), cap_s);
                 solo_first = 0;
             } else if (e == hipSuccess) pass(L, spec(RG, rtk::kSpecList), uint32_t(nmax), cap_s);
@@ -1062,7 +1100,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         ch.order = RG.fb_list;
         ch.order_count = RG.fb_count;
         ch.per_unit_begin = 1;
-        if (env_int("RT_SPEC_VALIDATE", 1) != 0) {  // reuse the records that are still exact
+        if (o.spec_validate != 0) {  // reuse the records that are still exact
             ch.rec_col = R.col; ch.rec_fin = R.fin; ch.rec_assume = R.assume; ch.rec_ctr = R.ctr;
             ch.rec_P = P;
         }
@@ -1080,7 +1118,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     return RT_OK;
 }
 
-// Pixel beams (DESIGN.md §5 "Pixel beams"; RT_INW_BEAM=0 turns them off).  Sample s of a pixel
+// Pixel beams (DESIGN.md §5 "Pixel beams"; rt_options.inw_beams = 0 turns them off).  Sample s of a pixel
 // starts its primary ray one unit behind tip = C0 + rr * ox + ru * oy (C0 = co + cd, |rr|, |ru|
 // <= 1, |ox| + |oy| <= aperture / 2 * sf_max) and aims it at F = co + cd * focus.  With
 // L = |F - C0| = focus - 1, the point of that ray at fraction u of the way from tip to F is
@@ -1093,7 +1131,7 @@ int set_beam(rt_dev_scene *s, const rtk::Frame &f, rtk::InwScene &sc) {
     const double units = double(rtk::units_of(f));
     const double ap = std::fabs(double(f.aperture)), L = double(f.focus) - 1.0;
     const double d0 = 0.5 * ap * double(s->sf_max) * (1.0 + 1e-4) + 1e-6;
-    if (env_int("RT_INW_BEAM", 1) == 0 || !sc.wnodes || f.n_focus > 0 || !(L > 8.0 * d0 + 1e-3) ||
+    if (!s->opt.inw_beams || !sc.wnodes || f.n_focus > 0 || !(L > 8.0 * d0 + 1e-3) ||
         units * cap * 8.0 > 2.0e9)
         return RT_OK;
     const double cam = std::sqrt(double(f.pos[0]) * f.pos[0] + double(f.pos[1]) * f.pos[1] + double(f.pos[2]) * f.pos[2]);
@@ -1105,15 +1143,19 @@ int set_beam(rt_dev_scene *s, const rtk::Frame &f, rtk::InwScene &sc) {
     const double r = d0 * std::fmax(1.0 - tmin / Ll, std::fabs(1.0 - tfar / Ll));
     const double R = r + 2e-3 + 1e-5 * (cam + tfar);
     const size_t need = size_t(units) * cap * sizeof(uint2), need_n = size_t(units) * 2 * sizeof(uint32_t);
+    // the lists are an optional speed-up: on a device short of memory the frame runs without them
+    size_t free_b = 0, total_b = 0;
+    const size_t grow = (s->inw_beam.bytes < need ? need : 0) + (s->inw_beam_n.bytes < need_n ? need_n : 0);
+    if (grow && (hipMemGetInfo(&free_b, &total_b) != hipSuccess || grow > free_b / 2)) return RT_OK;
     if (s->inw_beam.bytes < need) {
         s->inw_beam.~DevBuf();
         new (&s->inw_beam) DevBuf();
-        if (s->inw_beam.alloc(need) != hipSuccess) return RT_E_HIP;
+        if (s->inw_beam.alloc(need) != hipSuccess) { (void)hipGetLastError(); s->inw_beam.bytes = 0; return RT_OK; }
     }
     if (s->inw_beam_n.bytes < need_n) {
         s->inw_beam_n.~DevBuf();
         new (&s->inw_beam_n) DevBuf();
-        if (s->inw_beam_n.alloc(need_n) != hipSuccess) return RT_E_HIP;
+        if (s->inw_beam_n.alloc(need_n) != hipSuccess) { (void)hipGetLastError(); s->inw_beam_n.bytes = 0; return RT_OK; }
     }
     sc.beam = s->inw_beam.as<uint2>();
     sc.beam_n = s->inw_beam_n.as<uint32_t>();
@@ -1129,18 +1171,15 @@ int set_beam(rt_dev_scene *s, const rtk::Frame &f, rtk::InwScene &sc) {
 // INW with on-chip End() folds (DESIGN.md §5 "INW: on-chip End() folds"): the probe, then
 // k_inw_pm and k_inw_sm (one of them exits at once), persistent launches of one frame.  The
 // launches are bracketed by HIP events on their stream when kernel timing is on
-// (rt_debug_kernel_time).  RT_INW_ORDER = 1 / 2 forces pixel- / sample-major (tests, A/B);
-// RT_INW_RING_PM / RT_INW_RING_SM set the fold windows (samples per wave, powers of two).
+// (rt_debug_kernel_time).  rt_options.inw_order = 1 / 2 forces pixel- / sample-major (tests, A/B);
+// inw_ring_pm / inw_ring_sm set the fold windows (samples per wave, powers of two).
 int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
+    const rt_options &o = s->opt;
     const int blocks = s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 16 : 15);
-    auto ring_of = [](const char *name, uint32_t dflt) {
-        const int r = env_int(name, 0);
-        return (r >= 64 && (r & (r - 1)) == 0) ? uint32_t(r) : dflt;
-    };
-    const uint32_t ring_pm = ring_of("RT_INW_RING_PM", 1024), ring_sm = ring_of("RT_INW_RING_SM", 256);
+    const uint32_t ring_pm = uint32_t(o.inw_ring_pm), ring_sm = uint32_t(o.inw_ring_sm);
     // the top of the wide BVH staged in LDS (768-lane blocks, 3 waves per SIMD);
-    // RT_INW_LDS=0: 256-lane blocks reading every node from L1 / L2 (A/B)
-    const int blocks_ln = env_int("RT_INW_LDS", 1) == 1 && s->dfs_high
+    // inw_lds_nodes = 0: 256-lane blocks reading every node from L1 / L2 (A/B)
+    const int blocks_ln = o.inw_lds_nodes && s->dfs_high
                               ? s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 18 : 17) : 0;
     const size_t waves = std::max(size_t(blocks) * (rtk::kBlock / 64), size_t(blocks_ln) * (3 * rtk::kBlock / 64));
     const size_t ring_bytes = waves * std::max(ring_pm, ring_sm) * sizeof(float4);
@@ -1159,10 +1198,12 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     {
         const float cam = std::fmax(std::fabs(f.pos[0]), std::fmax(std::fabs(f.pos[1]), std::fabs(f.pos[2]))) +
                           2.0f + std::fabs(f.aperture);
-        sc.fused = (env_int("RT_INW_FMA", 1) != 0 && f.n_focus == 0 && std::fmax(cam, s->wbound) <= 1000.0f) ? 1 : 0;
+        sc.fused = (o.inw_fused_cull && f.n_focus == 0 && std::fmax(cam, s->wbound) <= 1000.0f) ? 1 : 0;
     }
-    const int ord = env_int("RT_INW_ORDER", 0);
-    const uint32_t force = (ord == 1 || ord == 2) ? uint32_t(ord) : 0u;
+    const uint32_t force = (o.inw_order == 1 || o.inw_order == 2) ? uint32_t(o.inw_order) : 0u;
+    s->last_force = force;
+    s->last_ring[0] = ring_pm;
+    s->last_ring[1] = ring_sm;
     s->last_kernel = s->layout == 4 ? "k_inw_fold<true>" : "k_inw_fold<false>";
     s->last_ln = blocks_ln > 0;
     s->last_fu = s->last_ln && sc.fused;
@@ -1181,9 +1222,9 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         s->kt_used = 1;
     }
     // the rings are reset first, so the events bracket the probe and the two fold kernels
-    // claim order, costliest blocks first (RT_INW_COST=0: unit order)
+    // claim order, costliest blocks first (inw_claim_order = 0: unit order)
     uint32_t *cost = nullptr;
-    if (env_int("RT_INW_COST", 1) != 0) {
+    if (o.inw_claim_order) {
         const size_t need = (2 * size_t(rtk::units_of(f) / 64) + 256) * sizeof(uint32_t);
         if (s->inw_cost.bytes < need) {
             s->inw_cost.~DevBuf();
@@ -1193,6 +1234,18 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         cost = s->inw_cost.as<uint32_t>();
     }
     if (int rc = set_beam(s, f, sc); rc != RT_OK) return rc;
+    {  // the path this frame takes (rt_debug_path; the order is resolved at query time)
+        rt_path_info &P = s->last_path;
+        P.launches = 1;
+        P.order_forced = force != 0;
+        P.order = int(force);
+        P.wide_walk = sc.wnodes != nullptr;
+        P.beams = sc.beam != nullptr;
+        P.ri_grid = sc.ri_cells != nullptr;
+        P.fused_cull = s->last_fu ? 1 : 0;
+        P.lds_nodes = s->last_ln ? 1 : 0;
+        P.claim_order = cost != nullptr;
+    }
     e = hipMemsetAsync(s->inw_ring.p, 0xff, ring_bytes, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->first, st);
     if (e == hipSuccess)
@@ -1332,6 +1385,46 @@ extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
+void rt_options_default(rt_options *o) {
+    if (o) *o = default_options();
+}
+
+int rt_options_set(const rt_options *o) {
+    if (!options_ok(o)) return RT_E_ARG;
+    g_opt = *o;
+    return RT_OK;
+}
+
+int rt_options_get(rt_options *o) {
+    if (!o) return RT_E_ARG;
+    *o = g_opt;
+    return RT_OK;
+}
+
+int rt_dev_scene_set_options(rt_dev_scene *s, const rt_options *o) {
+    if (!s || !options_ok(o)) return RT_E_ARG;
+    const int wide = s->opt.inw_wide_walk, linear = s->opt.iow_linear;  // [build] options stay
+    s->opt = *o;
+    s->opt.inw_wide_walk = wide;
+    s->opt.iow_linear = linear;
+    return RT_OK;
+}
+
+int rt_debug_path(rt_dev_scene *s, rt_path_info *out) {
+    if (!s || !out) return RT_E_ARG;
+    char name[64] = {0};
+    const int n = rt_debug_launches(s, name, int(sizeof(name)));  // resolves the fold kernel (synchronises)
+    if (n < 0) return n;
+    rt_path_info P = s->last_path;
+    std::memcpy(P.kernel, name, sizeof(P.kernel));
+    P.launches = n;
+    if (std::strncmp(name, "k_inw_pm", 8) == 0) { P.order = 1; P.ring_entries = int(s->last_ring[0]); }
+    else if (std::strncmp(name, "k_inw_sm", 8) == 0) { P.order = 2; P.ring_entries = int(s->last_ring[1]); }
+    if (P.order != 1) { P.beams = 0; P.claim_order = 0; }  // both serve the pixel-major kernel only
+    *out = P;
+    return RT_OK;
+}
+
 // Diagnostics (not part of the reference's surface): pass a device buffer of 8 u64 to make
 // the kernels tally lane occupancy per phase; NULL turns it off.
 int rt_debug_pixel_rays(uint32_t *d_buf) {
@@ -1433,7 +1526,7 @@ int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {
         uint32_t m[2] = {0, 0};
         HIP_OK(hipDeviceSynchronize());
         HIP_OK(hipMemcpy(m, s->inw_mode.p, sizeof(m), hipMemcpyDeviceToHost));
-        const int ord = env_int("RT_INW_ORDER", 0);
+        const uint32_t ord = s->last_force;  // the order the launch used (0: the probe's verdict)
         const bool sm = ord == 2 || (ord != 1 && m[0] > 0 && 2 * m[1] >= m[0]);
         // the template instance's name as rocprofv3 prints it, every argument: every template argument: <LIGHTS, LN (LDS-staged BVH top), FU (fused cull)>
         static const char *names[2][2][2] = {

@@ -2907,7 +2907,10 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         if (qdone && ji == nclaimed && gf == gi && __ballot(busy) == 0) break;
         // ---- one ray segment per busy lane (samples are independent invocations)
         INW_T0(t_seg);
-        if (busy) inw_segment<LIGHTS, LN, FU>(S, f, K, s, col, dep, c, bu);
+        if (busy) {
+            inw_segment<LIGHTS, LN, FU>(S, f, K, s, col, dep, c, bu);
+            if (f.px_rays) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
+        }
         INW_CYC(c, 4, t_seg);
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
@@ -3065,7 +3068,10 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             }
         }
         if (qdone && bi == nclaimed && bmin == nclaimed && __ballot(busy) == 0) break;
-        if (busy) inw_segment<LIGHTS, LN, FU>(S, f, K, s, col, dep, c);
+        if (busy) {
+            inw_segment<LIGHTS, LN, FU>(S, f, K, s, col, dep, c);
+            if (f.px_rays) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
+        }
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
                                         __uint_as_float(g));
@@ -3092,15 +3098,13 @@ static dim3 grid_iow01(const Frame &f) {
     return dim3((unsigned)(((f.tw + 15) >> 4) * ((f.th + 15) >> 4)));
 }
 
-bool iow_narrow(const Frame &f) {
-    const char *v = std::getenv("RT_IOW_NARROW");  // A/B switch (measured slower: VGPR spills)
-    return f.max_bounces <= 255 && v && v[0] == '1';
+bool iow_narrow(const Frame &f) {  // A/B switch (measured slower: VGPR spills)
+    return f.max_bounces <= 255 && f.narrow != 0;
 }
 
-// the LDS-node kernels (k_iow03L / k_iow03sL) when the BVH fits and RT_IOW_LDS is not 0
+// the LDS-node kernels (k_iow03L / k_iow03sL) when the BVH fits and rt_options.iow_lds_bvh is on
 bool iow_lds(const IowScene &sc) {
-    static const int on = [] { const char *v = std::getenv("RT_IOW_LDS"); return (v && v[0] == '0') ? 0 : 1; }();
-    return on && sc.nodes != nullptr && sc.n_nodes > 0 && sc.n_nodes <= (uint32_t)kIowLdsNodes;
+    return sc.lds_on && sc.nodes != nullptr && sc.n_nodes > 0 && sc.n_nodes <= (uint32_t)kIowLdsNodes;
 }
 
 int resident_blocks_per_cu(int kind) {
@@ -3357,6 +3361,16 @@ hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uin
         if (r < 64 || (r & (r - 1))) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(mode, 0, 2 * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
+    // the probe first: the claim-order and beam kernels below read its verdict and exit at once
+    // on a sample-major frame
+    if (force == 0) {
+        const uint32_t nblk = units_of(f) / 64u, waves = 1024u;  // ~1024 probe blocks of 8x8 pixels
+        const uint32_t stride = nblk > waves ? nblk / waves : 1u, nw = (nblk + stride - 1u) / stride;
+        const dim3 g((nw + 3u) / 4u);
+        if (sc.layout == 4) hipLaunchKernelGGL(k_inw_probe<true>, g, dim3(kBlock), 0, s, f, sc, stride, mode);
+        else hipLaunchKernelGGL(k_inw_probe<false>, g, dim3(kBlock), 0, s, f, sc, stride, mode);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     // claim order of k_inw_pm (cost: 2 * nblk + 256 uints, or null = unit order)
     const uint32_t *border = nullptr;
     if (cost && units_of(f) >= 64u) {
@@ -3371,14 +3385,6 @@ hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uin
                            order, nblk, mode, force);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         border = order;
-    }
-    if (force == 0) {
-        const uint32_t nblk = units_of(f) / 64u, waves = 1024u;  // ~1024 probe blocks of 8x8 pixels
-        const uint32_t stride = nblk > waves ? nblk / waves : 1u, nw = (nblk + stride - 1u) / stride;
-        const dim3 g((nw + 3u) / 4u);
-        if (sc.layout == 4) hipLaunchKernelGGL(k_inw_probe<true>, g, dim3(kBlock), 0, s, f, sc, stride, mode);
-        else hipLaunchKernelGGL(k_inw_probe<false>, g, dim3(kBlock), 0, s, f, sc, stride, mode);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (sc.beam && (e = launch_inw_beam(f, sc, mode, force, s)) != hipSuccess) return e;
     for (int k = 0; k < 2; k++) {  // (pm, then sm) each with its own queue counter

@@ -21,13 +21,15 @@ struct Frame {
     float sphere[4];    // IOW-01 only
     unsigned long long *dbg;  // optional lane-occupancy counters (kDbg* slots), null in production
     int leaf_batch;           // IOW-03 walk: test postponed leaves once this many lanes hold one
-    unsigned *px_rays;        // optional: rays cast per work unit, written when its pixel completes
+    unsigned *px_rays;        // optional: rays cast per work unit, written when its pixel completes (IOW);
+                              // INW fold kernels add one per segment at the output pixel's index
     int coop_max;             // IOW-03: wave-cooperative closest hits when at most this many lanes trace
     int dbg_first_stale;      // diagnostics: record the segment of a sample's first stale read (corrupts drops)
     // INW-01 MULTIFOCUS (01_BVH...glsl:388-404, 505-549; "#if MULTIFOCUS" in the reference):
     // n_focus = 0 is the single-focus camera the reference builds, 1..9 the lens chain
     int n_focus;
     float focus_list[9];
+    int narrow;               // rt_options.iow_narrow (host side: iow_narrow)
 };
 // lane-occupancy counters (per wave-iteration: 1 and popcount of the participating lanes)
 enum { kDbgOuter = 0, kDbgOuterLanes, kDbgTrav, kDbgTravLanes, kDbgLeaf, kDbgLeafLanes, kDbgSeg, kDbgSegLanes,
@@ -54,6 +56,7 @@ struct IowScene {
     int root_link;           // link of the BVH root (wide node 0 -> 1)
     const float4 *obox;      // the BVH leaves' conservative boxes: n float4 (lo.xyz, hi.x), n float2 (hi.yz); or null
     uint32_t n_nodes;        // 4-wide BVH nodes
+    int lds_on;              // rt_options.iow_lds_bvh: the LDS-staged kernels may run (iow_lds)
 };
 struct InwScene {
     const float4 *hot;       // n * 7 float4
@@ -291,9 +294,9 @@ hipError_t launch_inw_beam(const Frame &f, const InwScene &sc, const uint32_t *m
 int resident_blocks_per_cu(int kind);  // 5 = sample-parallel IOW-03, 6/7 = sample-parallel INW 1/4,
                                        // 8 = asynchronous-window IOW-03
 // IOW-03 kernel variant for this frame: narrow (byte bounce counts, 12-deep BVH stack, 4 waves
-// per SIMD with spills) when RT_IOW_NARROW=1 and u_NumOfBounce <= 255; wide otherwise
+// per SIMD with spills) when rt_options.iow_narrow and u_NumOfBounce <= 255; wide otherwise
 bool iow_narrow(const Frame &f);
-bool iow_lds(const IowScene &sc);  // k_iow03L / k_iow03sL (BVH in LDS) apply; their blocks_cap counts 256-lane slots
+bool iow_lds(const IowScene &sc);  // k_iow03L / k_iow03sL (BVH in LDS) apply (sc.lds_on and it fits); their blocks_cap counts 256-lane slots
 // order[i] = unit ids sorted by cost, most expensive first (hipcub radix sort)
 hipError_t sort_units_by_cost(const unsigned *cost, unsigned *keys_tmp, const unsigned *iota, unsigned *order,
                               uint32_t n, void *temp, size_t temp_bytes, hipStream_t s);

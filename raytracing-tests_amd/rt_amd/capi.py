@@ -23,7 +23,7 @@ RT_STAGE_IOW02 = 2
 RT_IOW_CUBOID, RT_IOW_ELLIPSOID = 1, 2
 RT_INW_ELLIPSOID, RT_INW_CUBOID = 1, 2
 
-ABI_VERSION = 1  # RT_ABI_VERSION, include/rt_hip.h
+ABI_VERSION = 2  # RT_ABI_VERSION, include/rt_hip.h
 
 PRESET_IOW03_REF3 = 1
 PRESET_IOW03_FINAL = 2
@@ -68,6 +68,36 @@ class RtCamDesc(C.Structure):
 
 class RtTexture(C.Structure):
     _fields_ = [("texels", C.c_void_p), ("width", C.c_int), ("height", C.c_int), ("channels", C.c_int)]
+
+
+class RtOptions(C.Structure):
+    """rt_options (include/rt_hip.h): the exact strategy switches of the render path."""
+    _fields_ = [("size", C.c_uint32)] + [(n, C.c_int) for n in (
+        "inw_wide_walk", "inw_order", "inw_beams", "inw_ri_grid", "inw_lds_nodes", "inw_fused_cull",
+        "inw_claim_order", "inw_ring_pm", "inw_ring_sm",
+        "iow_spec", "iow_linear", "iow_narrow", "iow_lds_bvh", "iow_leaf_batch", "iow_coop_max", "iow_chunks_lpt",
+        "rounds_seq", "rounds_spec", "park_min",
+        "spec_iters", "spec_probe", "spec_heavy", "spec_rounds", "spec_tail_rounds", "spec_tail_budget", "spec_scan",
+        "spec_chain", "spec_alt", "spec_alt_cap", "spec_alt_seg", "spec_alt_every", "spec_spread", "spec_prior_from",
+        "spec_sort", "spec_solo", "spec_validate")] + [("spec_max_gb", C.c_double)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "size"}
+
+
+class RtPathInfo(C.Structure):
+    """rt_path_info (include/rt_hip.h): what a scene's last render ran."""
+    _fields_ = [("kernel", C.c_char * 64), ("launches", C.c_int), ("order", C.c_int), ("order_forced", C.c_int),
+                ("wide_walk", C.c_int), ("beams", C.c_int), ("ri_grid", C.c_int), ("fused_cull", C.c_int),
+                ("lds_nodes", C.c_int), ("claim_order", C.c_int), ("ring_entries", C.c_int), ("iow_bvh", C.c_int)]
+
+    ORDERS = {0: None, 1: "pixel-major", 2: "sample-major", 3: "per-pixel", 4: "sample-parallel", 5: "sequential"}
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["kernel"] = self.kernel.decode()
+        d["order"] = self.ORDERS.get(self.order, self.order)
+        return d
 
 
 _FP = C.POINTER(C.c_float)
@@ -140,6 +170,11 @@ SIGNATURES = {
     "rt_debug_spec_list_hist": (C.c_int, [C.c_void_p, _U64P]),
     "rt_debug_spec_list_stale": (C.c_int, [C.c_void_p, _U64P]),
     "rt_debug_spec_dump": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "rt_options_default": (None, [C.POINTER(RtOptions)]),
+    "rt_options_set": (C.c_int, [C.POINTER(RtOptions)]),
+    "rt_options_get": (C.c_int, [C.POINTER(RtOptions)]),
+    "rt_dev_scene_set_options": (C.c_int, [C.c_void_p, C.POINTER(RtOptions)]),
+    "rt_debug_path": (C.c_int, [C.c_void_p, C.POINTER(RtPathInfo)]),
 }
 
 _lib = None
@@ -179,6 +214,51 @@ def fptr(a: np.ndarray | None):
 def check(rc: int, what: str) -> None:
     if rc != RT_OK:
         raise RuntimeError(f"{what} failed with status {rc}")
+
+
+# ---------------------------------------------------------------------------- options
+def default_options() -> RtOptions:
+    o = RtOptions()
+    load().rt_options_default(C.byref(o))
+    return o
+
+
+def get_options() -> RtOptions:
+    o = RtOptions()
+    check(load().rt_options_get(C.byref(o)), "rt_options_get")
+    return o
+
+
+def set_options(o: RtOptions) -> None:
+    check(load().rt_options_set(C.byref(o)), "rt_options_set")
+
+
+class options:
+    """Context manager: the library-wide rt_options with some fields changed, e.g.
+    `with R.options(inw_order=2, inw_ring_sm=64): R.render(sc)`; restores the previous ones."""
+
+    def __init__(self, **fields):
+        self.fields = fields
+
+    def __enter__(self) -> RtOptions:
+        self.prev = get_options()
+        o = RtOptions.from_buffer_copy(self.prev)
+        for k, v in self.fields.items():
+            if k not in dict(RtOptions._fields_):
+                raise KeyError(f"unknown rt_options field {k!r}")
+            setattr(o, k, v)
+        set_options(o)
+        return o
+
+    def __exit__(self, *exc) -> None:
+        set_options(self.prev)
+
+
+def debug_path(scene_handle) -> dict:
+    """rt_debug_path of a device scene: the kernel and exact shortcuts of its last render."""
+    p = RtPathInfo()
+    check(load().rt_debug_path(scene_handle, C.byref(p)), "rt_debug_path")
+    return p.as_dict()
 
 
 # ----------------------------------------------------------------------------- scenes

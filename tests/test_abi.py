@@ -32,7 +32,52 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert R.load().rt_abi_version() == 1
+    assert R.load().rt_abi_version() == R.ABI_VERSION == 2
+
+
+def test_options_roundtrip_and_validation():
+    """rt_options: the defaults are the measured-best settings, set / get round-trip, and
+    out-of-range values are rejected (the options stay as they were)."""
+    lib = R.load()
+    d = R.default_options()
+    assert d.size == C.sizeof(R.RtOptions)
+    assert (d.inw_wide_walk, d.inw_order, d.inw_beams, d.inw_ring_pm, d.inw_ring_sm) == (1, 0, 1, 1024, 256)
+    assert (d.iow_spec, d.spec_rounds, d.spec_tail_rounds, d.spec_tail_budget) == (1, 24, 60, 3072)
+    with R.options(inw_order=2, spec_iters=3) as o:
+        g = R.get_options()
+        assert g.inw_order == 2 and g.spec_iters == 3 and g.as_dict() == o.as_dict()
+    assert R.get_options().as_dict() == d.as_dict()
+    for field, bad in (("inw_ring_pm", 100), ("inw_ring_sm", 32), ("inw_order", 3), ("rounds_seq", 15),
+                       ("iow_leaf_batch", 0), ("spec_alt_cap", 1), ("spec_max_gb", 0.0)):
+        o = R.default_options()
+        setattr(o, field, bad)
+        assert lib.rt_options_set(C.byref(o)) == R.RT_E_ARG, field
+    o = R.default_options()
+    o.size = 8
+    assert lib.rt_options_set(C.byref(o)) == R.RT_E_ARG
+    assert lib.rt_options_set(None) == R.RT_E_ARG
+    assert R.get_options().as_dict() == d.as_dict()
+    with pytest.raises(KeyError):
+        with R.options(no_such_option=1):
+            pass
+    assert lib.rt_dev_scene_set_options(None, C.byref(d)) == R.RT_E_ARG
+    assert lib.rt_debug_path(None, None) == R.RT_E_ARG
+
+
+def test_render_path_reads_no_environment():
+    """What the library runs is set through rt_options only: the product sources read no
+    environment variable outside the diagnostic builds (#ifdef RT_DIAG)."""
+    csrc = os.path.join(ROOT, "raytracing-tests_amd", "csrc")
+    for fn in sorted(os.listdir(csrc)):
+        depth, in_diag = 0, []
+        for i, line in enumerate(open(os.path.join(csrc, fn)), 1):
+            t = line.strip()
+            if t.startswith("#if"):
+                in_diag.append("RT_DIAG" in t)
+            elif t.startswith("#endif") and in_diag:
+                in_diag.pop()
+            if "getenv" in t and not t.startswith("//"):
+                assert any(in_diag), f"{fn}:{i}: getenv outside #ifdef RT_DIAG"
 
 
 def test_argument_validation_without_device():

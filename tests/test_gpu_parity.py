@@ -40,15 +40,15 @@ def test_iow01_c1_matches_oracle(gpu):
 
 @pytest.mark.parametrize("wide,order", [("1", "0"), ("0", "0"), ("1", "1"), ("1", "2")])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_render_matches_oracle(gpu, name, wide, order, monkeypatch):
-    """wide: RT_INW_FAST (the INW wide walk, 1, or the reference's LBVH walk, 0); order:
-    RT_INW_ORDER (0: the probe picks the INW fold kernel, 1: pixel-major, 2: sample-major)."""
-    monkeypatch.setenv("RT_INW_FAST", wide)  # read by the library when it builds the device scene
-    monkeypatch.setenv("RT_INW_ORDER", order)  # read at every render
+def test_render_matches_oracle(gpu, name, wide, order):
+    """wide: rt_options.inw_wide_walk (the INW wide walk, 1, or the reference's LBVH walk, 0);
+    order: rt_options.inw_order (0: the probe picks the INW fold kernel, 1: pixel-major, 2:
+    sample-major)."""
     sc = CASES[name]()
     if sc.stage == R.RT_STAGE_IOW03 and (wide == "0" or order != "0"):
-        pytest.skip("RT_INW_FAST / RT_INW_ORDER only switch the INW kernels")
-    g, gd, gst = R.render(sc)
+        pytest.skip("inw_wide_walk / inw_order only switch the INW kernels")
+    with R.options(inw_wide_walk=int(wide), inw_order=int(order)):
+        g, gd, gst = R.render(sc)
     o, od, ost = O.render(sc)
     c = _check(name, g, o)
     if gd is not None:
@@ -56,9 +56,9 @@ def test_render_matches_oracle(gpu, name, wide, order, monkeypatch):
     print(name, "gpu", {k: gst[k] for k in COUNTERS}, "ms %.2f" % gst["ms"])
     print(name, "cpu", {k: ost[k] for k in COUNTERS}, "ms %.2f" % ost["ms"])
     # IOW-03 walks a culling BVH instead of the reference's linear object loop, and INW's wide
-    # walk (RT_INW_FAST, default on) a 4-wide culling BVH instead of the reference's LBVH walk, so
+    # walk (inw_wide_walk, default on) a 4-wide culling BVH instead of the reference's LBVH walk, so
     # their node / primitive counts are their own; every ray-level counter must still match
-    # exactly.  With RT_INW_FAST=0 the INW kernels walk the LBVH as the reference does, and the
+    # exactly.  With inw_wide_walk=0 the INW kernels walk the LBVH as the reference does, and the
     # node and primitive counts match too.
     own = sc.stage == R.RT_STAGE_IOW03 or wide == "1"
     exact = ("segments", "shadow_queries", "stack_drops", "nan_drops") if own else COUNTERS

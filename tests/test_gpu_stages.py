@@ -31,11 +31,11 @@ def test_iow00_matches_oracle(gpu, wh):
 
 @pytest.mark.parametrize("wide", ["1", "0"])
 @pytest.mark.parametrize("name", sorted(S.IOW02_CASES) + sorted(S.MF_CASES))
-def test_stage_matches_oracle(gpu, name, wide, monkeypatch):
+def test_stage_matches_oracle(gpu, name, wide):
     if name in S.IOW02_CASES and wide == "0":
-        pytest.skip("RT_INW_FAST only switches the INW walk")
-    monkeypatch.setenv("RT_INW_FAST", wide)  # the MULTIFOCUS cases run the INW kernels
-    g, gd, gst = S.render_gpu(name)
+        pytest.skip("inw_wide_walk only switches the INW walk")
+    with R.options(inw_wide_walk=int(wide)):  # the MULTIFOCUS cases run the INW kernels
+        g, gd, gst = S.render_gpu(name)
     o, od, ost = S.render_oracle(name)
     _exact(name, g, o)
     if gd is not None:

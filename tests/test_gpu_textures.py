@@ -85,13 +85,12 @@ TEXTURED = [
 
 @pytest.mark.parametrize("name,preset,seed,w,h,spp,ids", TEXTURED, ids=[t[0] for t in TEXTURED])
 @pytest.mark.parametrize("order,wide", [("0", "1"), ("1", "1"), ("2", "1"), ("-1", "1"), ("0", "0")])
-def test_textured_render_matches_oracle(gpu, name, preset, seed, w, h, spp, ids, order, wide, monkeypatch):
-    """order: RT_INW_ORDER (0 the probe's pick, 1 / 2 the pixel- / sample-major fold, -1 the
-    per-pixel kernel k_inw); wide: RT_INW_FAST."""
-    monkeypatch.setenv("RT_INW_ORDER", order)  # read by the library at launch time
-    monkeypatch.setenv("RT_INW_FAST", wide)  # read when the device scene is built
+def test_textured_render_matches_oracle(gpu, name, preset, seed, w, h, spp, ids, order, wide):
+    """order: rt_options.inw_order (0 the probe's pick, 1 / 2 the pixel- / sample-major fold, -1 the
+    per-pixel kernel k_inw); wide: rt_options.inw_wide_walk."""
     sc = _textured_scene(preset, seed, w, h, spp, ids)
-    g, gd, gst = R.render(sc)
+    with R.options(inw_order=int(order), inw_wide_walk=int(wide)):
+        g, gd, gst = R.render(sc)
     o, od, ost = O.render(sc)
     assert _same(g, o), np.argwhere(~(g.view(np.uint32) == o.view(np.uint32)).all(axis=2))[:10].tolist()
     assert _same(gd, od)

@@ -4,7 +4,8 @@ O=gpurun_out/lone
 rm -rf $O && mkdir -p $O
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp && cd "$R"
-export RT_IOW_SPEC=0 RT_COOP=4
+# (tools/lone_pixel.py runs the sequential kernel with cooperative closest hits: rt_options
+# iow_spec = 0, iow_coop_max = 4)
 timeout -k 10 120 python3 tools/lone_pixel.py > $O/run.json 2> $O/run.err || exit 1
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_SMEM" \

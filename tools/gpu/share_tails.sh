@@ -8,6 +8,6 @@ for sh in 0/8 6/8; do
   t=$(echo $sh | tr '/' 'o')
   RT_HIP_LIB=$L/librt_hip_split.so timeout -k 10 200 python3 tools/inw_split.py c3 500 $sh > $O/split_$t.json 2>> $O/err.txt || exit 1
   RT_HIP_LIB=$L/librt_hip_c64s.so timeout -k 10 200 python3 tools/inw_split.py c3 500 $sh > $O/split_c64_$t.json 2>> $O/err.txt || exit 1
-  RT_INW_COST=0 RT_HIP_LIB=$L/librt_hip_split.so timeout -k 10 200 python3 tools/inw_split.py c3 500 $sh > $O/split_nocost_$t.json 2>> $O/err.txt || exit 1
+  RT_HIP_LIB=$L/librt_hip_split.so timeout -k 10 200 python3 tools/inw_split.py c3 500 $sh inw_claim_order=0 > $O/split_nocost_$t.json 2>> $O/err.txt || exit 1
 done
 RT_HIP_LIB=$L/librt_hip_c64s.so timeout -k 10 200 python3 tools/inw_split.py c3 500 > $O/split_c64_full.json 2>> $O/err.txt || exit 1

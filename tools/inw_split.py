@@ -25,6 +25,12 @@ import rt_amd as R  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 shard = sys.argv[3] if len(sys.argv) > 3 else ""
+if len(sys.argv) > 4:  # rt_options fields, FIELD=VALUE
+    o = R.get_options()
+    for kv in sys.argv[4:]:
+        k, v = kv.split("=", 1)
+        setattr(o, k, int(v))
+    R.set_options(o)
 over = {"spp": spp} if spp else {}
 sc = (R.make_scene(R.PRESET_INW01_RANDOM, 1234, 10_000, **over) if cfg == "c3"
       else R.make_scene(R.PRESET_INW04_CORNELL, 7, 0, **over))

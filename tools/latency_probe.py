@@ -14,16 +14,15 @@ pr = torch.zeros(units, dtype=torch.int32, device="cuda")
 lib.rt_debug_pixel_rays(pr.data_ptr())
 p = R.RtParams(); C.memmove(C.addressof(p), C.addressof(sc.params), C.sizeof(p))
 p.tile_x0, p.tile_y0, p.tile_w, p.tile_h = x0, y0, tw, th
-os.environ["RT_IOW_SPEC"] = "0"
-R.render(sc, p)
+with R.options(iow_spec=0):
+    R.render(sc, p)
 lib.rt_debug_pixel_rays(None)
 u = int(torch.argmax(pr).item()); mx = int(pr.max().item())
 b, l = u >> 6, u & 63; nbx = (tw + 7) >> 3
 px, py = x0 + (b % nbx) * 8 + (l & 7), y0 + (b // nbx) * 8 + (l >> 3)
 out = {"pixel": [px, py], "rays": mx}
 for coop, mode in (("0", "0"), ("4", "0"), ("0", "1"), ("4", "1")):
-    os.environ["RT_IOW_SPEC"] = mode
-    os.environ["RT_COOP"] = coop
+    o = R.default_options(); o.iow_spec, o.iow_coop_max = int(mode), int(coop); R.set_options(o)
     q = R.RtParams(); C.memmove(C.addressof(q), C.addressof(sc.params), C.sizeof(q))
     q.tile_x0, q.tile_y0, q.tile_w, q.tile_h = px, py, 1, 1
     R.render(sc, q)

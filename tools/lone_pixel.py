@@ -5,6 +5,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "raytracing-tests_amd")]
 import rt_amd as R  # noqa: E402
 x, y = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (553, 404)
+o = R.default_options(); o.iow_spec, o.iow_coop_max = 0, 4; R.set_options(o)  # sequential, cooperative hits
 sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0)
 q = R.RtParams(); C.memmove(C.addressof(q), C.addressof(sc.params), C.sizeof(q))
 q.tile_x0, q.tile_y0, q.tile_w, q.tile_h = x, y, 1, 1

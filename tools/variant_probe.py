@@ -16,7 +16,7 @@ g, _, gs = R.render(sc, sc.params)
 o, _, os_ = O.render(sc, sc.params)
 out["parity_small"] = bool(np.array_equal(g, o)) and gs["segments"] == os_["segments"]
 # lone pixel, sequential kernel, cooperative closest hits
-os.environ["RT_IOW_SPEC"], os.environ["RT_COOP"] = "0", "4"
+o = R.get_options(); o.iow_spec, o.iow_coop_max = 0, 4; R.set_options(o)
 sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0)
 q = R.RtParams(); C.memmove(C.addressof(q), C.addressof(sc.params), C.sizeof(q))
 q.tile_x0, q.tile_y0, q.tile_w, q.tile_h = 553, 404, 1, 1
@@ -31,5 +31,5 @@ n = max(1, st["segments"])
 out["lone"] = {"segments": st["segments"], "us_per_segment": st["ms"] * 1e3 / n,
                "cyc_per_segment": {k: round(v / n, 1) for k, v in zip(names, dbg.cpu().numpy().tolist()) if v}}
 out["lone_rgba"] = [float(v) for v in img1.reshape(-1)[:3]]
-del os.environ["RT_IOW_SPEC"], os.environ["RT_COOP"]
+R.set_options(R.default_options())
 print(json.dumps(out))
