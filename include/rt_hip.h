@@ -248,6 +248,16 @@ int rt_lbvh_build_async(const float *d_aabbs, uint32_t n, float *d_nodes_out, vo
 /* Blocking convenience wrapper (host buffers); *ms (may be NULL) receives the device time. */
 int rt_lbvh_build_gpu(const float *aabbs, uint32_t n, float *nodes_out, int device, double *ms);
 
+/* Host-side builds of a device scene's acceleration structures, without a device (what
+ * rt_dev_scene_inw / rt_dev_scene_iow03 build on the host and upload):
+ *   INW: the wide walk's 4-wide culling BVH over the LBVH leaf boxes, the depth-first ranks and
+ *        leaf boxes, and the surrounding-RI grid; info = {wide nodes, dfs_high, wide depth,
+ *        RI grid built, RI cells, RI ids, 0, 0} (all 0 when the wide walk does not apply);
+ *   IOW-03: the culling BVH over the records; info = {wide nodes (0: linear loop), 0, 0, 0}.
+ * info may be NULL; *ms (may be NULL) receives the host time. */
+int rt_inw_host_build(const float *nodes /* (2N-1)*8 */, uint32_t n, uint32_t info[8], double *ms);
+int rt_iow_host_build(const float *types, const float *records /* N*24 */, uint32_t n, uint32_t info[4], double *ms);
+
 /* ---- asynchronous device entry points (bench / multi-GPU path) ---------------------
  * A prepared scene owns its device buffers (scene records, LBVH nodes, sample tables).
  * rt_scene_dev_* return an opaque handle; render calls enqueue on `stream`.

@@ -11,7 +11,8 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librt_oracle.so")
+# RT_ORACLE_LIB: the sanitizer build of the same sources (tools/san/run_san.sh)
+LIB_PATH = os.environ.get("RT_ORACLE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "librt_oracle.so")
 _FP = C.POINTER(C.c_float)
 _lib = None
 

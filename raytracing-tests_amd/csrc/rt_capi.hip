@@ -10,6 +10,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <algorithm>
+#include <chrono>
 #include <memory>
 #include <new>
 #include <string>
@@ -296,47 +297,13 @@ int make_iow03(rt_dev_scene *s, const float *types, const float *rec, uint32_t n
     HIP_OK(s->hot.upload(hot.data(), hot.size() * sizeof(float)));
     HIP_OK(s->cold.upload(cold.data(), cold.size() * sizeof(float)));
     // Culling BVH over the objects (the reference loops linearly; rtk::iow_launch_ray keeps its
-    // exact result).  World box = |M^T| * local half extents, inflated so it is conservative.
-    if (n >= 2 && !s->opt.iow_linear) {  // iow_linear: the reference's linear loop (A/B)
-        std::vector<float> boxes(size_t(n) * 6);
-        for (uint32_t j = 0; j < n; j++) {
-            const float *r = rec + size_t(j) * 24;
-            const bool ell = int(types[j]) == RT_IOW_ELLIPSOID;
-            float h[3];
-            for (int k = 0; k < 3; k++) h[k] = std::fabs(r[12 + k]) * (ell ? 1.0f : 0.5f);
-            float big = std::fmax(std::fabs(r[0]), std::fmax(std::fabs(r[1]), std::fabs(r[2])));
-            for (int k = 0; k < 3; k++) {
-                const float *col = r + 3 + 3 * k;  // column k of M: M_{row j, col k} = col[j]
-                float e = std::fabs(col[0]) * h[0] + std::fabs(col[1]) * h[1] + std::fabs(col[2]) * h[2];
-                e = e * 1.001f + 1e-3f + big * 1e-5f;
-                boxes[size_t(j) * 6 + k] = r[k] - e;
-                boxes[size_t(j) * 6 + 3 + k] = r[k] + e;
-            }
-        }
-        int depth = 0, depth4 = 0;
-        const std::vector<float> bin = rtamd::sah_build(boxes.data(), n, &depth);
-        std::vector<float> wide = rtamd::bvh4_collapse(bin, &depth4);
-        // the kernels read the child links (float 24..27 of a node) as int bits
-        for (size_t w = 0; w < wide.size() / 32; w++)
-            for (int k = 0; k < 4; k++) {
-                const int link = int(wide[w * 32 + 24 + size_t(k)]);
-                std::memcpy(&wide[w * 32 + 24 + size_t(k)], &link, sizeof(link));
-            }
-        // links travel as int16 on the traversal stack: wide node ids < n, object ids < n
-        if (n < 16384) {
-            HIP_OK(s->nodes.upload(wide.data(), wide.size() * sizeof(float)));
-            s->root_link = 1;
-            s->n_wide = uint32_t(wide.size() / 32);
-            // n float4 (lo.xyz, hi.x), then n float2 (hi.yz)
-            std::vector<float> ob(size_t(n) * 6);
-            for (uint32_t j = 0; j < n; j++) {
-                const float *b = boxes.data() + size_t(j) * 6;
-                for (int k = 0; k < 4; k++) ob[size_t(j) * 4 + k] = b[k];
-                ob[size_t(n) * 4 + size_t(j) * 2] = b[4];
-                ob[size_t(n) * 4 + size_t(j) * 2 + 1] = b[5];
-            }
-            HIP_OK(s->obox.upload(ob.data(), ob.size() * sizeof(float)));
-        }
+    // exact result); iow_linear: the reference's linear loop (A/B)
+    rtamd::IowCull cull;
+    if (!s->opt.iow_linear && rtamd::iow_cull_build(types, rec, n, cull)) {
+        HIP_OK(s->nodes.upload(cull.wide.data(), cull.wide.size() * sizeof(float)));
+        s->root_link = 1;
+        s->n_wide = cull.n_wide;
+        HIP_OK(s->obox.upload(cull.obox.data(), cull.obox.size() * sizeof(float)));
     }
     set_residency(s);
     return build_tables(s, spp);
@@ -369,148 +336,26 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     }
 }
 
-// The surrounding-RI grid (DESIGN.md §5 "RI grid"): about two cells per object over the union of
-// the LBVH leaf boxes; each object is entered in every cell its leaf box overlaps once widened by
-// a thousandth of a cell (far above the rounding of a float cell index), so the cell a point
-// falls in lists every object whose leaf box holds the point.  No grid when a cell would list
-// more than 64 objects.
-int make_ri_grid(rt_dev_scene *s, const std::vector<float> &lbox, uint32_t n) {
-    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
-    for (uint32_t g = 0; g < n; g++)
-        for (int a = 0; a < 3; a++) {
-            lo[a] = std::fmin(lo[a], double(lbox[size_t(g) * 8 + a]));
-            hi[a] = std::fmax(hi[a], double(lbox[size_t(g) * 8 + 3 + a]));
-        }
-    double ext[3], vol = 1.0;
-    for (int a = 0; a < 3; a++) {
-        if (!(hi[a] >= lo[a]) || !std::isfinite(lo[a]) || !std::isfinite(hi[a])) return RT_OK;
-        ext[a] = std::fmax(hi[a] - lo[a], 1e-6 * (1.0 + std::fabs(lo[a])));
-        vol *= ext[a];
-    }
-    const double cell = std::cbrt(vol / (2.0 * n));
-    int dim[3];
-    double inv[3];
-    for (int a = 0; a < 3; a++) {
-        dim[a] = int(std::fmin(512.0, std::fmax(1.0, std::ceil(ext[a] / cell))));
-        inv[a] = double(dim[a]) / ext[a];
-    }
-    const size_t nc = size_t(dim[0]) * dim[1] * dim[2];
-    std::vector<uint32_t> cnt(nc + 1, 0);
-    auto range = [&](uint32_t g, int a, int &c0, int &c1) {
-        const double m = 1e-3 / inv[a];
-        c0 = std::max(0, std::min(dim[a] - 1, int(std::floor((double(lbox[size_t(g) * 8 + a]) - m - lo[a]) * inv[a]))));
-        c1 = std::max(0, std::min(dim[a] - 1, int(std::floor((double(lbox[size_t(g) * 8 + 3 + a]) + m - lo[a]) * inv[a]))));
-    };
-    for (int pass = 0; pass < 2; pass++) {
-        std::vector<uint32_t> fill;
-        std::vector<uint32_t> ids;
-        if (pass == 1) {
-            for (size_t c = 0; c < nc; c++) cnt[c + 1] += cnt[c];
-            fill.assign(cnt.begin(), cnt.end() - 1);
-            ids.resize(cnt[nc]);
-        }
-        for (uint32_t g = 0; g < n; g++) {
-            int r0[3], r1[3];
-            for (int a = 0; a < 3; a++) range(g, a, r0[a], r1[a]);
-            for (int z = r0[2]; z <= r1[2]; z++)
-                for (int y = r0[1]; y <= r1[1]; y++)
-                    for (int x = r0[0]; x <= r1[0]; x++) {
-                        const size_t c = (size_t(z) * dim[1] + y) * dim[0] + x;
-                        if (pass == 0) {
-                            if (++cnt[c + 1] > 64) return RT_OK;
-                        } else ids[fill[c]++] = g;
-                    }
-        }
-        if (pass == 1) {
-            HIP_OK(s->ri_cells.upload(cnt.data(), cnt.size() * sizeof(uint32_t)));
-            HIP_OK(s->ri_ids.upload(ids.data(), std::max<size_t>(1, ids.size()) * sizeof(uint32_t)));
-        }
-    }
-    for (int a = 0; a < 3; a++) {
-        // float bounds: a point outside them is outside every leaf box
-        s->ri_lo[a] = float(lo[a]);
-        s->ri_hi[a] = float(hi[a]);
-        s->ri_inv[a] = float(inv[a]);
-        s->ri_dim[a] = dim[a];
-    }
-    return RT_OK;
-}
-
+// The wide walk's structures and the RI grid, built on the host (rtamd::inw_wide_build,
+// rtamd::ri_grid_build) and uploaded.
 int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
     s->dfs_high = 0;
-    if (n < 2 || !s->opt.inw_wide_walk) return RT_OK;
-    const uint32_t nn = 2 * n - 1;
-    std::vector<uint32_t> leaf(n, 0xffffffffu), rank(size_t(2) * n, 0);
-    for (uint32_t i = 0; i < nn; i++) {
-        const float left = nodes[size_t(i) * 8 + 6];
-        if (!(left > 0.1f)) {
-            const float g = -left;
-            if (!(g >= 0.0f) || g >= float(n)) return RT_OK;  // not a well-formed LBVH: exact walk only
-            leaf[uint32_t(g)] = i;
+    rtamd::InwWide w;
+    if (!s->opt.inw_wide_walk || !rtamd::inw_wide_build(nodes, n, w)) return RT_OK;
+    HIP_OK(s->wnodes.upload(w.wnodes.data(), w.wnodes.size() * sizeof(float)));
+    HIP_OK(s->wrank.upload(w.rank.data(), w.rank.size() * sizeof(uint32_t)));
+    HIP_OK(s->wleaf.upload(w.leafbox.data(), w.leafbox.size() * sizeof(float)));
+    const rtamd::RiGrid g = rtamd::ri_grid_build(w.leafbox.data(), n);
+    if (g.ok) {
+        HIP_OK(s->ri_cells.upload(g.cells.data(), g.cells.size() * sizeof(uint32_t)));
+        HIP_OK(s->ri_ids.upload(g.ids.data(), std::max<size_t>(1, g.ids.size()) * sizeof(uint32_t)));
+        for (int a = 0; a < 3; a++) {
+            s->ri_lo[a] = g.lo[a]; s->ri_hi[a] = g.hi[a]; s->ri_inv[a] = g.inv[a]; s->ri_dim[a] = g.dim[a];
         }
     }
-    for (uint32_t g = 0; g < n; g++)
-        if (leaf[g] == 0xffffffffu) return RT_OK;
-    // depth-first order of the leaves and the stack high-water mark, both child orders
-    // (01_BVH...glsl:456-460: push(invert ? right : left), push(invert ? left : right))
-    uint32_t high = 0;
-    for (int inv = 0; inv < 2; inv++) {
-        std::vector<uint32_t> st{0};
-        uint32_t r = 0;
-        high = std::max<uint32_t>(high, 1);
-        while (!st.empty()) {
-            const uint32_t i = st.back();
-            st.pop_back();
-            const float left = nodes[size_t(i) * 8 + 6];
-            if (left > 0.1f) {
-                const uint32_t l = uint32_t(left), rr = l + 1;
-                if (rr >= nn) return RT_OK;
-                st.push_back(inv ? rr : l);
-                st.push_back(inv ? l : rr);
-                high = std::max<uint32_t>(high, uint32_t(st.size()));
-            } else {
-                rank[size_t(inv) * n + uint32_t(-left)] = r++;
-            }
-        }
-        if (r != n) return RT_OK;
-    }
-    // culling boxes: the leaf boxes, inflated as the IOW culling BVH's
-    std::vector<float> boxes(size_t(n) * 6);
-    float wbound = 0.0f;
-    for (uint32_t g = 0; g < n; g++) {
-        const float *b = nodes + size_t(leaf[g]) * 8;  // bbmin xyz, bbmax xyz
-        float big = 0.0f;
-        for (int k = 0; k < 6; k++) big = std::fmax(big, std::fabs(b[k]));
-        for (int k = 0; k < 3; k++) {
-            const float e = (b[3 + k] - b[k]) * 1e-3f + 1e-3f + big * 1e-5f;
-            boxes[size_t(g) * 6 + k] = b[k] - e;
-            boxes[size_t(g) * 6 + 3 + k] = b[3 + k] + e;
-            wbound = std::fmax(wbound, std::fmax(std::fabs(b[k] - e), std::fabs(b[3 + k] + e)));
-        }
-    }
-    int depth = 0, depth4 = 0;
-    const std::vector<float> bin = rtamd::sah_build(boxes.data(), n, &depth);
-    std::vector<float> wide = rtamd::bvh4_collapse(bin, &depth4);
-    // rtk::kInwNodeF4 = 10 float4 per node: lx ly lz hx hy hz lx ly lz, child links as int bits
-    const size_t nw = wide.size() / 32;
-    std::vector<float> wn(nw * 40);
-    for (size_t w = 0; w < nw; w++) {
-        std::memcpy(&wn[w * 40], &wide[w * 32], 24 * sizeof(float));
-        std::memcpy(&wn[w * 40 + 24], &wide[w * 32], 12 * sizeof(float));
-        for (int k = 0; k < 4; k++) {
-            const int link = int(wide[w * 32 + 24 + size_t(k)]);
-            std::memcpy(&wn[w * 40 + 36 + size_t(k)], &link, sizeof(link));
-        }
-    }
-    HIP_OK(s->wnodes.upload(wn.data(), wn.size() * sizeof(float)));
-    HIP_OK(s->wrank.upload(rank.data(), rank.size() * sizeof(uint32_t)));
-    std::vector<float> lbox(size_t(n) * 8);  // each object's LBVH leaf node, indexed by object
-    for (uint32_t g = 0; g < n; g++) std::memcpy(&lbox[size_t(g) * 8], nodes + size_t(leaf[g]) * 8, 8 * sizeof(float));
-    HIP_OK(s->wleaf.upload(lbox.data(), lbox.size() * sizeof(float)));
-    if (int rc = make_ri_grid(s, lbox, n); rc != RT_OK) return rc;
-    s->dfs_high = high;
-    s->wdepth = depth4;
-    s->wbound = wbound;
+    s->dfs_high = w.dfs_high;
+    s->wdepth = w.depth;
+    s->wbound = w.wbound;
     return RT_OK;
 }
 
@@ -1665,6 +1510,45 @@ int rt_render_inw_tex(const float *geom, uint32_t n, int layout, const float *no
     rc = make_inw(s.get(), geom, n, layout, nodes, lights, n_lights, tex, n_tex, p->spp);
     if (rc != RT_OK) return rc;
     return render_blocking(s.get(), cam, p, rgba, depth, st);
+}
+
+int rt_inw_host_build(const float *nodes, uint32_t n, uint32_t info[8], double *ms) {
+    if (!nodes || n == 0) return RT_E_ARG;
+    try {
+        const auto t0 = std::chrono::steady_clock::now();
+        rtamd::InwWide w;
+        rtamd::RiGrid g;
+        const bool ok = rtamd::inw_wide_build(nodes, n, w);
+        if (ok) g = rtamd::ri_grid_build(w.leafbox.data(), n);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        if (info) {
+            const uint32_t v[8] = {uint32_t(w.wnodes.size() / 40), w.dfs_high, uint32_t(w.depth), g.ok ? 1u : 0u,
+                                   g.ok ? uint32_t(g.cells.size() - 1) : 0u, uint32_t(g.ids.size()), 0u, 0u};
+            std::memcpy(info, v, sizeof(v));
+        }
+    } catch (...) {
+        return RT_E_ARG;
+    }
+    return RT_OK;
+}
+
+int rt_iow_host_build(const float *types, const float *records, uint32_t n, uint32_t info[4], double *ms) {
+    if (!types || !records || n == 0) return RT_E_ARG;
+    try {
+        const auto t0 = std::chrono::steady_clock::now();
+        rtamd::IowCull c;
+        const bool ok = rtamd::iow_cull_build(types, records, n, c);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        if (info) {
+            const uint32_t v[4] = {ok ? c.n_wide : 0u, 0u, 0u, 0u};
+            std::memcpy(info, v, sizeof(v));
+        }
+    } catch (...) {
+        return RT_E_ARG;
+    }
+    return RT_OK;
 }
 
 int rt_lbvh_build(const float *aabbs, uint32_t n, float *nodes_out) {

@@ -695,4 +695,177 @@ std::vector<SpiralTile> tile_spiral(int W, int H, int tw, int th) {
     return out;
 }
 
+// ---------------------------------------------------------------- device-scene structures
+bool iow_cull_build(const float *types, const float *rec, uint32_t n, IowCull &out) {
+    // links travel as int16 on the IOW traversal stack: wide node ids < n, object ids < n
+    if (n < 2 || n >= 16384) return false;
+    // world box of each record = |M^T| * local half extents, inflated so it is conservative
+    std::vector<float> boxes(size_t(n) * 6);
+    for (uint32_t j = 0; j < n; j++) {
+        const float *r = rec + size_t(j) * 24;
+        const bool ell = int(types[j]) == RT_IOW_ELLIPSOID;
+        float h[3];
+        for (int k = 0; k < 3; k++) h[k] = std::fabs(r[12 + k]) * (ell ? 1.0f : 0.5f);
+        const float big = std::fmax(std::fabs(r[0]), std::fmax(std::fabs(r[1]), std::fabs(r[2])));
+        for (int k = 0; k < 3; k++) {
+            const float *col = r + 3 + 3 * k;  // column k of M: M_{row j, col k} = col[j]
+            float e = std::fabs(col[0]) * h[0] + std::fabs(col[1]) * h[1] + std::fabs(col[2]) * h[2];
+            e = e * 1.001f + 1e-3f + big * 1e-5f;
+            boxes[size_t(j) * 6 + k] = r[k] - e;
+            boxes[size_t(j) * 6 + 3 + k] = r[k] + e;
+        }
+    }
+    int depth = 0, depth4 = 0;
+    out.wide = bvh4_collapse(sah_build(boxes.data(), n, &depth), &depth4);
+    for (size_t w = 0; w < out.wide.size() / 32; w++)  // the kernels read the links as int bits
+        for (int k = 0; k < 4; k++) {
+            const int link = int(out.wide[w * 32 + 24 + size_t(k)]);
+            std::memcpy(&out.wide[w * 32 + 24 + size_t(k)], &link, sizeof(link));
+        }
+    out.n_wide = uint32_t(out.wide.size() / 32);
+    out.obox.assign(size_t(n) * 6, 0.0f);
+    for (uint32_t j = 0; j < n; j++) {
+        const float *b = boxes.data() + size_t(j) * 6;
+        for (int k = 0; k < 4; k++) out.obox[size_t(j) * 4 + k] = b[k];
+        out.obox[size_t(n) * 4 + size_t(j) * 2] = b[4];
+        out.obox[size_t(n) * 4 + size_t(j) * 2 + 1] = b[5];
+    }
+    return true;
+}
+
+bool inw_wide_build(const float *nodes, uint32_t n, InwWide &out) {
+    if (n < 2) return false;
+    const uint32_t nn = 2 * n - 1;
+    std::vector<uint32_t> leaf(n, 0xffffffffu);
+    out.rank.assign(size_t(2) * n, 0);
+    for (uint32_t i = 0; i < nn; i++) {
+        const float left = nodes[size_t(i) * 8 + 6];
+        if (!(left > 0.1f)) {
+            const float g = -left;
+            if (!(g >= 0.0f) || g >= float(n)) return false;  // not a well-formed LBVH: exact walk only
+            leaf[uint32_t(g)] = i;
+        }
+    }
+    for (uint32_t g = 0; g < n; g++)
+        if (leaf[g] == 0xffffffffu) return false;
+    // depth-first order of the leaves and the stack high-water mark, both child orders
+    // (01_BVH...glsl:456-460: push(invert ? right : left), push(invert ? left : right))
+    uint32_t high = 0;
+    for (int inv = 0; inv < 2; inv++) {
+        std::vector<uint32_t> st{0};
+        uint32_t r = 0;
+        high = std::max<uint32_t>(high, 1);
+        while (!st.empty()) {
+            const uint32_t i = st.back();
+            st.pop_back();
+            const float left = nodes[size_t(i) * 8 + 6];
+            if (left > 0.1f) {
+                const uint32_t l = uint32_t(left), rr = l + 1;
+                if (rr >= nn || st.size() + 2 > size_t(nn)) return false;
+                st.push_back(inv ? rr : l);
+                st.push_back(inv ? l : rr);
+                high = std::max<uint32_t>(high, uint32_t(st.size()));
+            } else {
+                if (r == n) return false;
+                out.rank[size_t(inv) * n + uint32_t(-left)] = r++;
+            }
+        }
+        if (r != n) return false;
+    }
+    // culling boxes: the leaf boxes, inflated as the IOW culling BVH's
+    std::vector<float> boxes(size_t(n) * 6);
+    float wbound = 0.0f;
+    for (uint32_t g = 0; g < n; g++) {
+        const float *b = nodes + size_t(leaf[g]) * 8;  // bbmin xyz, bbmax xyz
+        float big = 0.0f;
+        for (int k = 0; k < 6; k++) big = std::fmax(big, std::fabs(b[k]));
+        for (int k = 0; k < 3; k++) {
+            const float e = (b[3 + k] - b[k]) * 1e-3f + 1e-3f + big * 1e-5f;
+            boxes[size_t(g) * 6 + k] = b[k] - e;
+            boxes[size_t(g) * 6 + 3 + k] = b[3 + k] + e;
+            wbound = std::fmax(wbound, std::fmax(std::fabs(b[k] - e), std::fabs(b[3 + k] + e)));
+        }
+    }
+    int depth = 0, depth4 = 0;
+    const std::vector<float> wide = bvh4_collapse(sah_build(boxes.data(), n, &depth), &depth4);
+    // 10 float4 per node: lx ly lz hx hy hz lx ly lz, child links as int bits
+    const size_t nw = wide.size() / 32;
+    out.wnodes.assign(nw * 40, 0.0f);
+    for (size_t w = 0; w < nw; w++) {
+        std::memcpy(&out.wnodes[w * 40], &wide[w * 32], 24 * sizeof(float));
+        std::memcpy(&out.wnodes[w * 40 + 24], &wide[w * 32], 12 * sizeof(float));
+        for (int k = 0; k < 4; k++) {
+            const int link = int(wide[w * 32 + 24 + size_t(k)]);
+            std::memcpy(&out.wnodes[w * 40 + 36 + size_t(k)], &link, sizeof(link));
+        }
+    }
+    out.leafbox.assign(size_t(n) * 8, 0.0f);
+    for (uint32_t g = 0; g < n; g++) std::memcpy(&out.leafbox[size_t(g) * 8], nodes + size_t(leaf[g]) * 8, 8 * sizeof(float));
+    out.dfs_high = high;
+    out.depth = depth4;
+    out.wbound = wbound;
+    return true;
+}
+
+RiGrid ri_grid_build(const float *lbox, uint32_t n) {
+    RiGrid G;
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (uint32_t g = 0; g < n; g++)
+        for (int a = 0; a < 3; a++) {
+            lo[a] = std::fmin(lo[a], double(lbox[size_t(g) * 8 + a]));
+            hi[a] = std::fmax(hi[a], double(lbox[size_t(g) * 8 + 3 + a]));
+        }
+    double ext[3], vol = 1.0;
+    for (int a = 0; a < 3; a++) {
+        if (!(hi[a] >= lo[a]) || !std::isfinite(lo[a]) || !std::isfinite(hi[a])) return G;
+        ext[a] = std::fmax(hi[a] - lo[a], 1e-6 * (1.0 + std::fabs(lo[a])));
+        vol *= ext[a];
+    }
+    const double cell = std::cbrt(vol / (2.0 * n));
+    int dim[3];
+    double inv[3];
+    for (int a = 0; a < 3; a++) {
+        dim[a] = int(std::fmin(512.0, std::fmax(1.0, std::ceil(ext[a] / cell))));
+        inv[a] = double(dim[a]) / ext[a];
+    }
+    const size_t nc = size_t(dim[0]) * dim[1] * dim[2];
+    std::vector<uint32_t> cnt(nc + 1, 0);
+    auto range = [&](uint32_t g, int a, int &c0, int &c1) {
+        const double m = 1e-3 / inv[a];
+        c0 = std::max(0, std::min(dim[a] - 1, int(std::floor((double(lbox[size_t(g) * 8 + a]) - m - lo[a]) * inv[a]))));
+        c1 = std::max(0, std::min(dim[a] - 1, int(std::floor((double(lbox[size_t(g) * 8 + 3 + a]) + m - lo[a]) * inv[a]))));
+    };
+    std::vector<uint32_t> fill, ids;
+    for (int pass = 0; pass < 2; pass++) {
+        if (pass == 1) {
+            for (size_t c = 0; c < nc; c++) cnt[c + 1] += cnt[c];
+            fill.assign(cnt.begin(), cnt.end() - 1);
+            ids.resize(cnt[nc]);
+        }
+        for (uint32_t g = 0; g < n; g++) {
+            int r0[3], r1[3];
+            for (int a = 0; a < 3; a++) range(g, a, r0[a], r1[a]);
+            for (int z = r0[2]; z <= r1[2]; z++)
+                for (int y = r0[1]; y <= r1[1]; y++)
+                    for (int x = r0[0]; x <= r1[0]; x++) {
+                        const size_t c = (size_t(z) * dim[1] + y) * dim[0] + x;
+                        if (pass == 0) {
+                            if (++cnt[c + 1] > 64) return G;
+                        } else ids[fill[c]++] = g;
+                    }
+        }
+    }
+    for (int a = 0; a < 3; a++) {
+        // float bounds: a point outside them is outside every leaf box
+        G.lo[a] = float(lo[a]);
+        G.hi[a] = float(hi[a]);
+        G.inv[a] = float(inv[a]);
+        G.dim[a] = dim[a];
+    }
+    G.cells = std::move(cnt);
+    G.ids = std::move(ids);
+    G.ok = true;
+    return G;
+}
+
 }  // namespace rtamd

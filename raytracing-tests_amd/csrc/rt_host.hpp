@@ -107,6 +107,43 @@ std::vector<float> sah_build(const float *aabbs, uint32_t n, int *depth);
 // *depth receives the number of wide levels.
 std::vector<float> bvh4_collapse(const std::vector<float> &bin, int *depth);
 
+// ---- device-scene structures built on the host -------------------------
+// IOW-03 culling BVH (the reference loops linearly over the objects, 03...glsl:196-256): a SAH
+// tree over conservative world boxes of the records, collapsed to 4-wide nodes whose child
+// links are int bits (float 24..27 of a node), and the leaves' boxes as n float4 (lo.xyz, hi.x)
+// followed by n float2 (hi.yz).  Returns false (linear loop) for fewer than 2 or 16384+ objects.
+struct IowCull {
+    std::vector<float> wide, obox;
+    uint32_t n_wide = 0;
+};
+bool iow_cull_build(const float *types, const float *rec, uint32_t n, IowCull &out);
+
+// INW wide walk: from the reference's LBVH nodes ((2n-1) x 8), each object's
+// leaf box, its rank in the LBVH's depth-first order for both child orders, the walk's stack
+// high-water mark dfs_high, and a 4-wide culling BVH over the leaf boxes (inflated), 40 floats
+// per node (lx ly lz hx hy hz lx ly lz links).  Returns false (reference walk only) for fewer
+// than 2 objects or an LBVH that is not well formed.
+struct InwWide {
+    uint32_t dfs_high = 0;
+    int depth = 0;
+    float wbound = 0.0f;           // largest |coordinate| of the culling boxes
+    std::vector<float> wnodes;     // 40 floats per node
+    std::vector<uint32_t> rank;    // 2n: rank[inv * n + g]
+    std::vector<float> leafbox;    // 8n: object g's LBVH leaf node
+};
+bool inw_wide_build(const float *nodes, uint32_t n, InwWide &out);
+
+// The surrounding-RI grid (DESIGN.md §5 "RI grid") over the leaf boxes: about two cells per
+// object, every object entered in each cell its leaf box overlaps once widened by a thousandth of
+// a cell.  ok = false when some cell would list more than 64 objects (the walk answers instead).
+struct RiGrid {
+    bool ok = false;
+    float lo[3] = {}, hi[3] = {}, inv[3] = {};
+    int dim[3] = {};
+    std::vector<uint32_t> cells, ids;  // cell offsets (cells + 1), object ids
+};
+RiGrid ri_grid_build(const float *leafbox, uint32_t n);
+
 // ---- camera (materials.cpp:321-328, base.h:274-281) ------------------------------------
 Vec3 front_from_pitch_yaw(float pitch_deg, float yaw_deg, bool normalize);
 

@@ -170,6 +170,8 @@ SIGNATURES = {
     "rt_debug_spec_list_hist": (C.c_int, [C.c_void_p, _U64P]),
     "rt_debug_spec_list_stale": (C.c_int, [C.c_void_p, _U64P]),
     "rt_debug_spec_dump": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "rt_inw_host_build": (C.c_int, [_FP, C.c_uint32, _U32P, C.POINTER(C.c_double)]),
+    "rt_iow_host_build": (C.c_int, [_FP, _FP, C.c_uint32, _U32P, C.POINTER(C.c_double)]),
     "rt_options_default": (None, [C.POINTER(RtOptions)]),
     "rt_options_set": (C.c_int, [C.POINTER(RtOptions)]),
     "rt_options_get": (C.c_int, [C.POINTER(RtOptions)]),
@@ -393,6 +395,24 @@ def lbvh_build_gpu(aabbs, device: int = -1):
     ms = C.c_double(0.0)
     check(load().rt_lbvh_build_gpu(fptr(aabbs), n, fptr(nodes), device, C.byref(ms)), "rt_lbvh_build_gpu")
     return nodes, ms.value
+
+
+def inw_host_build(nodes: np.ndarray, n: int) -> dict:
+    """rt_inw_host_build: the INW device scene's host-built structures (sizes) and host time."""
+    info = (C.c_uint32 * 8)()
+    ms = C.c_double(0.0)
+    check(load().rt_inw_host_build(fptr(np.ascontiguousarray(nodes, np.float32)), n, info, C.byref(ms)),
+          "rt_inw_host_build")
+    keys = ("wide_nodes", "dfs_high", "wide_depth", "ri_grid", "ri_cells", "ri_ids")
+    return {**dict(zip(keys, list(info)[:6])), "ms": ms.value}
+
+
+def iow_host_build(types: np.ndarray, records: np.ndarray, n: int) -> dict:
+    """rt_iow_host_build: the IOW-03 culling BVH's size (0: linear loop) and host time."""
+    info = (C.c_uint32 * 4)()
+    ms = C.c_double(0.0)
+    check(load().rt_iow_host_build(fptr(types), fptr(records), n, info, C.byref(ms)), "rt_iow_host_build")
+    return {"wide_nodes": info[0], "ms": ms.value}
 
 
 def lbvh_build(aabbs: np.ndarray) -> np.ndarray:

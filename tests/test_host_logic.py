@@ -122,3 +122,31 @@ def test_inw04_light_ssbo():
     assert np.array_equal(pk["lights"][:, :6], pk["aabbs"][[0, 1]])
     g = pk["geom"]
     assert np.all(g[[0, 1], 24:27] == 1.0) and np.all(g[[0, 1], 20:22] == 0.0)  # emissive packing
+
+
+@pytest.mark.parametrize("preset,seed,n_hint", [(R.PRESET_INW01_RANDOM, 1234, 10_000), (R.PRESET_INW01_RANDOM, 5, 2),
+                                                (R.PRESET_INW04_CORNELL, 7, 0), (R.PRESET_INW01_GRID, 0, 9)])
+def test_inw_host_structures(preset, seed, n_hint):
+    """The INW device scene's host-built structures (rt_inw_host_build, what rt_dev_scene_inw
+    uploads): the wide walk applies to every well-formed LBVH of 2+ objects, its stack high-water
+    mark fits the shader's 40-float stack, and the RI grid covers C3's objects."""
+    sc = R.make_scene(preset, seed, n_hint, width=8, height=8, spp=1)
+    info = R.inw_host_build(sc.nodes, sc.n)
+    print(sc.n, info)
+    assert info["wide_nodes"] >= 1 and 1 <= info["dfs_high"] <= 40 and info["wide_depth"] >= 1
+    assert info["wide_nodes"] <= sc.n  # 4-wide: fewer nodes than objects
+    if sc.n >= 1000:
+        assert info["ri_grid"] == 1 and info["ri_cells"] >= sc.n and info["ri_ids"] >= sc.n
+    # a malformed LBVH (a leaf id out of range) turns the wide walk off instead of failing
+    bad = sc.nodes.copy()
+    bad[np.argmax(bad[:, 6] <= 0.1), 6] = -float(sc.n + 5)
+    assert R.inw_host_build(bad, sc.n)["wide_nodes"] == 0
+
+
+def test_iow_host_structures():
+    """The IOW-03 culling BVH (rt_iow_host_build): built for the final scene, absent (linear
+    loop) for a single object."""
+    sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0, width=8, height=8, spp=1)
+    info = R.iow_host_build(sc.types, sc.records, sc.n)
+    assert 1 <= info["wide_nodes"] < sc.n
+    assert R.iow_host_build(sc.types[:1], sc.records[:1], 1)["wide_nodes"] == 0
