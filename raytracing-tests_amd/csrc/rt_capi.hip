@@ -162,6 +162,7 @@ struct rt_dev_scene {
     bool last_fu = false;         // ... their fused-fma cull instances
     uint32_t last_force = 0;      // ... its forced order (0: the probe's pick, read back from inw_mode)
     uint32_t last_ring[2] = {0, 0};  // ... its fold windows (pixel-major, sample-major)
+    uint32_t ring_frame = 0;         // frames rendered with the current fold rings (their tag epoch)
     rt_path_info last_path{};     // rt_debug_path: what the last render ran
     float wbound = 0.0f;          // largest |coordinate| of the INW culling boxes (the fused cull's condition)
     uint32_t dfs_high = 0;
@@ -1032,11 +1033,16 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         s->inw_ring.~DevBuf();
         new (&s->inw_ring) DevBuf();
         if (s->inw_ring.alloc(ring_bytes) != hipSuccess) return RT_E_HIP;
+        s->ring_frame = 0;  // fresh memory: clear it before the first frame
     }
+    // ring tags carry the frame's epoch (rtk::ring_tag); the rings are cleared only when it wraps
+    const uint32_t epoch = s->ring_frame % 63u;
+    s->ring_frame++;
     rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
                      s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>(),
                      s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
     set_wide(s, sc);
+    sc.ring_epoch = epoch << 26;
     // the fused cull (cull4nf<true>: one fma per plane) while every ray origin -- the camera (+ lens and the unit step
     // of the primary ray), hit points inside the scene's boxes -- lies within 1000 of the origin
     // (DESIGN.md §2); not with the MULTIFOCUS lens chain, whose lens points are farther out
@@ -1066,7 +1072,8 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         ev = &s->kt_ev[0];
         s->kt_used = 1;
     }
-    // the rings are reset first, so the events bracket the probe and the two fold kernels
+    // the rings are cleared first (when the epoch wraps), so the events bracket the probe and the
+    // two fold kernels
     // claim order, costliest blocks first (inw_claim_order = 0: unit order)
     uint32_t *cost = nullptr;
     if (o.inw_claim_order) {
@@ -1091,7 +1098,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         P.lds_nodes = s->last_ln ? 1 : 0;
         P.claim_order = cost != nullptr;
     }
-    e = hipMemsetAsync(s->inw_ring.p, 0xff, ring_bytes, st);
+    if (epoch == 0) e = hipMemsetAsync(s->inw_ring.p, 0xff, s->inw_ring.bytes, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->first, st);
     if (e == hipSuccess)
         e = rtk::launch_inw_fold(f, sc, s->inw_ring.as<float4>(), ring_pm, ring_sm, s->counter.as<unsigned>(),

@@ -2552,6 +2552,14 @@ __global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S, Chunk ch, C
 // k_inw_probe picks one per frame on the device (mode[]): over a sparse set of 8x8 blocks it
 // traces one primary ray per pixel; the frame is "coarse" when most blocks with a hit see one
 // object in all their pixels.  Both kernels are launched; the one not picked exits at once.
+// A fold-ring entry's tag: the low 26 bits of its stream position and the frame's ring epoch
+// (0..62) in the high 6 (InwScene::ring_epoch).  An entry left by one of the 62 frames before
+// carries another epoch, and the host clears the rings with 0xff bytes (an epoch of 63, never
+// valid) whenever the epoch wraps to 0, so a stale entry never passes for a finished one and no
+// per-frame clear is needed.  Within a frame, slot g mod R last held g - R (R <= 2^16 < 2^26).
+__device__ __forceinline__ uint32_t ring_tag(const InwScene &S, uint32_t g) {
+    return (g & 0x03ffffffu) | S.ring_epoch;
+}
 __device__ __forceinline__ float rdl(float v, uint32_t l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
 }
@@ -2803,7 +2811,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             if (k - gf < gi - gf) {
                 v = wr[k & rmask];
-                fin = __float_as_uint(v.w) == k;
+                fin = __float_as_uint(v.w) == ring_tag(S, k);
             }
             const unsigned long long m = __ballot(fin);
             const uint32_t n = ~m == 0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
@@ -2894,7 +2902,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                         inw_start_sample_cd(S, f, K, pcd, s, c);
                     } else {  // a padding slot: an empty sample, folded as zero
                         if ((uint32_t)s == mid && f.out_depth && px.out != (size_t)-1) f.out_depth[px.out] = 0.0f;
-                        wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
+                        wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(ring_tag(S, g)));
                     }
                 }
                 gi += take;
@@ -2914,7 +2922,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         INW_CYC(c, 4, t_seg);
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
-                                        __uint_as_float(g));
+                                        __uint_as_float(ring_tag(S, g)));
             if ((uint32_t)s == mid && f.out_depth) f.out_depth[px.out] = dep;  // 01_BVH...glsl:667-668
             busy = false;
         }
@@ -2988,11 +2996,11 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                     const uint32_t sk = sf + (uint32_t)k;
                     gg[k] = bf * E + (sk < spp ? sk : spp - 1u) * 64u + lane;
                     const bool ok = sk < spp && gg[k] - (gi - rsize) < rsize;  // issued (and inside the window)
-                    v[k] = ok ? wr[gg[k] & rmask] : make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(~gg[k]));
+                    v[k] = ok ? wr[gg[k] & rmask] : make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(~ring_tag(S, gg[k])));
                 }
 #pragma unroll
                 for (int k = 0; k < 2; k++) {
-                    if (__float_as_uint(v[k].w) != gg[k] || sf == spp) break;
+                    if (__float_as_uint(v[k].w) != ring_tag(S, gg[k]) || sf == spp) break;
                     const f3 gv = f3{v[k].x, v[k].y, v[k].z};
                     acc = sf == 0 ? gv : acc + gv;
                     if (++sf == spp) {  // pixel complete: End()'s imageStore (01_BVH...glsl:652)
@@ -3059,7 +3067,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                         inw_start_sample(S, f, K, px.x, px.y, s, c);
                     } else {  // a padding slot: an empty sample, folded as zero
                         if ((uint32_t)s == mid && f.out_depth && px.out != (size_t)-1) f.out_depth[px.out] = 0.0f;
-                        wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(g));
+                        wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(ring_tag(S, g)));
                     }
                 }
                 gi += take;
@@ -3074,7 +3082,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         }
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
-                                        __uint_as_float(g));
+                                        __uint_as_float(ring_tag(S, g)));
             if ((uint32_t)s == mid && f.out_depth) f.out_depth[px.out] = dep;  // 01_BVH...glsl:667-668
             busy = false;
         }

@@ -125,3 +125,43 @@ def test_unsupported_texture_index_fails_loudly(gpu):
     sc.geom[2, 27] = 1.0  # TextureIndex > 0 with no texture bound (rt_render_inw_tex binds them)
     with pytest.raises(RuntimeError):
         R.render(sc)
+
+
+def test_repeated_frames_on_one_device_scene(gpu):
+    """A device scene renders frame after frame with its fold rings kept (their tags carry a
+    frame epoch; they are cleared only when it wraps every 63 frames): 70 frames, alternating the
+    fold windows and the fold order between them, all bit-identical to the first, colour and depth,
+    with the same ray counts."""
+    import ctypes as C
+
+    import torch
+
+    sc = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 3000, width=64, height=40, spp=37)
+    lib = R.load()
+    dev = torch.device("cuda")
+    s = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, 1, R.fptr(sc.nodes), None, 0, sc.params.spp, -1)
+    assert s
+    frames = []
+    try:
+        for i in range(70):
+            o = R.default_options()
+            o.inw_ring_pm, o.inw_ring_sm = (1024, 256) if i % 3 else (64, 128)
+            o.inw_order = (0, 1, 2)[i % 3]
+            assert lib.rt_dev_scene_set_options(s, C.byref(o)) == 0
+            img = torch.zeros((40, 64, 4), dtype=torch.float32, device=dev)
+            dep = torch.zeros((40, 64), dtype=torch.float32, device=dev)
+            ctr = torch.zeros(6, dtype=torch.int64, device=dev)
+            rc = lib.rt_render_image_async(s, C.byref(sc.camera), C.byref(sc.params), img.data_ptr(), dep.data_ptr(),
+                                           ctr.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            assert rc == 0
+            torch.cuda.synchronize()
+            frames.append((img.cpu().numpy(), dep.cpu().numpy(), int(ctr[0].item())))
+    finally:
+        lib.rt_dev_scene_free(s)
+    g, gd, gs = frames[0]
+    o, od, ost = O.render(sc)
+    assert compare(g, o)["exact_frac"] == 1.0 and compare(gd, od)["exact_frac"] == 1.0 and gs == ost["segments"]
+    for i, (a, d, n) in enumerate(frames[1:], 1):
+        assert compare(a, g)["exact_frac"] == 1.0, i
+        assert compare(d, gd)["exact_frac"] == 1.0, i
+        assert n == gs, i

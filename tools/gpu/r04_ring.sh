@@ -1,0 +1,32 @@
+# Fold-ring window A/B (round 4): parity gate, then bench frames and PMC HBM bytes per ring size.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r04_ring; rm -rf $O; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "repeated or inw01_random" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/gate.log 2>&1 || { echo GATE_FAILED; exit 1; }
+A="--steps 5 --warmup 1 --no-cpu-baseline"
+for pass in 1 2; do
+  for r in ${RINGS:-1024 512 256}; do
+    timeout -k 10 200 python3 bench.py $A --opt inw_ring_pm=$r > $O/b_${r}_p$pass.json 2> $O/b_${r}_p$pass.err || exit 1
+  done
+done
+for r in ${RINGS:-1024 512 256}; do
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 200 rocprofv3 --pmc $c -d $O/pmc_${r}_$c -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --opt inw_ring_pm=$r > $O/pmc_${r}_$c.log 2>&1 || exit 1
+  done
+done
+python3 - $O <<'PY'
+import json, glob, sys, os, csv, collections
+o = sys.argv[1]
+for f in sorted(glob.glob(o + "/b_*.json")):
+    b = json.load(open(f))
+    print(os.path.basename(f), b["ms_per_step"], b["roofline"]["avg_launch_ms"], b["path"]["ring_entries"])
+for d in sorted(glob.glob(o + "/pmc_*_*")):
+    if not os.path.isdir(d):
+        continue
+    agg = collections.defaultdict(float)
+    for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "k_inw_pm" in r.get("Kernel_Name", ""):
+                agg[r["Counter_Name"]] += float(r["Counter_Value"])
+    print(os.path.basename(d), {k: round(v * 1024 / 2 / 1e9, 3) for k, v in agg.items()}, "GB per frame (KiB x 1024 / 2 frames, FETCH not doubled)")
+PY
