@@ -217,6 +217,10 @@ def main():
                          "(measured neutral on the 8-way frames: their time is set by long samples, not by rays)")
     ap.add_argument("--occupancy", action="store_true", help="report per-phase lane occupancy (diagnostic)")
     ap.add_argument("--save-image", default="", help="rank 0 saves the assembled frame (.npy) for checking")
+    ap.add_argument("--rebuild", action="store_true",
+                    help="secondary line: every step also does the reference's per-redraw scene work "
+                         "(RT_Base::OnUpdateBase, In-Next-Week/base.h:96-175): rt_pack_inw of the scene "
+                         "descriptions, then rt_dev_scene_inw_update with the LBVH built on the device, then the frame")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
                     help="set an rt_options field for this run (A/B of the exact strategies; recorded in the line)")
     ap.add_argument("--config", default="c3", choices=("c3", "c4", "c2", "ns"),
@@ -293,16 +297,38 @@ def main():
 
     per_rank = max(len(v) for v in lists)
     use_tiles(lists[part], per_rank)
+    if args.rebuild and not inw:
+        raise SystemExit("--rebuild: INW configs only (c3 / c4)")
+    rb_ms = np.zeros(6)  # per timed step: pack, records, LBVH, host structures, their upload, (unused)
+    rb_on = [False]
     lib.rt_debug_time_kernels(1)
     if args.occupancy:
         lib.rt_debug_counters(dbg.data_ptr())
     image = torch.empty((ny * T, nx * T, 4), dtype=torch.float32, device=dev) if rank == 0 else None
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
+    def rebuild():
+        """RT_Base<>::OnUpdateBase's per-redraw scene work on the device scene: FillBuffer and the
+        swept boxes (rt_pack_inw), the records, the LBVH on the device (ConstructLBVH_Buff,
+        base.h:135-142), the wide walk and RI grid on the host, every upload."""
+        t0 = time.perf_counter()
+        pk = R.pack(sc.desc, sc.n, sc.stage, build_lbvh=False)
+        t1 = time.perf_counter()
+        lt = pk["lights"] if len(pk["lights"]) else None
+        tm = (C.c_double * 4)()
+        rc = lib.rt_dev_scene_inw_update(scene, R.fptr(pk["geom"]), sc.n, None, R.fptr(pk["aabbs"]), R.fptr(lt),
+                                         pk["n_lights"], tm)
+        if rc != 0:
+            raise RuntimeError(f"rt_dev_scene_inw_update -> {rc}")
+        if rb_on[0]:
+            rb_ms[:5] += [(t1 - t0) * 1e3, tm[0], tm[1], tm[2], tm[3]]
+
     def step(i=None):
         mine, d_tiles, packed, depth = buf["mine"], buf["d_tiles"], buf["packed"], buf["depth"]
         gathered = buf["gathered"]
         stream = torch.cuda.current_stream()
+        if args.rebuild:
+            rebuild()
         if i is not None:
             ev[i][0].record(stream)
         if mine:
@@ -380,6 +406,7 @@ def main():
     if args.occupancy:
         lib.rt_debug_pixel_rays(buf["px_rays"].data_ptr())
     counters.zero_()
+    rb_on[0] = True
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -388,6 +415,12 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    rb_on[0] = False
+    blocking_ms = None
+    if args.rebuild and world == 1:  # the blocking entry point INTEGRATION.md binds (rt_render_inw): host in / out
+        tb = time.perf_counter()
+        R.render(sc)
+        blocking_ms = (time.perf_counter() - tb) * 1e3
 
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     ctr = counters.clone()
@@ -529,11 +562,21 @@ def main():
             "path": path,
             "options": {k: v for k, v in R.get_options().as_dict().items()
                         if v != R.default_options().as_dict()[k]} or "defaults",
-            "timed_region": "rt_render_tiles_async of one full frame per step (+ the RCCL gather and rank 0's "
-                            "frame assembly at N > 1) on a device scene built before timing: the host "
-                            "acceleration structures, the scene upload and the device allocations of the first "
-                            "frame are outside it (bench.py --rebuild times them per step)",
+            "timed_region": ("per step: rt_pack_inw + rt_dev_scene_inw_update (records, device LBVH, host wide "
+                             "walk + RI grid, uploads) + rt_render_tiles_async of one full frame (the reference's "
+                             "whole redraw, RT_Base::OnUpdateBase); only the first frame's device allocations are "
+                             "outside it") if args.rebuild else
+                            ("rt_render_tiles_async of one full frame per step (+ the RCCL gather and rank 0's "
+                             "frame assembly at N > 1) on a device scene built before timing: the host "
+                             "acceleration structures, the scene upload and the device allocations of the first "
+                             "frame are outside it (bench.py --rebuild times them per step)"),
         }
+        if args.rebuild:
+            out["rebuild_ms_per_step"] = dict(zip(("pack", "records", "lbvh_device", "host_structures", "upload"),
+                                                  [round(v / args.steps, 3) for v in rb_ms[:5]]))
+            out["rebuild_ms_per_step"]["render_events"] = round(kernel_ms, 3)
+            out["blocking_rt_render_inw_ms"] = round(blocking_ms, 1) if blocking_ms is not None else None
+            out["config"]["workload"] += " + per-step scene rebuild (--rebuild)"
         if args.occupancy:
             d = [int(v) for v in dbg.cpu().tolist()]
             out["lane_occupancy"] = {name: round(d[2 * i + 1] / max(d[2 * i], 1) / 64, 4)

@@ -273,6 +273,16 @@ rt_dev_scene *rt_dev_scene_inw_tex(const float *geom, uint32_t n, int layout, co
                                    const float *lights, uint32_t n_lights, const rt_texture *tex, int n_tex,
                                    int spp, int device);
 void rt_dev_scene_free(rt_dev_scene *s);
+/* The next frame's geometry for an INW scene: RT_Base<>::OnUpdateBase's per-redraw work
+ * (In-Next-Week/base.h:96-175: FillBuffer, LBVH::ConstructLBVH_Buff at :135-142, the texture
+ * uploads) on the scene's existing device buffers.  geom: N*28 records of the scene's layout;
+ * nodes: the caller's LBVH ((2N-1)*8), or NULL to build it on the device from aabbs (N*6, the
+ * swept boxes rt_pack_inw writes) with rt_lbvh_build_async; lights: the layout-4 light SSBO.
+ * The wide walk's structures and the RI grid are rebuilt on the host.  Synchronises the device
+ * first.  timing_ms (may be NULL) receives the host time of {records, LBVH (upload + device
+ * build + read-back), host structures, their upload}. */
+int rt_dev_scene_inw_update(rt_dev_scene *s, const float *geom, uint32_t n, const float *nodes, const float *aabbs,
+                            const float *lights, uint32_t n_lights, double timing_ms[4]);
 /* Replace the scene's options (the [build] ones keep the values the scene was built with). */
 int rt_dev_scene_set_options(rt_dev_scene *s, const rt_options *o);
 

@@ -77,6 +77,16 @@ struct DevBuf {  // RAII device allocation
         if (e != hipSuccess || !b) return e;
         return hipMemcpy(p, src, b, hipMemcpyHostToDevice);
     }
+    // copy b bytes in, reusing the allocation when it is large enough (a scene update); `bytes`
+    // stays the capacity
+    hipError_t store(const void *src, size_t b) {
+        if (!p || b > bytes) {
+            if (p) { (void)hipFree(p); p = nullptr; }
+            hipError_t e = alloc(b);
+            if (e != hipSuccess) return e;
+        }
+        return b ? hipMemcpy(p, src, b, hipMemcpyHostToDevice) : hipSuccess;
+    }
     template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
@@ -158,6 +168,9 @@ struct rt_dev_scene {
     float ri_lo[3] = {}, ri_hi[3] = {}, ri_inv[3] = {};
     int ri_dim[3] = {};
     int wdepth = 0;               // levels of the 4-wide culling BVH
+    uint32_t n_wnodes = 0;        // its nodes
+    bool ri_ok = false;           // the RI grid applies (ri_cells / ri_ids hold it)
+    DevBuf lbvh_ws;               // rt_dev_scene_inw_update: device LBVH workspace
     bool last_ln = false;         // the last INW fold launch used the LDS-staged kernels
     bool last_fu = false;         // ... their fused-fma cull instances
     uint32_t last_force = 0;      // ... its forced order (0: the probe's pick, read back from inw_mode)
@@ -327,8 +340,8 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     sc.rank = s->wrank.as<uint32_t>();
     sc.leafbox = s->wleaf.as<float4>();
     sc.dfs_high = s->dfs_high;
-    sc.n_wnodes = uint32_t(s->wnodes.bytes / (10 * sizeof(float4)));
-    if (s->ri_cells.p && s->opt.inw_ri_grid) {
+    sc.n_wnodes = s->n_wnodes;
+    if (s->ri_ok && s->opt.inw_ri_grid) {
         sc.ri_cells = s->ri_cells.as<uint32_t>();
         sc.ri_ids = s->ri_ids.as<uint32_t>();
         for (int a = 0; a < 3; a++) {
@@ -339,17 +352,26 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
 
 // The wide walk's structures and the RI grid, built on the host (rtamd::inw_wide_build,
 // rtamd::ri_grid_build) and uploaded.
-int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
+// ms (may be null): host time of the builds, then of the uploads
+int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n, double *ms = nullptr) {
     s->dfs_high = 0;
+    s->ri_ok = false;
+    const auto t0 = std::chrono::steady_clock::now();
     rtamd::InwWide w;
-    if (!s->opt.inw_wide_walk || !rtamd::inw_wide_build(nodes, n, w)) return RT_OK;
-    HIP_OK(s->wnodes.upload(w.wnodes.data(), w.wnodes.size() * sizeof(float)));
-    HIP_OK(s->wrank.upload(w.rank.data(), w.rank.size() * sizeof(uint32_t)));
-    HIP_OK(s->wleaf.upload(w.leafbox.data(), w.leafbox.size() * sizeof(float)));
-    const rtamd::RiGrid g = rtamd::ri_grid_build(w.leafbox.data(), n);
+    rtamd::RiGrid g;
+    const bool ok = s->opt.inw_wide_walk && rtamd::inw_wide_build(nodes, n, w);
+    if (ok) g = rtamd::ri_grid_build(w.leafbox.data(), n);
+    const auto t1 = std::chrono::steady_clock::now();
+    if (ms) ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    if (!ok) return RT_OK;
+    HIP_OK(s->wnodes.store(w.wnodes.data(), w.wnodes.size() * sizeof(float)));
+    s->n_wnodes = uint32_t(w.wnodes.size() / 40);
+    HIP_OK(s->wrank.store(w.rank.data(), w.rank.size() * sizeof(uint32_t)));
+    HIP_OK(s->wleaf.store(w.leafbox.data(), w.leafbox.size() * sizeof(float)));
     if (g.ok) {
-        HIP_OK(s->ri_cells.upload(g.cells.data(), g.cells.size() * sizeof(uint32_t)));
-        HIP_OK(s->ri_ids.upload(g.ids.data(), std::max<size_t>(1, g.ids.size()) * sizeof(uint32_t)));
+        HIP_OK(s->ri_cells.store(g.cells.data(), g.cells.size() * sizeof(uint32_t)));
+        HIP_OK(s->ri_ids.store(g.ids.data(), std::max<size_t>(1, g.ids.size()) * sizeof(uint32_t)));
+        s->ri_ok = true;
         for (int a = 0; a < 3; a++) {
             s->ri_lo[a] = g.lo[a]; s->ri_hi[a] = g.hi[a]; s->ri_inv[a] = g.inv[a]; s->ri_dim[a] = g.dim[a];
         }
@@ -357,13 +379,14 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n) {
     s->dfs_high = w.dfs_high;
     s->wdepth = w.depth;
     s->wbound = w.wbound;
+    if (ms) ms[1] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     return RT_OK;
 }
 
-int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const float *nodes,
-             const float *lights, uint32_t n_lights, const rt_texture *tex, int n_tex, int spp) {
-    if (int rc = upload_textures(s, layout == 4 ? tex : nullptr, layout == 4 ? n_tex : 0); rc != RT_OK) return rc;
-    std::vector<float> hot(size_t(n) * rtk::kInwHot, 0.0f), cold(size_t(n) * rtk::kInwCold, 0.0f);
+// The kernels' hot / cold records from the reference's GeometryBuff(_04) records (28 floats).
+void inw_records(const float *geom, uint32_t n, int layout, std::vector<float> &hot, std::vector<float> &cold) {
+    hot.assign(size_t(n) * rtk::kInwHot, 0.0f);
+    cold.assign(size_t(n) * rtk::kInwCold, 0.0f);
     for (uint32_t j = 0; j < n; j++) {
         const float *f = geom + size_t(j) * 28;
         float *h = hot.data() + size_t(j) * rtk::kInwHot;
@@ -387,16 +410,71 @@ int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const f
             std::memcpy(&c[7], &tu, 4);
         }
     }
+}
+
+int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const float *nodes,
+             const float *lights, uint32_t n_lights, const rt_texture *tex, int n_tex, int spp) {
+    if (int rc = upload_textures(s, layout == 4 ? tex : nullptr, layout == 4 ? n_tex : 0); rc != RT_OK) return rc;
+    std::vector<float> hot, cold;
+    inw_records(geom, n, layout, hot, cold);
     s->kind = layout == 4 ? 14 : 11;
     s->n = n; s->layout = layout; s->n_lights = layout == 4 ? n_lights : 0;
-    HIP_OK(s->hot.upload(hot.data(), hot.size() * sizeof(float)));
-    HIP_OK(s->cold.upload(cold.data(), cold.size() * sizeof(float)));
-    HIP_OK(s->nodes.upload(nodes, size_t(2 * n - 1) * 8 * sizeof(float)));
+    HIP_OK(s->hot.store(hot.data(), hot.size() * sizeof(float)));
+    HIP_OK(s->cold.store(cold.data(), cold.size() * sizeof(float)));
+    HIP_OK(s->nodes.store(nodes, size_t(2 * n - 1) * 8 * sizeof(float)));
     if (int rc = make_inw_wide(s, nodes, n); rc != RT_OK) return rc;
-    if (s->n_lights) HIP_OK(s->lights.upload(lights, size_t(s->n_lights) * 7 * sizeof(float)));
-    else HIP_OK(s->lights.alloc(16));
+    if (s->n_lights) HIP_OK(s->lights.store(lights, size_t(s->n_lights) * 7 * sizeof(float)));
+    else HIP_OK(s->lights.store(nullptr, 0));
     set_residency(s);
     return build_tables(s, spp);
+}
+
+// RT_Base<>::OnUpdateBase's per-redraw work on an existing device scene (In-Next-Week/base.h:
+// 96-175): new records, the LBVH (the caller's, or built on the device from the boxes), the wide
+// walk and RI grid rebuilt on the host, every upload into the scene's buffers.  ms[4]: host time
+// of the records, the LBVH (upload + device build + read-back), the host structures, their upload.
+int update_inw(rt_dev_scene *s, const float *geom, uint32_t n, const float *nodes, const float *aabbs,
+               const float *lights, uint32_t n_lights, double *ms) {
+    using clk = std::chrono::steady_clock;
+    auto t = clk::now();
+    auto lap = [&](int k) {
+        const auto now = clk::now();
+        if (ms) ms[k] = std::chrono::duration<double, std::milli>(now - t).count();
+        t = now;
+    };
+    std::vector<float> hot, cold;
+    inw_records(geom, n, s->layout, hot, cold);
+    s->n = n;
+    s->n_lights = s->layout == 4 ? n_lights : 0;
+    HIP_OK(s->hot.store(hot.data(), hot.size() * sizeof(float)));
+    HIP_OK(s->cold.store(cold.data(), cold.size() * sizeof(float)));
+    if (s->n_lights) HIP_OK(s->lights.store(lights, size_t(s->n_lights) * 7 * sizeof(float)));
+    lap(0);
+    const size_t nbytes = size_t(2 * n - 1) * 8 * sizeof(float);
+    std::vector<float> host_nodes;
+    if (!nodes) {  // ConstructLBVH_Buff on the device (rt_lbvh_build_async), read back for the host builders
+        if (n > (1u << 24)) return RT_E_UNSUPPORTED;
+        if (s->nodes.bytes < nbytes) {
+            s->nodes.~DevBuf();
+            new (&s->nodes) DevBuf();
+            HIP_OK(s->nodes.alloc(nbytes));
+        }
+        DevBuf d_aabb;
+        HIP_OK(d_aabb.upload(aabbs, size_t(n) * 6 * sizeof(float)));
+        const size_t ws = rtk::lbvh_workspace_bytes(n);
+        if (s->lbvh_ws.bytes < ws) { s->lbvh_ws.~DevBuf(); new (&s->lbvh_ws) DevBuf(); HIP_OK(s->lbvh_ws.alloc(ws)); }
+        HIP_OK(rtk::lbvh_build_device(d_aabb.as<float>(), n, s->nodes.as<float>(), s->lbvh_ws.p, ws, nullptr));
+        host_nodes.resize(nbytes / sizeof(float));
+        HIP_OK(hipMemcpy(host_nodes.data(), s->nodes.p, nbytes, hipMemcpyDeviceToHost));
+        nodes = host_nodes.data();
+    } else {
+        HIP_OK(s->nodes.store(nodes, nbytes));
+    }
+    lap(1);
+    double w[2] = {0.0, 0.0};
+    if (int rc = make_inw_wide(s, nodes, n, w); rc != RT_OK) return rc;
+    if (ms) { ms[2] = w[0]; ms[3] = w[1]; }
+    return RT_OK;
 }
 
 // Sample ranges of the render.  Default: one range (tail compaction keeps the SIMDs full).
@@ -1251,6 +1329,16 @@ int rt_options_get(rt_options *o) {
     if (!o) return RT_E_ARG;
     *o = g_opt;
     return RT_OK;
+}
+
+int rt_dev_scene_inw_update(rt_dev_scene *s, const float *geom, uint32_t n, const float *nodes, const float *aabbs,
+                            const float *lights, uint32_t n_lights, double timing_ms[4]) {
+    if (!s || s->kind == 3 || !geom || n == 0 || (!nodes && !aabbs)) return RT_E_ARG;
+    if (s->layout == 4 && n_lights > 0 && !lights) return RT_E_ARG;
+    if (s->n_tex == 0 && inw_textured(geom, n, s->layout)) return RT_E_UNSUPPORTED;
+    HIP_OK(hipSetDevice(s->device));
+    HIP_OK(hipDeviceSynchronize());  // the scene's last frame may still read the buffers being replaced
+    return update_inw(s, geom, n, nodes, aabbs, lights, n_lights, timing_ms);
 }
 
 int rt_dev_scene_set_options(rt_dev_scene *s, const rt_options *o) {

@@ -176,6 +176,8 @@ SIGNATURES = {
     "rt_options_set": (C.c_int, [C.POINTER(RtOptions)]),
     "rt_options_get": (C.c_int, [C.POINTER(RtOptions)]),
     "rt_dev_scene_set_options": (C.c_int, [C.c_void_p, C.POINTER(RtOptions)]),
+    "rt_dev_scene_inw_update": (C.c_int, [C.c_void_p, _FP, C.c_uint32, _FP, _FP, _FP, C.c_uint32,
+                                          C.POINTER(C.c_double)]),
     "rt_debug_path": (C.c_int, [C.c_void_p, C.POINTER(RtPathInfo)]),
 }
 

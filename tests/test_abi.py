@@ -95,6 +95,7 @@ def test_argument_validation_without_device():
     assert lib.rt_sample_tables(0, None, None, None) == R.RT_E_ARG
     assert lib.rt_scene_preset(999, 0, 0, None, 0, None, None) == R.RT_E_ARG
     assert lib.rt_render_tiles_async(None, None, None, None, 0, 16, None, None, None, None) == R.RT_E_ARG
+    assert lib.rt_dev_scene_inw_update(None, R.fptr(buf), 1, None, None, None, 0, None) == R.RT_E_ARG
 
 
 def test_textured_records_rejected_before_device():

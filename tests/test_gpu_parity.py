@@ -165,3 +165,53 @@ def test_repeated_frames_on_one_device_scene(gpu):
         assert compare(a, g)["exact_frac"] == 1.0, i
         assert compare(d, gd)["exact_frac"] == 1.0, i
         assert n == gs, i
+
+
+@pytest.mark.parametrize("device_lbvh", [False, True])
+def test_scene_update_matches_fresh_scene(gpu, device_lbvh):
+    """rt_dev_scene_inw_update (the per-redraw work of RT_Base::OnUpdateBase, In-Next-Week/base.h:
+    96-175) on an existing device scene: moved objects, the LBVH given or built on the device,
+    then a frame -- bit-identical to a scene built from scratch for the moved objects, and to the
+    oracle."""
+    import ctypes as C
+
+    import torch
+
+    a = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 3000, width=64, height=36, spp=12)
+    b = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 3000, width=64, height=36, spp=12)
+    for i in range(b.n):  # every object moves
+        for k in range(3):
+            b.desc[i].position[k] += 0.25 * ((i + k) % 3 - 1)
+    for k, v in R.pack(b.desc, b.n, b.stage).items():
+        setattr(b, k, v)
+    lib = R.load()
+    dev = torch.device("cuda")
+
+    def frame(s):
+        img = torch.zeros((36, 64, 4), dtype=torch.float32, device=dev)
+        dep = torch.zeros((36, 64), dtype=torch.float32, device=dev)
+        ctr = torch.zeros(6, dtype=torch.int64, device=dev)
+        assert lib.rt_render_image_async(s, C.byref(b.camera), C.byref(b.params), img.data_ptr(), dep.data_ptr(),
+                                         ctr.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        return img.cpu().numpy(), dep.cpu().numpy(), int(ctr[0].item())
+
+    s = lib.rt_dev_scene_inw(R.fptr(a.geom), a.n, 1, R.fptr(a.nodes), None, 0, a.params.spp, -1)
+    f = lib.rt_dev_scene_inw(R.fptr(b.geom), b.n, 1, R.fptr(b.nodes), None, 0, b.params.spp, -1)
+    assert s and f
+    try:
+        frame(s)  # a frame of the old geometry first
+        tm = (C.c_double * 4)()
+        rc = lib.rt_dev_scene_inw_update(s, R.fptr(b.geom), b.n, None if device_lbvh else R.fptr(b.nodes),
+                                         R.fptr(b.aabbs), None, 0, tm)
+        assert rc == 0
+        print("update ms", list(tm))
+        g, gd, gs = frame(s)
+        h, hd, hs = frame(f)
+    finally:
+        lib.rt_dev_scene_free(s)
+        lib.rt_dev_scene_free(f)
+    o, od, ost = O.render(b)
+    for x, y in ((g, h), (gd, hd), (g, o), (gd, od)):
+        assert compare(x, y)["exact_frac"] == 1.0
+    assert gs == hs == ost["segments"]
