@@ -1795,7 +1795,9 @@ __device__ float inw_surrounding_ri(const InwScene &S, FStack &K, f3 hp, float r
 // then the child links.  The repeat lets a ray read its near and far planes of axis a at
 // a + 3*s_a and a + 3 + 3*s_a (s_a = 1 when d_a < 0): one per-lane offset per axis (inw_wnode_nf).
 constexpr int kInwNodeF4 = 10;
-constexpr int kInwLdsNodes = 256;  // 40 KB: what 3 x 256-lane stacks (120 KB) leave of 160 KB
+// 236 nodes (36.9 KB): what the 3 x 256-lane stacks (120 KB) and k_inw_pm's depth slots (3 KB)
+// leave of 160 KB
+constexpr int kInwLdsNodes = 236;
 __shared__ float4 g_inw_lnodes[kInwLdsNodes * kInwNodeF4];
 template <bool LN>
 __device__ __forceinline__ const float4 *inw_node_ptr(const InwScene &S, int cur) {
@@ -2765,6 +2767,9 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     if (inw_sample_major(mode, force)) return;  // the probe picked k_inw_sm for this frame
     constexpr int SUB = LN ? 3 : 1;
     __shared__ float lds[SUB * kFStack * kBlock];
+    // per wave: the middle sample's depth of claimed ordinal j (slot j % 64; at most 64 ordinals lie
+    // between the fold and the issue), written out with the pixel's colour
+    __shared__ float s_pdep[SUB * kBlock];
     InwScene S = S0;
     if constexpr (LN) {
         const uint32_t n = S.wnodes ? (S.n_wnodes < (uint32_t)kInwLdsNodes ? S.n_wnodes : (uint32_t)kInwLdsNodes) : 0u;
@@ -2781,6 +2786,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t rsize = rmask + 1u;
     float4 *wr = ring + (size_t)uni((blockIdx.x * (SUB * kBlock) + threadIdx.x) >> 6) * rsize;
+    float *pdep = s_pdep + (threadIdx.x & ~63u);
     const uint32_t spp = (uint32_t)f.spp, mid = spp / 2u, total = units_total(f);
     const float inv = rcp((float)f.spp);
     // wave-uniform: stream positions (entry gi / fold gf) as (pixel ordinal, sample), claims
@@ -2792,7 +2798,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     uint32_t pix_slot = 0xffffffffu;   // lane l: the unit of the claimed ordinal j with j % 64 == l
     // per lane: the sample it traces
     bool busy = false;
-    uint32_t g = 0;
+    uint32_t g = 0, pj = 0;  // the lane's stream entry and its pixel's ordinal slot (j % 64)
     int s = 0;
     UnitPix px{};
     uint32_t bu = kBeamOff;  // the lane's pixel unit for its beam list (S.beam)
@@ -2829,14 +2835,16 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 for (; j < e; j++) acc = acc + f3{rdl(v.x, j), rdl(v.y, j), rdl(v.z, j)};
                 sf += e - i;
                 i = e;
-                if (sf == spp) {  // pixel jf complete: End()'s imageStore (01_BVH...glsl:652)
+                if (sf == spp) {  // pixel jf complete: End()'s imageStores (01_BVH...glsl:652, 667-668)
                     const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
                     if (lane == 0) {
                         const UnitPix p = unit_pixel(f, unit);
-                        if (p.out != (size_t)-1)
+                        if (p.out != (size_t)-1) {
                             reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
                                 make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
                                             p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
+                            if (f.out_depth) f.out_depth[p.out] = pdep[jf & 63u];
+                        }
                     }
                     sf = 0;
                     jf++;
@@ -2888,6 +2896,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 const uint32_t unit = (uint32_t)__shfl((int)pix_slot, (int)(jl & 63u), 64);
                 if (!busy && rank < take) {
                     g = gi + rank;
+                    pj = jl & 63u;
                     s = (int)(adv - q * spp);
                     if (unit != pu) {
                         pu = unit;
@@ -2901,7 +2910,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                         busy = true;
                         inw_start_sample_cd(S, f, K, pcd, s, c);
                     } else {  // a padding slot: an empty sample, folded as zero
-                        if ((uint32_t)s == mid && f.out_depth && px.out != (size_t)-1) f.out_depth[px.out] = 0.0f;
+                        if ((uint32_t)s == mid) pdep[pj] = 0.0f;
                         wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(ring_tag(S, g)));
                     }
                 }
@@ -2923,7 +2932,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
                                         __uint_as_float(ring_tag(S, g)));
-            if ((uint32_t)s == mid && f.out_depth) f.out_depth[px.out] = dep;  // 01_BVH...glsl:667-668
+            if ((uint32_t)s == mid) pdep[pj] = dep;  // 01_BVH...glsl:667-668, stored with the pixel's colour
             busy = false;
         }
     }

@@ -30,3 +30,5 @@ for d in sorted(glob.glob(o + "/pmc_*_*")):
                 agg[r["Counter_Name"]] += float(r["Counter_Value"])
     print(os.path.basename(d), {k: round(v * 1024 / 2 / 1e9, 3) for k, v in agg.items()}, "GB per frame (KiB x 1024 / 2 frames, FETCH not doubled)")
 PY
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "update" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/update.log 2>&1 || { echo UPDATE_FAILED; exit 1; }
+timeout -k 10 300 python3 bench.py --rebuild --steps 5 --warmup 1 --no-cpu-baseline > $O/rebuild.json 2> $O/rebuild.err || exit 1
