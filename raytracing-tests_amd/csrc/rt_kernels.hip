@@ -48,13 +48,31 @@ __device__ __forceinline__ Pix map_pixel(const Frame &f) {
     return p;
 }
 
+// occupancy slots (RT_DIAG_OCC): pairs (wave iterations, lanes) of: the fold loop's iterations with
+// busy lanes; wide-walk trips with walking lanes; their node steps; leaf batches; beam-list trips;
+// reference-walk entries (lanes that fell back); surrounding-RI queries
+enum { kOccSeg = 0, kOccWalk = 2, kOccNode = 4, kOccLeaf = 6, kOccBeam = 8, kOccRef = 10, kOccRi = 12, kOccSlots = 14 };
 struct Ctr {
     uint32_t seg = 0, nodes = 0, prims = 0, shadow = 0, drops = 0, nans = 0;
     unsigned long long *wdbg = nullptr;  // diagnostics: this wave's kDbg* row in LDS, or null
 #ifdef RT_DIAG_SPLIT
     unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // INW phase cycles of this wave (k_inw_pm/sm)
 #endif
+#ifdef RT_DIAG_OCC
+    unsigned long long occ[kOccSlots] = {};  // INW lane occupancy per phase (OCC_TALLY), wave-uniform
+#endif
 };
+// INW lane occupancy (diagnostic builds, -DRT_DIAG_OCC; tools/inw_occ.py): per phase, the wave
+// iterations and the lanes in them doing that phase's work, summed into Frame::dbg[32 + slot] at exit
+#ifdef RT_DIAG_OCC
+#define OCC_TALLY(c, k, pred)                                                    \
+    do {                                                                         \
+        (c).occ[k] += 1;                                                         \
+        (c).occ[(k) + 1] += (unsigned long long)__popcll(__ballot(pred));        \
+    } while (0)
+#else
+#define OCC_TALLY(c, k, pred) ((void)0)
+#endif
 // INW phase split (diagnostic builds, -DRT_DIAG_SPLIT): shader-clock cycles per wave of a phase,
 // summed into Frame::dbg slots by the fold kernels at exit
 #ifdef RT_DIAG_SPLIT
@@ -1928,6 +1946,8 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
         }
     };
     for (;;) {
+        OCC_TALLY(c, kOccWalk, walking);
+        OCC_TALLY(c, kOccNode, walking && cur > 0);
         if (walking) {
             bool pop;
             if (cur > 0) {
@@ -1960,6 +1980,7 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
             if (ovf) walking = false;
         }
         if (__all(!walking || pend >= 0)) {
+            OCC_TALLY(c, kOccLeaf, pend >= 0);
             if (pend >= 0) { leaf(pend); pend = -1; }
             if (__all(!walking)) break;
         }
@@ -2015,6 +2036,7 @@ __device__ float inw_closest_beam(const InwScene &S, const FStack &K, f3 o, f3 d
             act = __uint_as_float(e.y) <= lim;
         }
         if (!__any(act)) break;
+        OCC_TALLY(c, kOccBeam, act);
         if (act) {
             const int g = (int)e.x;
             c.prims++;
@@ -2178,6 +2200,7 @@ __device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o,
                                              float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c) {
     bool ok = false;
     const float g = inw_traverse_wide<WANT_NORMAL, LN, FU>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c, ok);
+    OCC_TALLY(c, kOccRef, !ok);
     if (ok) return g;
     return inw_traverse<WANT_NORMAL>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
 }
@@ -2366,6 +2389,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         if (!LIGHTS && (ri_forced || (ri_read && contribution > 0.01f && bounced + 1.0f < (float)F.max_bounces)))
         {
             INW_T0(t_ri);
+            OCC_TALLY(c, kOccRi, true);
             surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
             INW_CYC(c, 1, t_ri);
         }
@@ -2924,6 +2948,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         if (qdone && ji == nclaimed && gf == gi && __ballot(busy) == 0) break;
         // ---- one ray segment per busy lane (samples are independent invocations)
         INW_T0(t_seg);
+        OCC_TALLY(c, kOccSeg, busy);
         if (busy) {
             inw_segment<LIGHTS, LN, FU>(S, f, K, s, col, dep, c, bu);
             if (f.px_rays) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
@@ -2952,6 +2977,10 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         if (t_qd) atomicMin(t + 2, t_qd);
         atomicMin(t + 3, t_end); atomicMax(t + 4, t_end);
     }
+#endif
+#ifdef RT_DIAG_OCC
+    if (f.dbg && lane == 0)
+        for (int k = 0; k < kOccSlots; k++) atomicAdd(f.dbg + 32 + k, c.occ[k]);
 #endif
     flush(f, c);
 }

@@ -32,3 +32,5 @@ for d in sorted(glob.glob(o + "/pmc_*_*")):
 PY
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "update" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/update.log 2>&1 || { echo UPDATE_FAILED; exit 1; }
 timeout -k 10 300 python3 bench.py --rebuild --steps 5 --warmup 1 --no-cpu-baseline > $O/rebuild.json 2> $O/rebuild.err || exit 1
+RT_HIP_LIB=$GRAFT_REPO_ROOT/raytracing-tests_amd/librt_hip_occ.so timeout -k 10 200 python3 tools/inw_occ.py c3 > $O/occ_c3.json 2> $O/occ_c3.err || exit 1
+RT_HIP_LIB=$GRAFT_REPO_ROOT/raytracing-tests_amd/librt_hip_occ.so timeout -k 10 200 python3 tools/inw_occ.py c5 64 > $O/occ_c5.json 2> $O/occ_c5.err || exit 1
