@@ -68,6 +68,12 @@ CONFIGS = {
            "In-One-Weekend 03_Adding_Materials final scene, 1200x800, 100 spp, 50 bounces, tile-partitioned "
            "across {n} MI355X with an RCCL gather",
            "synthetic (seeded final-scene generator, SURVEY 8d seed 20250131)"),
+    "c5": ("INW04_CORNELL", 7, 0, {},
+           "In-Next-Week 04_Lighting Cornell-box emissive scene, 4096x4096, 2000 spp, 50 bounces, 1 MI355X "
+           "(BASELINE configs[4])",
+           "In-Next-Week 04_Lighting Cornell-box emissive scene, 4096x4096, 2000 spp, 50 bounces, tile-partitioned "
+           "across {n} MI355X with an RCCL gather",
+           "synthetic (Cornell-style box generator, SURVEY 8d seed 7)"),
     "ns": ("IOW03_FINAL", 20250131, 0, {"width": 1920, "height": 1080, "spp": 500},
            "In-One-Weekend 03 final scene, 1920x1080, 500 spp, 50 bounces (BASELINE north_star workload)",
            "In-One-Weekend 03 final scene, 1920x1080, 500 spp, 50 bounces, tile-partitioned across {n} MI355X "
@@ -83,9 +89,9 @@ def algorithmic_flops(st: dict) -> float:
 
 def algorithmic_bytes(st: dict, pixels: int, inw: bool = False) -> float:
     """SURVEY.md 8d contract: B_alg = 32*node_visits + 96*prim_tests (IOW records) + 16*W*H;
-    INW: 112-B records and 20 B per pixel (colour + depth)."""
-    if inw:
-        return 32.0 * st["node_visits"] + 112.0 * st["prim_tests"] + 20.0 * pixels
+    INW: 112-B records, 28 B per shadow query's light record and 20 B per pixel (colour + depth)."""
+    if inw:  # + the 28-B light record each shadow query reads (INW-04)
+        return 32.0 * st["node_visits"] + 112.0 * st["prim_tests"] + 28.0 * st["shadow_queries"] + 20.0 * pixels
     return 32.0 * st["node_visits"] + 96.0 * st["prim_tests"] + 16.0 * pixels
 
 
@@ -223,9 +229,9 @@ def main():
                          "descriptions, then rt_dev_scene_inw_update with the LBVH built on the device, then the frame")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
                     help="set an rt_options field for this run (A/B of the exact strategies; recorded in the line)")
-    ap.add_argument("--config", default="c3", choices=("c3", "c4", "c2", "ns"),
+    ap.add_argument("--config", default="c3", choices=("c3", "c4", "c2", "c5", "ns"),
                     help="c3 (= c4): BASELINE configs[2] / configs[3], the headline; c2: configs[1]; "
-                         "ns: the north star's IOW-03 workload")
+                         "c5: configs[4]; ns: the north star's IOW-03 workload")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -277,7 +283,9 @@ def main():
     lists = [allt[r::nparts] for r in range(nparts)]  # the hashed deal (first frame)
 
     if inw:
-        scene = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, sc.layout, R.fptr(sc.nodes), None, 0, spp, local)
+        lt = sc.lights if sc.lights is not None and len(sc.lights) else None
+        scene = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, sc.layout, R.fptr(sc.nodes), R.fptr(lt), sc.n_lights, spp,
+                                     local)
     else:
         scene = lib.rt_dev_scene_iow03(R.fptr(sc.types), R.fptr(sc.records), sc.n, spp, local)
     if not scene:
@@ -503,6 +511,8 @@ def main():
             # ~10-20 s of host work on the GPU box (C3: 3.2 Mrays/s on 16 cores for the central block)
             if cfg == "c3":
                 cpu, ref = cpu_baseline(sc, cores, args.cpu_spp or sc.params.spp, bw=256, rows_per_core=4)
+            elif cfg == "c5":  # 2000 spp, ~6 rays per sample with the shadow queries
+                cpu, ref = cpu_baseline(sc, cores, args.cpu_spp or sc.params.spp, bw=32, rows_per_core=2)
             else:  # IOW-03: ~280 rays per sample; ns has 5x the samples per pixel of c2
                 cpu, ref = cpu_baseline(sc, cores, args.cpu_spp or sc.params.spp, bw=16 if cfg == "ns" else 64)
             rect, ref_rgba, ref_depth, ref_spp = ref
