@@ -1926,6 +1926,9 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
     const int base = (int)K.size, cap = kFStack - 3 - base;  // 3 spare slots for branch-free pushes
     const uint32_t ox = d.x < 0.0f ? 3u : 0u, oy = d.y < 0.0f ? 4u : 1u, oz = d.z < 0.0f ? 5u : 2u;
     int sp = 0, pend = -1, cur = S.wroot;
+#ifdef RT_INW_PEND2
+    int pend2 = -1;
+#endif
     bool walking = ok, ovf = false;
     float lim = bt * 1.0001f + 1e-3f;
     auto leaf = [&](int g) {
@@ -1970,8 +1973,14 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
                 cur = k0;
                 pop = t0 == kMiss;
             } else {
+#ifdef RT_INW_PEND2  // experiment: two postponed leaves per lane
+                pop = pend2 < 0;
+                if (pend < 0) pend = -cur;
+                else if (pend2 < 0) pend2 = -cur;
+#else
                 pop = pend < 0;  // a leaf waits while the lane still holds one
                 if (pop) pend = -cur;
+#endif
             }
             if (pop) {
                 if (sp == 0) walking = false;
@@ -1979,11 +1988,22 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
             }
             if (ovf) walking = false;
         }
+#ifdef RT_INW_PEND2
+        if (__all(!walking || pend2 >= 0)) {
+            OCC_TALLY(c, kOccLeaf, pend >= 0);
+            if (pend >= 0) { leaf(pend); pend = pend2; pend2 = -1; }
+            if (__all(!walking)) {
+                if (pend >= 0) { leaf(pend); pend = -1; }
+                break;
+            }
+        }
+#else
         if (__all(!walking || pend >= 0)) {
             OCC_TALLY(c, kOccLeaf, pend >= 0);
             if (pend >= 0) { leaf(pend); pend = -1; }
             if (__all(!walking)) break;
         }
+#endif
     }
     if (ovf) ok = false;
     if (!ok) return init_geom;

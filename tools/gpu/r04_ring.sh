@@ -1,19 +1,29 @@
-# Fold-ring window A/B (round 4): parity gate, then bench frames and PMC HBM bytes per ring size.
+# Round-4 A/B on one box: parity gates, bench frames for fold-ring windows and the two-leaf walk
+# variant, PMC HBM bytes per ring size, INW lane occupancy, the --rebuild line.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/r04_ring; rm -rf $O; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "repeated or inw01_random" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/gate.log 2>&1 || { echo GATE_FAILED; exit 1; }
+L=$GRAFT_REPO_ROOT/raytracing-tests_amd
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "repeated or inw01_random or update" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/gate.log 2>&1 || { echo GATE_FAILED; exit 1; }
+RT_HIP_LIB=$L/librt_hip_pend2.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "inw01_random or inw04" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/gate_pend2.log 2>&1 || { echo GATE_PEND2_FAILED; exit 1; }
 A="--steps 5 --warmup 1 --no-cpu-baseline"
 for pass in 1 2; do
-  for r in ${RINGS:-1024 512 256}; do
-    timeout -k 10 200 python3 bench.py $A --opt inw_ring_pm=$r > $O/b_${r}_p$pass.json 2> $O/b_${r}_p$pass.err || exit 1
+  for v in base r512 r256 pend2; do
+    X=""; LIB=$L/librt_hip.so
+    [ $v = r512 ] && X="--opt inw_ring_pm=512"
+    [ $v = r256 ] && X="--opt inw_ring_pm=256"
+    [ $v = pend2 ] && LIB=$L/librt_hip_pend2.so
+    RT_HIP_LIB=$LIB timeout -k 10 200 python3 bench.py $A $X > $O/b_${v}_p$pass.json 2> $O/b_${v}_p$pass.err || exit 1
   done
 done
-for r in ${RINGS:-1024 512 256}; do
+for r in 1024 256; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 200 rocprofv3 --pmc $c -d $O/pmc_${r}_$c -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --opt inw_ring_pm=$r > $O/pmc_${r}_$c.log 2>&1 || exit 1
   done
 done
+RT_HIP_LIB=$L/librt_hip_occ.so timeout -k 10 200 python3 tools/inw_occ.py c3 > $O/occ_c3.json 2> $O/occ_c3.err || exit 1
+RT_HIP_LIB=$L/librt_hip_occ.so timeout -k 10 200 python3 tools/inw_occ.py c5 64 > $O/occ_c5.json 2> $O/occ_c5.err || exit 1
+timeout -k 10 300 python3 bench.py --rebuild --steps 5 --warmup 1 --no-cpu-baseline > $O/rebuild.json 2> $O/rebuild.err || exit 1
 python3 - $O <<'PY'
 import json, glob, sys, os, csv, collections
 o = sys.argv[1]
@@ -30,7 +40,3 @@ for d in sorted(glob.glob(o + "/pmc_*_*")):
                 agg[r["Counter_Name"]] += float(r["Counter_Value"])
     print(os.path.basename(d), {k: round(v * 1024 / 2 / 1e9, 3) for k, v in agg.items()}, "GB per frame (KiB x 1024 / 2 frames, FETCH not doubled)")
 PY
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "update" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/update.log 2>&1 || { echo UPDATE_FAILED; exit 1; }
-timeout -k 10 300 python3 bench.py --rebuild --steps 5 --warmup 1 --no-cpu-baseline > $O/rebuild.json 2> $O/rebuild.err || exit 1
-RT_HIP_LIB=$GRAFT_REPO_ROOT/raytracing-tests_amd/librt_hip_occ.so timeout -k 10 200 python3 tools/inw_occ.py c3 > $O/occ_c3.json 2> $O/occ_c3.err || exit 1
-RT_HIP_LIB=$GRAFT_REPO_ROOT/raytracing-tests_amd/librt_hip_occ.so timeout -k 10 200 python3 tools/inw_occ.py c5 64 > $O/occ_c5.json 2> $O/occ_c5.err || exit 1
