@@ -1923,6 +1923,10 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
     const uint32_t *rank = S.rank + (invert ? S.n : 0u);
     const f3 fid = f3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
     const f3 noid = f3{-(o.x * fid.x), -(o.y * fid.y), -(o.z * fid.z)};  // the fused cull's per-ray term (FU)
+    // the fused planes need a finite per-ray term: a direction component near the smallest normal
+    // float with |o| ~ 10^3 overflows it, and every fma would be -inf or NaN (every child culled);
+    // such a ray takes the reference walk
+    if (FU) ok = ok && __builtin_isfinite(noid.x) && __builtin_isfinite(noid.y) && __builtin_isfinite(noid.z);
     const int base = (int)K.size, cap = kFStack - 3 - base;  // 3 spare slots for branch-free pushes
     const uint32_t ox = d.x < 0.0f ? 3u : 0u, oy = d.y < 0.0f ? 4u : 1u, oz = d.z < 0.0f ? 5u : 2u;
     int sp = 0, pend = -1, cur = S.wroot;
