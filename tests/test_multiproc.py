@@ -3,8 +3,10 @@
 bench.py deals tiles round-robin to ranks (64x64 on one GPU, 16x16 across ranks in a hashed
 order), each rank packs its tiles, one gather brings
 them to rank 0, and rank 0 assembles the frame.  Here every rank "renders" a
-deterministic per-pixel pattern into its packed tiles; the assembled frame must equal the
-pattern everywhere, and the tile lists must cover every tile exactly once.
+deterministic per-pixel pattern into its packed tiles (the assembled frame must equal the
+pattern everywhere, and the tile lists must cover every tile exactly once), and, with the CPU
+oracle as the renderer, the tiles of real INW-01 / IOW-03 frames, whose assembly must equal the
+single render bit for bit with the same summed ray count.
 """
 import math
 import os
@@ -111,3 +113,67 @@ def test_lpt_deal_balances_and_assembles():
             blk = ref[ty * T:ty * T + T, tx * T:tx * T + T]
             src[r, k, :blk.shape[0], :blk.shape[1]] = blk
     assert torch.equal(bench.assemble_lists(src, lists, nx, ny)[:H, :W], ref)
+
+
+def _render_worker(rank, world, port, T, case, q):
+    """One rank of a rendered partition: this rank's tiles of a real frame (rendered by the CPU
+    oracle, tile by tile, as the reference dispatches tile rectangles), packed as
+    rt_render_tiles_async packs them, gathered to rank 0 and assembled there; the ray counters
+    are summed over ranks as bench.py sums them."""
+    import sys
+    sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__)))]
+    import numpy as np
+
+    import rt_amd as R
+    from oracle import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        O.set_threads(1)
+        preset, seed, n, over = case
+        sc = R.make_scene(preset, seed, n, **over)
+        W, H = sc.params.width, sc.params.height
+        allt, mine, per_rank = bench.tiles_for_rank(W, H, world, rank, T)
+        packed = torch.zeros((per_rank, T, T, 4))
+        seg = torch.zeros(1, dtype=torch.float64)
+        for k, (tx, ty) in enumerate(mine):
+            p = R.RtParams.from_buffer_copy(sc.params)
+            p.tile_x0, p.tile_y0 = tx * T, ty * T
+            p.tile_w, p.tile_h = min(T, W - tx * T), min(T, H - ty * T)
+            img, _, st = O.render(sc, p)
+            blk = torch.from_numpy(img[p.tile_y0:p.tile_y0 + p.tile_h, p.tile_x0:p.tile_x0 + p.tile_w].copy())
+            packed[k, :blk.shape[0], :blk.shape[1]] = blk
+            seg += st["segments"]
+        gathered = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
+        dist.gather(packed, gathered, dst=0)
+        dist.all_reduce(seg)
+        if rank == 0:
+            nx, ny = math.ceil(W / T), math.ceil(H / T)
+            img = bench.assemble_frame(torch.stack(gathered, 0), allt, nx, ny)[:H, :W].numpy()
+            full, _, fst = O.render(sc)
+            q.put(bool(np.array_equal(img.view(np.uint32), full.view(np.uint32))) and int(seg.item()) == fst["segments"])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,T,case", [
+    (2, 16, ("INW", 1234, 3000, dict(width=72, height=40, spp=6))),
+    (3, 16, ("IOW", 20250131, 0, dict(width=40, height=24, spp=3))),
+])
+def test_gather_of_rendered_tiles(world, T, case):
+    """The multi-GPU exchange on rendered content: ranks render their dealt tiles of a real INW-01 /
+    IOW-03 frame, one gather assembles the frame on rank 0, and it equals the single render bit
+    for bit with the same ray count (CPU oracle as the renderer, gloo as the transport)."""
+    import rt_amd as R
+    preset = R.PRESET_INW01_RANDOM if case[0] == "INW" else R.PRESET_IOW03_FINAL
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_render_worker, args=(r, world, port, T, (preset,) + case[1:], q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True
