@@ -194,6 +194,7 @@ struct rt_dev_scene {
     DevBuf sp_front;   // checkpoint rounds: per-pixel frontier (uint4)
     DevBuf sp_sorder, sp_fcost;  // heavy-first enumeration: sample indices by cost, their costs
     DevBuf inw_ring;             // k_inw_pm / k_inw_sm: the waves' fold rings
+    DevBuf inw_park;             // RT_INW_PARK builds: parked walk state per lane
     DevBuf inw_mode;             // k_inw_probe's verdict (2 uints)
     DevBuf inw_cost;             // claim order: block cost keys, the order, 256 bucket offsets
     DevBuf inw_beam, inw_beam_n;  // pixel beams: beam_cap (id, entry t) per unit; count + cut per unit
@@ -1121,6 +1122,17 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                      s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
     set_wide(s, sc);
     sc.ring_epoch = epoch << 26;
+#ifdef RT_INW_PARK  // walk parking (experiment): 2 float4 per lane of the fold grid
+    {
+        const size_t need = waves * 64 * 2 * sizeof(float4);
+        if (s->inw_park.bytes < need) {
+            s->inw_park.~DevBuf();
+            new (&s->inw_park) DevBuf();
+            if (s->inw_park.alloc(need) != hipSuccess) return RT_E_HIP;
+        }
+        sc.park = s->inw_park.as<float4>();
+    }
+#endif
     // the fused cull (cull4nf<true>: one fma per plane) while every ray origin -- the camera (+ lens and the unit step
     // of the primary ray), hit points inside the scene's boxes -- lies within 1000 of the origin
     // (DESIGN.md §2); not with the MULTIFOCUS lens chain, whose lens points are farther out

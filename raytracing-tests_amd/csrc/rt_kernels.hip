@@ -1909,9 +1909,30 @@ __device__ __forceinline__ void cull4nf(const float4 nx, const float4 ny, const 
 // inside its own box, and then skipping it changes nothing; but where an object's face coincides
 // with its box face, rounding can put t an ulp below te.  Any accepted candidate with t < te
 // therefore hands the ray to the reference walk (ok = false).
-template <bool WANT_NORMAL, bool LN = false, bool FU = false>
+// Walk parking (RT_INW_PARK experiment, DESIGN.md §5 "Walk parking"): a wave's walk loop runs
+// as long as its slowest lane; with PK, once at most kParkLanes lanes still walk (after at least
+// kParkMinTrips trips) the wave tests the pending leaves, saves those lanes' walk state to their
+// slot (2 float4: cur, sp, best object, its rank; best t, culling limit) and leaves the loop, so
+// the other lanes shade and start their next segments; the parked lanes resume their walk in the
+// next iteration of the fold kernel, next to the new walks.  The segment's ray stays in the
+// shared stack (the walk's stack starts 8 floats above it).  The walk's result does not depend on
+// when its node steps run, so the image and the counters are unchanged.
+#ifndef RT_INW_PARK_LANES
+#define RT_INW_PARK_LANES 8
+#endif
+#ifndef RT_INW_PARK_MIN
+#define RT_INW_PARK_MIN 4
+#endif
+constexpr int kParkLanes = RT_INW_PARK_LANES, kParkMinTrips = RT_INW_PARK_MIN;
+struct WalkPark {
+    float4 *slot;   // this lane's 2 float4
+    bool resume;    // the walk was parked in an earlier iteration: restore it
+    bool parked;    // out: parked again
+};
+template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false>
 __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
-                                   f3 &normal, float &extra, float init_geom, Ctr &c, bool &ok) {
+                                   f3 &normal, float &extra, float init_geom, Ctr &c, bool &ok,
+                                   WalkPark *wp = nullptr) {
     const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};  // the reference's reciprocals (test_aabb)
     ok = S.wnodes != nullptr && K.size + S.dfs_high <= (uint32_t)kFStack && __builtin_isfinite(id.x) &&
          __builtin_isfinite(id.y) && __builtin_isfinite(id.z) && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
@@ -1927,7 +1948,8 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
     // float with |o| ~ 10^3 overflows it, and every fma would be -inf or NaN (every child culled);
     // such a ray takes the reference walk
     if (FU) ok = ok && __builtin_isfinite(noid.x) && __builtin_isfinite(noid.y) && __builtin_isfinite(noid.z);
-    const int base = (int)K.size, cap = kFStack - 3 - base;  // 3 spare slots for branch-free pushes
+    // 3 spare slots for branch-free pushes; PK: the segment's ray (8 floats) stays below the walk
+    const int base = (int)K.size + (PK ? 8 : 0), cap = kFStack - 3 - base;
     const uint32_t ox = d.x < 0.0f ? 3u : 0u, oy = d.y < 0.0f ? 4u : 1u, oz = d.z < 0.0f ? 5u : 2u;
     int sp = 0, pend = -1, cur = S.wroot;
 #ifdef RT_INW_PEND2
@@ -1935,6 +1957,15 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
 #endif
     bool walking = ok, ovf = false;
     float lim = bt * 1.0001f + 1e-3f;
+    if constexpr (PK) {
+        if (wp->resume) {  // a parked walk: its state from the slot (ok held when it parked)
+            const float4 a = wp->slot[0], b = wp->slot[1];
+            cur = __float_as_int(a.x); sp = __float_as_int(a.y); bg = __float_as_int(a.z); br = __float_as_uint(a.w);
+            bt = b.x; lim = b.y;
+        }
+        wp->parked = false;
+    }
+    int trips = 0;
     auto leaf = [&](int g) {
         c.prims++;
         const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
@@ -2008,7 +2039,23 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
             if (__all(!walking)) break;
         }
 #endif
+        if constexpr (PK) {
+            if (++trips >= kParkMinTrips && __popcll(__ballot(walking)) <= kParkLanes) {
+                if (__any(pend >= 0)) {  // every pending leaf is tested before the lanes part
+                    OCC_TALLY(c, kOccLeaf, pend >= 0);
+                    if (pend >= 0) { leaf(pend); pend = -1; }
+                }
+                if (ovf) walking = false;
+                if (walking) {
+                    wp->slot[0] = make_float4(__int_as_float(cur), __int_as_float(sp), __int_as_float(bg), __uint_as_float(br));
+                    wp->slot[1] = make_float4(bt, lim, 0.0f, 0.0f);
+                    wp->parked = true;
+                }
+                break;
+            }
+        }
     }
+    if (PK && wp->parked) return init_geom;
     if (ovf) ok = false;
     if (!ok) return init_geom;
     if (bg < 0) return init_geom;
@@ -2219,11 +2266,14 @@ __device__ float inw_ri_grid(const InwScene &S, f3 hp, float ratio, Ctr &c, bool
     return acc;
 }
 
-template <bool WANT_NORMAL, bool LN = false, bool FU = false>
+template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false>
 __device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
-                                             float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c) {
+                                             float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c,
+                                             WalkPark *wp = nullptr) {
     bool ok = false;
-    const float g = inw_traverse_wide<WANT_NORMAL, LN, FU>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c, ok);
+    const float g = inw_traverse_wide<WANT_NORMAL, LN, FU, PK>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom,
+                                                               c, ok, wp);
+    if (PK && wp->parked) return g;
     OCC_TALLY(c, kOccRef, !ok);
     if (ok) return g;
     return inw_traverse<WANT_NORMAL>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
@@ -2341,18 +2391,21 @@ __device__ f3 inw_tex_color(const InwScene &S, uint32_t k, f3 lp) {
 // One iteration of out_Pixel's ray loop (01_BVH...glsl:414-597 / 04...glsl:510-713):
 // pop a ray, closest hit, surrounding RI, shadow rays, push reflect/refract, accumulate.
 // bunit: the lane's pixel unit when its primary ray may use the pixel's beam list (k_inw_pm), else kBeamOff
-template <bool LIGHTS, bool LN = false, bool FU = false>
+// PK (walk parking, above): wp->resume continues a parked walk of this segment (its ray still
+// sits above K.size); wp->parked on return: the walk parked again and the segment is not done.
+template <bool LIGHTS, bool LN = false, bool FU = false, bool PK = false>
 __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s, f3 &color, float &depth, Ctr &c,
-                            uint32_t bunit = kBeamOff) {
+                            uint32_t bunit = kBeamOff, WalkPark *wp = nullptr) {
     const f3 D = mk(F.dir[0], F.dir[1], F.dir[2]);
     const float ratio = (float)s * F.inv_spp;
     const bool invert = dot(D, f3{1, 1, 1}) > 0.0f;
     do {
-        K.size -= 8;
+        const bool resumed = PK && wp->resume;
+        if (!resumed) K.size -= 8;
         const uint32_t b = K.size;
         f3 co = mk(K.at(b), K.at(b + 1), K.at(b + 2)), cd = mk(K.at(b + 3), K.at(b + 4), K.at(b + 5));
         float contribution = K.at(b + 6), bounced = (float)(int)K.at(b + 7);
-        c.seg++;
+        if (!resumed) c.seg++;
         // SET LIMIT (01_BVH...glsl:424-428): a MULTIFOCUS primary ray stops at the lens
         const bool mf0 = !LIGHTS && F.n_focus > 0 && (int)(bounced + 0.1f) == 0;
         const float tlim0 = mf0 ? K.at(4) : kMaxT;
@@ -2361,11 +2414,14 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         INW_T0(t_ch);
         float fg;
         bool beam_ok = false;
-        if (bunit != kBeamOff && (int)(bounced + 0.1f) == 0 && !mf0)  // a primary ray (pushed rays have bounced >= 1)
+        if (!resumed && bunit != kBeamOff && (int)(bounced + 0.1f) == 0 && !mf0)  // a primary ray (pushed rays have bounced >= 1)
             fg = inw_closest_beam<true>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c, bunit,
                                         beam_ok);
-        if (!beam_ok)
-            fg = inw_closest<true, LN, FU>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c);
+        if (!beam_ok) {
+            fg = inw_closest<true, LN, FU, PK>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c,
+                                               wp);
+            if (PK && wp->parked) return;  // the walk goes on in the next iteration
+        }
         INW_CYC(c, 0, t_ch);
         const f3 hitpoint = co + cd * tlim;
         if (!(tlim < tlim0)) {
@@ -2851,6 +2907,13 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     UnitPix px{};
     uint32_t bu = kBeamOff;  // the lane's pixel unit for its beam list (S.beam)
     uint32_t pu = 0xffffffffu;  // the unit px and pcd belong to: a lane's next sample is mostly the same pixel's
+#ifdef RT_INW_PARK
+    constexpr bool PK = true;
+#else
+    constexpr bool PK = false;
+#endif
+    bool parked = false;  // PK: this lane's walk is parked (its segment resumes next iteration)
+    float4 *pslot = S.park ? S.park + 2 * ((size_t)blockIdx.x * blockDim.x + threadIdx.x) : nullptr;
     f3 pcd = f3{0, 0, 0};
     f3 col = f3{0, 0, 0};
     float dep = 0.0f;
@@ -2974,11 +3037,13 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         INW_T0(t_seg);
         OCC_TALLY(c, kOccSeg, busy);
         if (busy) {
-            inw_segment<LIGHTS, LN, FU>(S, f, K, s, col, dep, c, bu);
-            if (f.px_rays) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
+            WalkPark wp{pslot, parked, false};
+            if (f.px_rays && !parked) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
+            inw_segment<LIGHTS, LN, FU, PK>(S, f, K, s, col, dep, c, bu, &wp);
+            parked = PK && wp.parked;
         }
         INW_CYC(c, 4, t_seg);
-        if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
+        if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
                                         __uint_as_float(ring_tag(S, g)));
             if ((uint32_t)s == mid) pdep[pj] = dep;  // 01_BVH...glsl:667-668, stored with the pixel's colour

@@ -84,6 +84,7 @@ struct InwScene {
     uint32_t n_lnodes = 0;  // the first n_lnodes wide nodes are staged in LDS (LN kernels only)
     int fused = 0;          // the wide walk culls with one fma per plane (cull4nf<true>; set per frame)
     uint32_t ring_epoch = 0;  // fold-ring tags: the frame's epoch (0..62) << 26 (ring_tag, rt_kernels.hip)
+    float4 *park = nullptr;   // RT_INW_PARK builds: 2 float4 of parked walk state per lane of the fold grid
     // Pixel beams (DESIGN.md §5 "Pixel beams"; null beam = off): for each pixel unit, the objects
     // whose culling box the beam of its primary rays can cross, sorted by the entry t of the
     // central ray into the box inflated by beam_R (k_inw_beam).  beam_n[u] = count (kBeamOff: use

@@ -5,14 +5,16 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/r04_ring; rm -rf $O; mkdir -p $O
 L=$GRAFT_REPO_ROOT/raytracing-tests_amd
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "repeated or inw01_random or update" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/gate.log 2>&1 || { echo GATE_FAILED; exit 1; }
-RT_HIP_LIB=$L/librt_hip_pend2.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "inw01_random or inw04" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/gate_pend2.log 2>&1 || { echo GATE_PEND2_FAILED; exit 1; }
+for v in pend2 park; do
+  RT_HIP_LIB=$L/librt_hip_$v.so timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bvh_exact.py -k "inw" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/gate_$v.log 2>&1 || { echo GATE_${v}_FAILED; exit 1; }
+done
 A="--steps 5 --warmup 1 --no-cpu-baseline"
 for pass in 1 2; do
-  for v in base r512 r256 pend2; do
+  for v in base r512 r256 pend2 park park16 park4m8; do
     X=""; LIB=$L/librt_hip.so
     [ $v = r512 ] && X="--opt inw_ring_pm=512"
     [ $v = r256 ] && X="--opt inw_ring_pm=256"
-    [ $v = pend2 ] && LIB=$L/librt_hip_pend2.so
+    case $v in pend2|park*) LIB=$L/librt_hip_$v.so;; esac
     RT_HIP_LIB=$LIB timeout -k 10 200 python3 bench.py $A $X > $O/b_${v}_p$pass.json 2> $O/b_${v}_p$pass.err || exit 1
   done
 done
