@@ -3036,19 +3036,34 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         // ---- one ray segment per busy lane (samples are independent invocations)
         INW_T0(t_seg);
         OCC_TALLY(c, kOccSeg, busy);
-        if (busy) {
-            WalkPark wp{pslot, parked, false};
-            if (f.px_rays && !parked) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
-            inw_segment<LIGHTS, LN, FU, PK>(S, f, K, s, col, dep, c, bu, &wp);
-            parked = PK && wp.parked;
+#ifdef RT_INW_TWO
+        // Two rounds per iteration (RT_INW_TWO experiment, DESIGN.md §5 "Primary and bounce
+        // rounds"): primary rays take the beam lists, bounce rays the wide walk, two code paths a
+        // wave runs one after the other; round 0 runs the lanes whose next ray is a primary one,
+        // round 1 every lane with a ray left (the bounce rays those primaries pushed included), so
+        // the walk runs with the bounce rays of the whole wave at once.
+#pragma unroll 1
+        for (int round = 0; round < 2; round++) {
+            const bool prim = bu != kBeamOff && !parked && K.size >= 8u && K.at(K.size - 1u) == 0.0f;
+            const bool go = busy && (round == 0 ? prim : (parked || K.size > 0u));
+#else
+        {
+            const bool go = busy;
+#endif
+            if (go) {
+                WalkPark wp{pslot, parked, false};
+                if (f.px_rays && !parked) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
+                inw_segment<LIGHTS, LN, FU, PK>(S, f, K, s, col, dep, c, bu, &wp);
+                parked = PK && wp.parked;
+            }
+            if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
+                wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
+                                            __uint_as_float(ring_tag(S, g)));
+                if ((uint32_t)s == mid) pdep[pj] = dep;  // 01_BVH...glsl:667-668, stored with the pixel's colour
+                busy = false;
+            }
         }
         INW_CYC(c, 4, t_seg);
-        if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
-            wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
-                                        __uint_as_float(ring_tag(S, g)));
-            if ((uint32_t)s == mid) pdep[pj] = dep;  // 01_BVH...glsl:667-668, stored with the pixel's colour
-            busy = false;
-        }
     }
 #ifdef RT_DIAG_SPLIT
     // phases 0-1 run inside `if (busy)`: the wave's time there is the largest of its lanes'
