@@ -3036,20 +3036,21 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         // ---- one ray segment per busy lane (samples are independent invocations)
         INW_T0(t_seg);
         OCC_TALLY(c, kOccSeg, busy);
-#ifdef RT_INW_TWO
-        // Two rounds per iteration (RT_INW_TWO experiment, DESIGN.md §5 "Primary and bounce
-        // rounds"): primary rays take the beam lists, bounce rays the wide walk, two code paths a
-        // wave runs one after the other; round 0 runs the lanes whose next ray is a primary one,
-        // round 1 every lane with a ray left (the bounce rays those primaries pushed included), so
-        // the walk runs with the bounce rays of the whole wave at once.
+        // Two rounds per iteration (DESIGN.md §5 "Primary and bounce rounds"): primary rays take
+        // the beam lists, bounce rays the wide walk, two code paths a wave runs one after the other
+        // (one walk trip then carries only the lanes with a bounce ray).  Round 0 runs the lanes
+        // whose next ray is a primary one; round 1 every lane with a ray left, the bounce rays those
+        // primaries just pushed included, so the walk runs with the bounce rays of the whole wave.
+        // INW-04 (LIGHTS) keeps one round: with its shadow walks the two-round loop spills 17 VGPRs
+#ifdef RT_INW_ONE  // A/B: one segment per lane and iteration (round 3)
+        constexpr int kRounds = 1;
+#else
+        constexpr int kRounds = LIGHTS ? 1 : 2;
+#endif
 #pragma unroll 1
-        for (int round = 0; round < 2; round++) {
+        for (int round = 2 - kRounds; round < 2; round++) {
             const bool prim = bu != kBeamOff && !parked && K.size >= 8u && K.at(K.size - 1u) == 0.0f;
             const bool go = busy && (round == 0 ? prim : (parked || K.size > 0u));
-#else
-        {
-            const bool go = busy;
-#endif
             if (go) {
                 WalkPark wp{pslot, parked, false};
                 if (f.px_rays && !parked) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
