@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* status codes */
 #define RT_OK            0
@@ -110,7 +110,9 @@ typedef struct rt_options {
     int inw_lds_nodes;      /* top of the wide BVH staged in LDS (768-lane blocks) */
     int inw_fused_cull;     /* one fma per culling plane where the error bound holds */
     int inw_claim_order;    /* pixel-major claims costliest 8x8 blocks first */
-    int inw_ring_pm;        /* fold window (entries per wave) of the pixel-major kernel, power of two >= 64 */
+    int inw_ring_pm;        /* pixel-major fold ring: 0 (default) in LDS, 256 entries per wave, beside
+                               5 staged nodes; else a global ring of that many entries per wave
+                               (power of two >= 64) beside 236 staged nodes */
     int inw_ring_sm;        /* ... of the sample-major kernel */
     /* IOW-03 (In-One-Weekend 03) */
     int iow_spec;           /* sample-parallel speculation (0: the sequential per-pixel kernel) */
@@ -296,9 +298,12 @@ typedef struct rt_path_info {
     int launches;
     int order;            /* INW: 1 pixel-major, 2 sample-major, 3 per-pixel k_inw; IOW-03: 4 sample-parallel, 5 sequential */
     int order_forced;     /* 1 when rt_options.inw_order chose it, 0 when the probe did */
-    int wide_walk, beams, ri_grid, fused_cull, lds_nodes, claim_order;
+    int wide_walk, beams, ri_grid, fused_cull;
+    int lds_nodes;        /* wide BVH nodes staged in LDS (0: none) */
+    int claim_order;
     int ring_entries;     /* fold window of the kernel that ran */
     int iow_bvh;          /* IOW-03: 0 linear loop, 1 culling BVH, 2 culling BVH in LDS */
+    int ring_lds;         /* 1: the fold ring was in LDS (k_inw_pm, inw_ring_pm = 0) */
 } rt_path_info;
 int rt_debug_path(rt_dev_scene *s, rt_path_info *out);
 

@@ -31,7 +31,7 @@ rt_options default_options() {
     std::memset(&o, 0, sizeof(o));
     o.size = sizeof(rt_options);
     o.inw_wide_walk = 1; o.inw_order = 0; o.inw_beams = 1; o.inw_ri_grid = 1; o.inw_lds_nodes = 1;
-    o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 1024; o.inw_ring_sm = 256;
+    o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 0; o.inw_ring_sm = 256;
     o.iow_spec = 1; o.iow_linear = 0; o.iow_narrow = 0; o.iow_lds_bvh = 1;
     o.iow_leaf_batch = 32;  // 32 measured 2.5% faster on the bench frame than 65 (round 2)
     o.iow_coop_max = 4; o.iow_chunks_lpt = 0;
@@ -44,7 +44,7 @@ rt_options default_options() {
 }
 bool options_ok(const rt_options *o) {
     auto pow2 = [](int r) { return r >= 64 && r <= (1 << 16) && (r & (r - 1)) == 0; };
-    return o && o->size == sizeof(rt_options) && o->inw_order >= -1 && o->inw_order <= 2 && pow2(o->inw_ring_pm) &&
+    return o && o->size == sizeof(rt_options) && o->inw_order >= -1 && o->inw_order <= 2 && (o->inw_ring_pm == 0 || pow2(o->inw_ring_pm)) &&
            pow2(o->inw_ring_sm) && o->iow_leaf_batch >= 1 && o->iow_leaf_batch <= 65 && o->iow_coop_max >= 0 &&
            o->rounds_seq >= 0 && o->rounds_seq <= 14 && o->rounds_spec >= 0 && o->rounds_spec <= 14 &&
            o->park_min >= -1 && o->spec_iters >= 0 && o->spec_probe >= 1 && o->spec_heavy >= -1 &&
@@ -174,6 +174,7 @@ struct rt_dev_scene {
     bool last_ln = false;         // the last INW fold launch used the LDS-staged kernels
     bool last_fu = false;         // ... their fused-fma cull instances
     uint32_t last_force = 0;      // ... its forced order (0: the probe's pick, read back from inw_mode)
+    bool last_lring = false;      // ... k_inw_pm's fold ring was in LDS
     uint32_t last_ring[2] = {0, 0};  // ... its fold windows (pixel-major, sample-major)
     uint32_t ring_frame = 0;         // frames rendered with the current fold rings (their tag epoch)
     rt_path_info last_path{};     // rt_debug_path: what the last render ran
@@ -1101,13 +1102,17 @@ int set_beam(rt_dev_scene *s, const rtk::Frame &f, rtk::InwScene &sc) {
 int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const rt_options &o = s->opt;
     const int blocks = s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 16 : 15);
-    const uint32_t ring_pm = uint32_t(o.inw_ring_pm), ring_sm = uint32_t(o.inw_ring_sm);
     // the top of the wide BVH staged in LDS (768-lane blocks, 3 waves per SIMD);
     // inw_lds_nodes = 0: 256-lane blocks reading every node from L1 / L2 (A/B)
     const int blocks_ln = o.inw_lds_nodes && s->dfs_high
                               ? s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 18 : 17) : 0;
+    // inw_ring_pm = 0: k_inw_pm's fold ring in LDS (768-lane blocks), else a global
+    // ring of that many entries per wave (1024 for the 256-lane blocks)
+    const bool lring = o.inw_ring_pm == 0 && blocks_ln > 0;
+    const uint32_t ring_pm = lring ? rtk::kPmLdsRing : uint32_t(o.inw_ring_pm ? o.inw_ring_pm : 1024);
+    const uint32_t ring_sm = uint32_t(o.inw_ring_sm);
     const size_t waves = std::max(size_t(blocks) * (rtk::kBlock / 64), size_t(blocks_ln) * (3 * rtk::kBlock / 64));
-    const size_t ring_bytes = waves * std::max(ring_pm, ring_sm) * sizeof(float4);
+    const size_t ring_bytes = waves * std::max(lring ? 0u : ring_pm, ring_sm) * sizeof(float4);
     if (s->inw_ring.bytes < ring_bytes) {
         s->inw_ring.~DevBuf();
         new (&s->inw_ring) DevBuf();
@@ -1122,6 +1127,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                      s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
     set_wide(s, sc);
     sc.ring_epoch = epoch << 26;
+    sc.lring = lring ? 1u : 0u;
 #ifdef RT_INW_PARK  // walk parking (experiment): 2 float4 per lane of the fold grid
     {
         const size_t need = waves * 64 * 2 * sizeof(float4);
@@ -1144,6 +1150,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const uint32_t force = (o.inw_order == 1 || o.inw_order == 2) ? uint32_t(o.inw_order) : 0u;
     s->last_force = force;
     s->last_ring[0] = ring_pm;
+    s->last_lring = lring;
     s->last_ring[1] = ring_sm;
     s->last_kernel = s->layout == 4 ? "k_inw_fold<true>" : "k_inw_fold<false>";
     s->last_ln = blocks_ln > 0;
@@ -1185,7 +1192,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         P.beams = sc.beam != nullptr;
         P.ri_grid = sc.ri_cells != nullptr;
         P.fused_cull = s->last_fu ? 1 : 0;
-        P.lds_nodes = s->last_ln ? 1 : 0;
+        P.lds_nodes = s->last_ln ? int(std::min<uint32_t>(s->n_wnodes, uint32_t(rtk::kInwLdsNodes))) : 0;
         P.claim_order = cost != nullptr;
     }
     if (epoch == 0) e = hipMemsetAsync(s->inw_ring.p, 0xff, s->inw_ring.bytes, st);
@@ -1370,7 +1377,12 @@ int rt_debug_path(rt_dev_scene *s, rt_path_info *out) {
     rt_path_info P = s->last_path;
     std::memcpy(P.kernel, name, sizeof(P.kernel));
     P.launches = n;
-    if (std::strncmp(name, "k_inw_pm", 8) == 0) { P.order = 1; P.ring_entries = int(s->last_ring[0]); }
+    if (std::strncmp(name, "k_inw_pm", 8) == 0) {
+        P.order = 1;
+        P.ring_entries = int(s->last_ring[0]);
+        P.ring_lds = s->last_lring ? 1 : 0;
+        if (s->last_lring) P.lds_nodes = std::min(P.lds_nodes, int(rtk::kPmLdsNodes));
+    }
     else if (std::strncmp(name, "k_inw_sm", 8) == 0) { P.order = 2; P.ring_entries = int(s->last_ring[1]); }
     if (P.order != 1) { P.beams = 0; P.claim_order = 0; }  // both serve the pixel-major kernel only
     *out = P;

@@ -1815,8 +1815,14 @@ __device__ float inw_surrounding_ri(const InwScene &S, FStack &K, f3 hp, float r
 constexpr int kInwNodeF4 = 10;
 // 236 nodes (36.9 KB): what the 3 x 256-lane stacks (120 KB) and k_inw_pm's depth slots (3 KB)
 // leave of 160 KB
-constexpr int kInwLdsNodes = 236;
+// (kInwLdsNodes = 236: rt_kernels.hpp)
 __shared__ float4 g_inw_lnodes[kInwLdsNodes * kInwNodeF4];
+// k_inw_pm with LN and InwScene::lring (rt_options.inw_ring_pm = 0, the default): the first
+// kPmLdsNodes nodes, then the 12 waves' fold rings of kPmLdsRing entries (r, g, b planes) in the
+// same LDS (a 256-entry window costs 0.5% against 1024, 128 entries 7%; the ring
+// takes the LDS of all but the top 5 nodes, which were worth 1.5%, and saves 1% of global ring
+// traffic -- 0.57 against 42 GB of L2-to-fabric traffic per C3 frame)
+static_assert(kPmLdsNodes * kInwNodeF4 * 16 + 12 * 3 * kPmLdsRing * 4 <= kInwLdsNodes * kInwNodeF4 * 16, "LDS ring");
 template <bool LN>
 __device__ __forceinline__ const float4 *inw_node_ptr(const InwScene &S, int cur) {
     if (LN && (uint32_t)(cur - 1) < S.n_lnodes) return g_inw_lnodes + kInwNodeF4 * (cur - 1);
@@ -2638,10 +2644,13 @@ __global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S, Chunk ch, C
 // stores the mean.  The INW kernels below keep that sum on chip.  A wave claims work from the
 // global queue, hands its samples to its lanes as a stream g = 0, 1, 2, ... in a fixed order, and
 // a lane that finishes a sample takes the next stream entry at once (lane persistence).  A
-// finished sample stores {sqrt(colour), tag g} into the wave's private ring (a few KB per wave,
-// L2-resident); the wave folds the ring in each pixel's sample order, End()'s float order, and
-// writes a pixel when its last sample is folded.  The middle sample's depth is written by the
-// lane that finishes it.  Entries beyond the oldest unfolded one + ring size are not issued (a
+// finished sample stores its sqrt(colour) into the wave's private ring; the wave folds the ring in
+// each pixel's sample order, End()'s float order, and writes a pixel when its last sample is
+// folded.  The ring: k_inw_pm's 768-lane instances keep it in LDS (InwScene::lring, the default:
+// 256 entries per wave as r, g, b planes; an entry is finished when no busy lane holds it); the
+// other kernels keep a global ring of {sqrt(colour), tag g} per wave (16 KB per wave at 1024
+// entries, not L2-resident at the chip's 3,000-odd waves: it reaches the fabric).
+// The middle sample's depth goes with the pixel's colour.  Entries beyond the oldest unfolded one + ring size are not issued (a
 // straggling sample holds the window; the other lanes keep running until it fills).  Counters
 // accumulate per lane.  Two stream orders, one per kind of ray coherence:
 //  - k_inw_pm (pixel-major): the wave claims pixels and runs all samples of one pixel back to
@@ -2875,8 +2884,11 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     // between the fold and the issue), written out with the pixel's colour
     __shared__ float s_pdep[SUB * kBlock];
     InwScene S = S0;
+    // the fold ring in LDS, after the first kPmLdsNodes staged nodes (InwScene::lring)
+    const bool LR = LN && S.lring;
     if constexpr (LN) {
-        const uint32_t n = S.wnodes ? (S.n_wnodes < (uint32_t)kInwLdsNodes ? S.n_wnodes : (uint32_t)kInwLdsNodes) : 0u;
+        const uint32_t cap = LR ? (uint32_t)kPmLdsNodes : (uint32_t)kInwLdsNodes;
+        const uint32_t n = S.wnodes ? (S.n_wnodes < cap ? S.n_wnodes : cap) : 0u;
         for (uint32_t i = threadIdx.x; i < n * (uint32_t)kInwNodeF4; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
         __syncthreads();
         S.n_lnodes = n;
@@ -2888,8 +2900,11 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
 #endif
     FStack K{lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock), 0};
     const uint32_t lane = threadIdx.x & 63u;
+    if (LR) rmask = kPmLdsRing - 1u;
     const uint32_t rsize = rmask + 1u;
     float4 *wr = ring + (size_t)uni((blockIdx.x * (SUB * kBlock) + threadIdx.x) >> 6) * rsize;
+    // LR: this wave's ring, three planes (r, g, b) of kPmLdsRing floats
+    float *lr = reinterpret_cast<float *>(g_inw_lnodes + kPmLdsNodes * kInwNodeF4) + uni((threadIdx.x >> 6) * (3u * kPmLdsRing));
     float *pdep = s_pdep + (threadIdx.x & ~63u);
     const uint32_t spp = (uint32_t)f.spp, mid = spp / 2u, total = units_total(f);
     const float inv = rcp((float)f.spp);
@@ -2922,16 +2937,30 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         // ---- fold the finished entries gf, gf+1, ... (stored in earlier iterations)
         INW_T0(t_fold);
         if (gf != gi) {
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's ring stores have landed (same CU: L1 write-through)
             const uint32_t k = gf + lane;
-            bool fin = false;
             float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (k - gf < gi - gf) {
-                v = wr[k & rmask];
-                fin = __float_as_uint(v.w) == ring_tag(S, k);
+            uint32_t n;
+            if (LR) {
+                // Every issued entry is either held by a busy lane or stored, so the entries below
+                // the smallest one a busy lane holds are finished: no tags.  LDS ops of one wave
+                // complete in order, so the stores of earlier iterations are visible.
+                n = uni(__ockl_wfred_min_u32(busy ? g - gf : 0xffffffffu));  // DPP reduction
+                if (n > gi - gf) n = gi - gf;
+                if (n > 64u) n = 64u;
+                if (lane < n) {
+                    const uint32_t e = k & rmask;
+                    v = make_float4(lr[e], lr[kPmLdsRing + e], lr[2u * kPmLdsRing + e], 0.0f);
+                }
+            } else {
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's ring stores have landed (same CU: L1 write-through)
+                bool fin = false;
+                if (k - gf < gi - gf) {
+                    v = wr[k & rmask];
+                    fin = __float_as_uint(v.w) == ring_tag(S, k);
+                }
+                const unsigned long long m = __ballot(fin);
+                n = ~m == 0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
             }
-            const unsigned long long m = __ballot(fin);
-            const uint32_t n = ~m == 0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
             // the run splits at pixel ends: per pixel, its entries are added with no test between them
             for (uint32_t i = 0; i < n;) {
                 const uint32_t e = i + (n - i < spp - sf ? n - i : spp - sf);
@@ -3022,7 +3051,12 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                         inw_start_sample_cd(S, f, K, pcd, s, c);
                     } else {  // a padding slot: an empty sample, folded as zero
                         if ((uint32_t)s == mid) pdep[pj] = 0.0f;
-                        wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(ring_tag(S, g)));
+                        if (LR) {
+                            const uint32_t e = g & rmask;
+                            lr[e] = 0.0f; lr[kPmLdsRing + e] = 0.0f; lr[2u * kPmLdsRing + e] = 0.0f;
+                        } else {
+                            wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(ring_tag(S, g)));
+                        }
                     }
                 }
                 gi += take;
@@ -3058,8 +3092,15 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 parked = PK && wp.parked;
             }
             if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
-                wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
-                                            __uint_as_float(ring_tag(S, g)));
+                if (LR) {
+                    const uint32_t e = g & rmask;
+                    lr[e] = __builtin_sqrtf(col.x);
+                    lr[kPmLdsRing + e] = __builtin_sqrtf(col.y);
+                    lr[2u * kPmLdsRing + e] = __builtin_sqrtf(col.z);
+                } else {
+                    wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
+                                                __uint_as_float(ring_tag(S, g)));
+                }
                 if ((uint32_t)s == mid) pdep[pj] = dep;  // 01_BVH...glsl:667-668, stored with the pixel's colour
                 busy = false;
             }

@@ -83,6 +83,7 @@ struct InwScene {
     uint32_t n_wnodes = 0;  // wide nodes
     uint32_t n_lnodes = 0;  // the first n_lnodes wide nodes are staged in LDS (LN kernels only)
     int fused = 0;          // the wide walk culls with one fma per plane (cull4nf<true>; set per frame)
+    uint32_t lring = 0;       // k_inw_pm (768-lane instances): the fold ring in LDS (kPmLdsRing entries per wave)
     uint32_t ring_epoch = 0;  // fold-ring tags: the frame's epoch (0..62) << 26 (ring_tag, rt_kernels.hip)
     float4 *park = nullptr;   // RT_INW_PARK builds: 2 float4 of parked walk state per lane of the fold grid
     // Pixel beams (DESIGN.md §5 "Pixel beams"; null beam = off): for each pixel unit, the objects
@@ -185,6 +186,9 @@ enum { kSpecFirst = 0, kSpecRest = 1, kSpecList = 2 };
 // lanes from `in` in full waves.  in == null: the launch's units are pixels.  out == null or
 // fewer than park_min units in the launch: lanes run to completion (the final round).
 constexpr int kBlock = 256;      // threads per block of every render kernel
+constexpr int kInwLdsNodes = 236;        // wide BVH nodes the INW fold kernels stage in LDS (rt_kernels.hip)
+constexpr uint32_t kPmLdsRing = 256;     // k_inw_pm's LDS fold ring: entries per wave (InwScene::lring) ...
+constexpr uint32_t kPmLdsNodes = 5;      // ... and the nodes it leaves staged
 constexpr int kParkBelow = 32;    // park when fewer than half the wave's lanes are busy
 constexpr int kContSlots = 13;    // float4 per parked lane
 struct Cont {

@@ -23,7 +23,7 @@ RT_STAGE_IOW02 = 2
 RT_IOW_CUBOID, RT_IOW_ELLIPSOID = 1, 2
 RT_INW_ELLIPSOID, RT_INW_CUBOID = 1, 2
 
-ABI_VERSION = 2  # RT_ABI_VERSION, include/rt_hip.h
+ABI_VERSION = 3  # RT_ABI_VERSION, include/rt_hip.h
 
 PRESET_IOW03_REF3 = 1
 PRESET_IOW03_FINAL = 2
@@ -89,7 +89,8 @@ class RtPathInfo(C.Structure):
     """rt_path_info (include/rt_hip.h): what a scene's last render ran."""
     _fields_ = [("kernel", C.c_char * 64), ("launches", C.c_int), ("order", C.c_int), ("order_forced", C.c_int),
                 ("wide_walk", C.c_int), ("beams", C.c_int), ("ri_grid", C.c_int), ("fused_cull", C.c_int),
-                ("lds_nodes", C.c_int), ("claim_order", C.c_int), ("ring_entries", C.c_int), ("iow_bvh", C.c_int)]
+                ("lds_nodes", C.c_int), ("claim_order", C.c_int), ("ring_entries", C.c_int), ("iow_bvh", C.c_int),
+                ("ring_lds", C.c_int)]
 
     ORDERS = {0: None, 1: "pixel-major", 2: "sample-major", 3: "per-pixel", 4: "sample-parallel", 5: "sequential"}
 

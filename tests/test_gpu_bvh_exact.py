@@ -143,6 +143,8 @@ def _same_frames(over, w, h, spp, scene):
     ({"inw_order": 1}, INW1, 97, 43, 3),          # ragged 8x8 units (padding samples)
     ({"inw_order": 2}, INW1, 97, 43, 3),
     ({"inw_order": 1, "inw_ring_pm": 64}, INW1, 128, 72, 300),  # a window smaller than a pixel
+    ({"inw_order": 1, "inw_ring_pm": 1024}, INW1, 128, 72, 300),  # the global ring (default: LDS)
+    ({"inw_order": 1, "inw_ring_pm": 1024}, INW4, 128, 128, 16),
     ({"inw_order": 2, "inw_ring_sm": 64}, INW1, 128, 72, 20),   # a window of one sample row
     ({"inw_order": -1}, INW4, 128, 128, 16),
     ({"inw_order": 1}, INW4, 128, 128, 16),

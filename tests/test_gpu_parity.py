@@ -130,7 +130,7 @@ def test_unsupported_texture_index_fails_loudly(gpu):
 def test_repeated_frames_on_one_device_scene(gpu):
     """A device scene renders frame after frame with its fold rings kept (their tags carry a
     frame epoch; they are cleared only when it wraps every 63 frames): 70 frames, alternating the
-    fold windows and the fold order between them, all bit-identical to the first, colour and depth,
+    fold windows (global rings, k_inw_pm's LDS ring) and the fold order between them, all bit-identical to the first, colour and depth,
     with the same ray counts."""
     import ctypes as C
 
@@ -145,7 +145,8 @@ def test_repeated_frames_on_one_device_scene(gpu):
     try:
         for i in range(70):
             o = R.default_options()
-            o.inw_ring_pm, o.inw_ring_sm = (1024, 256) if i % 3 else (64, 128)
+            # pixel-major ring: global (64, 1024 entries) or in LDS (0); sample-major windows
+            o.inw_ring_pm, o.inw_ring_sm = ((64, 128), (0, 256), (1024, 256), (0, 64))[i % 4]
             o.inw_order = (0, 1, 2)[i % 3]
             assert lib.rt_dev_scene_set_options(s, C.byref(o)) == 0
             img = torch.zeros((40, 64, 4), dtype=torch.float32, device=dev)
@@ -215,3 +216,44 @@ def test_scene_update_matches_fresh_scene(gpu, device_lbvh):
     for x, y in ((g, h), (gd, hd), (g, o), (gd, od)):
         assert compare(x, y)["exact_frac"] == 1.0
     assert gs == hs == ost["segments"]
+
+
+def test_debug_path_reports_the_fold_ring(gpu):
+    """rt_debug_path names the kernel and where its fold ring lived: k_inw_pm's ring in LDS by
+    default (256 entries per wave, 5 staged nodes), a global ring with inw_ring_pm > 0 (236 staged
+    nodes); the sample-major kernel keeps its global ring."""
+    import ctypes as C
+
+    import torch
+
+    sc = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 3000, width=64, height=40, spp=8)
+    lib = R.load()
+    dev = torch.device("cuda")
+    s = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, 1, R.fptr(sc.nodes), None, 0, sc.params.spp, -1)
+    assert s
+    paths = {}
+    try:
+        for name, over in (("lds", {"inw_order": 1}), ("global", {"inw_order": 1, "inw_ring_pm": 1024}),
+                           ("sm", {"inw_order": 2})):
+            o = R.default_options()
+            for k, v in over.items():
+                setattr(o, k, v)
+            assert lib.rt_dev_scene_set_options(s, C.byref(o)) == 0
+            img = torch.zeros((40, 64, 4), dtype=torch.float32, device=dev)
+            ctr = torch.zeros(6, dtype=torch.int64, device=dev)
+            rc = lib.rt_render_image_async(s, C.byref(sc.camera), C.byref(sc.params), img.data_ptr(), None,
+                                           ctr.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            assert rc == 0
+            torch.cuda.synchronize()
+            paths[name] = R.debug_path(s)
+    finally:
+        lib.rt_dev_scene_free(s)
+    print(paths)
+    p = paths["lds"]
+    assert p["kernel"].startswith("k_inw_pm") and p["ring_lds"] == 1 and p["ring_entries"] == 256
+    assert p["lds_nodes"] == 5
+    p = paths["global"]
+    assert p["kernel"].startswith("k_inw_pm") and p["ring_lds"] == 0 and p["ring_entries"] == 1024
+    assert p["lds_nodes"] > 5
+    p = paths["sm"]
+    assert p["kernel"].startswith("k_inw_sm") and p["ring_lds"] == 0 and p["lds_nodes"] > 5
