@@ -175,6 +175,7 @@ struct rt_dev_scene {
     bool last_fu = false;         // ... their fused-fma cull instances
     uint32_t last_force = 0;      // ... its forced order (0: the probe's pick, read back from inw_mode)
     bool last_lring = false;      // ... k_inw_pm's fold ring was in LDS
+    char kname[64] = {0};         // the fold kernel's instance name (rt_debug_launches)
     uint32_t last_ring[2] = {0, 0};  // ... its fold windows (pixel-major, sample-major)
     uint32_t ring_frame = 0;         // frames rendered with the current fold rings (their tag epoch)
     rt_path_info last_path{};     // rt_debug_path: what the last render ran
@@ -1492,16 +1493,16 @@ int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {
         HIP_OK(hipMemcpy(m, s->inw_mode.p, sizeof(m), hipMemcpyDeviceToHost));
         const uint32_t ord = s->last_force;  // the order the launch used (0: the probe's verdict)
         const bool sm = ord == 2 || (ord != 1 && m[0] > 0 && 2 * m[1] >= m[0]);
-        // the template instance's name as rocprofv3 prints it, every argument: every template argument: <LIGHTS, LN (LDS-staged BVH top), FU (fused cull)>
-        static const char *names[2][2][2] = {
-            {{"k_inw_pm<false, false, false>", "k_inw_pm<true, false, false>"},
-             {"k_inw_sm<false, false, false>", "k_inw_sm<true, false, false>"}},
-            {{"k_inw_pm<false, true, false>", "k_inw_pm<true, true, false>"},
-             {"k_inw_sm<false, true, false>", "k_inw_sm<true, true, false>"}}};
-        static const char *names_fu[2][2] = {{"k_inw_pm<false, true, true>", "k_inw_pm<true, true, true>"},
-                                             {"k_inw_sm<false, true, true>", "k_inw_sm<true, true, true>"}};
-        s->last_kernel = s->last_fu ? names_fu[sm ? 1 : 0][s->layout == 4 ? 1 : 0]
-                                    : names[s->last_ln ? 1 : 0][sm ? 1 : 0][s->layout == 4 ? 1 : 0];
+        // the template instance's name as rocprofv3 prints it, every template argument:
+        // <LIGHTS, LN (LDS-staged BVH top), FU (fused cull)[, LRING (k_inw_pm: the fold ring in LDS)]>
+        auto tf = [](bool b) { return b ? "true" : "false"; };
+        const bool fu = s->last_fu, ln = s->last_ln, lights = s->layout == 4;
+        if (sm)
+            std::snprintf(s->kname, sizeof(s->kname), "k_inw_sm<%s, %s, %s>", tf(lights), tf(ln), tf(fu));
+        else
+            std::snprintf(s->kname, sizeof(s->kname), "k_inw_pm<%s, %s, %s, %s>", tf(lights), tf(ln), tf(fu),
+                          tf(s->last_lring));
+        s->last_kernel = s->kname;
     }
     if (name_out && name_cap > 0) {
         std::strncpy(name_out, s->last_kernel, size_t(name_cap) - 1);

@@ -50,8 +50,10 @@ __device__ __forceinline__ Pix map_pixel(const Frame &f) {
 
 // occupancy slots (RT_DIAG_OCC): pairs (wave iterations, lanes) of: the fold loop's iterations with
 // busy lanes; wide-walk trips with walking lanes; their node steps; leaf batches; beam-list trips;
-// reference-walk entries (lanes that fell back); surrounding-RI queries
-enum { kOccSeg = 0, kOccWalk = 2, kOccNode = 4, kOccLeaf = 6, kOccBeam = 8, kOccRef = 10, kOccRi = 12, kOccSlots = 14 };
+// reference-walk entries (lanes that fell back); surrounding-RI queries; node steps with the
+// lanes on the first stepping lane's node; node steps where every stepping lane is on one node
+enum { kOccSeg = 0, kOccWalk = 2, kOccNode = 4, kOccLeaf = 6, kOccBeam = 8, kOccRef = 10, kOccRi = 12, kOccSame = 14,
+       kOccUni = 16, kOccSlots = 18 };
 struct Ctr {
     uint32_t seg = 0, nodes = 0, prims = 0, shadow = 0, drops = 0, nans = 0;
     unsigned long long *wdbg = nullptr;  // diagnostics: this wave's kDbg* row in LDS, or null
@@ -1992,6 +1994,17 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
     for (;;) {
         OCC_TALLY(c, kOccWalk, walking);
         OCC_TALLY(c, kOccNode, walking && cur > 0);
+#ifdef RT_DIAG_OCC
+        {  // how often a node step's lanes share one node (a wave-uniform node load would serve them)
+            const unsigned long long m = __ballot(walking && cur > 0);
+            if (m) {
+                const int c0 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(m));
+                const bool on = walking && cur == c0;
+                OCC_TALLY(c, kOccSame, on);
+                if (__ballot(walking && cur > 0 && cur != c0) == 0ull) OCC_TALLY(c, kOccUni, on);
+            }
+        }
+#endif
         if (walking) {
             bool pop;
             if (cur > 0) {
@@ -2875,7 +2888,7 @@ __global__ __launch_bounds__(kBlock) void k_inw_order_scatter(const uint32_t *ke
 // pixel-major stream (see above): entry g = (claimed pixel ordinal j, sample s).  LN: 768-lane
 // blocks (3 waves per SIMD) that stage the top of the wide BVH in the LDS their three 256-lane
 // stacks leave free (kInwLdsNodes nodes)
-template <bool LIGHTS, bool LN = false, bool FU = false>
+template <bool LIGHTS, bool LN = false, bool FU = false, bool LRING = false>
 __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_waves_per_eu(LN ? 3 : (LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES)))) void k_inw_pm(Frame f, InwScene S0, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force, const uint32_t *border) {
     if (inw_sample_major(mode, force)) return;  // the probe picked k_inw_sm for this frame
     constexpr int SUB = LN ? 3 : 1;
@@ -2884,8 +2897,9 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     // between the fold and the issue), written out with the pixel's colour
     __shared__ float s_pdep[SUB * kBlock];
     InwScene S = S0;
-    // the fold ring in LDS, after the first kPmLdsNodes staged nodes (InwScene::lring)
-    const bool LR = LN && S.lring;
+    // LRING: the fold ring in LDS, after the first kPmLdsNodes staged nodes (InwScene::lring; an
+    // instance of its own: as a per-frame branch it cost 1% of C3 in either mode)
+    constexpr bool LR = LN && LRING;
     if constexpr (LN) {
         const uint32_t cap = LR ? (uint32_t)kPmLdsNodes : (uint32_t)kInwLdsNodes;
         const uint32_t n = S.wnodes ? (S.n_wnodes < cap ? S.n_wnodes : cap) : 0u;
@@ -2900,7 +2914,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
 #endif
     FStack K{lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock), 0};
     const uint32_t lane = threadIdx.x & 63u;
-    if (LR) rmask = kPmLdsRing - 1u;
+    if constexpr (LR) rmask = kPmLdsRing - 1u;
     const uint32_t rsize = rmask + 1u;
     float4 *wr = ring + (size_t)uni((blockIdx.x * (SUB * kBlock) + threadIdx.x) >> 6) * rsize;
     // LR: this wave's ring, three planes (r, g, b) of kPmLdsRing floats
@@ -2940,7 +2954,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             const uint32_t k = gf + lane;
             float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             uint32_t n;
-            if (LR) {
+            if constexpr (LR) {
                 // Every issued entry is either held by a busy lane or stored, so the entries below
                 // the smallest one a busy lane holds are finished: no tags.  LDS ops of one wave
                 // complete in order, so the stores of earlier iterations are visible.
@@ -3051,7 +3065,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                         inw_start_sample_cd(S, f, K, pcd, s, c);
                     } else {  // a padding slot: an empty sample, folded as zero
                         if ((uint32_t)s == mid) pdep[pj] = 0.0f;
-                        if (LR) {
+                        if constexpr (LR) {
                             const uint32_t e = g & rmask;
                             lr[e] = 0.0f; lr[kPmLdsRing + e] = 0.0f; lr[2u * kPmLdsRing + e] = 0.0f;
                         } else {
@@ -3092,7 +3106,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 parked = PK && wp.parked;
             }
             if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
-                if (LR) {
+                if constexpr (LR) {
                     const uint32_t e = g & rmask;
                     lr[e] = __builtin_sqrtf(col.x);
                     lr[kPmLdsRing + e] = __builtin_sqrtf(col.y);
@@ -3587,7 +3601,8 @@ hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uin
             const dim3 g(blocks_ln), b(3 * kBlock);
 #define RT_INW_LN_LAUNCH(L, F)                                                                              \
     do {                                                                                                    \
-        if (k == 0) hipLaunchKernelGGL((k_inw_pm<L, true, F>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border); \
+        if (k == 0 && sc.lring) hipLaunchKernelGGL((k_inw_pm<L, true, F, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border); \
+        else if (k == 0) hipLaunchKernelGGL((k_inw_pm<L, true, F>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border); \
         else hipLaunchKernelGGL((k_inw_sm<L, true, F>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border);        \
     } while (0)
             if (sc.layout == 4) {

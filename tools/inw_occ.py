@@ -43,8 +43,9 @@ lib.rt_debug_counters(dbg.data_ptr())
 lib.rt_render_image_async(scene, C.byref(sc.camera), C.byref(p), rgba.data_ptr(), depth.data_ptr(), ctr.data_ptr(), st)
 torch.cuda.synchronize()
 lib.rt_debug_counters(None)
-d = [int(v) for v in dbg.cpu().tolist()][32:46]
-names = ("segment_iterations", "walk_trips", "node_steps", "leaf_batches", "beam_trips", "reference_walks", "ri_queries")
+d = [int(v) for v in dbg.cpu().tolist()][32:50]
+names = ("segment_iterations", "walk_trips", "node_steps", "leaf_batches", "beam_trips", "reference_walks", "ri_queries",
+         "node_steps_same_node_as_first", "node_steps_all_one_node")
 out = {"config": cfg, "spp": p.spp, "path": R.debug_path(scene), "segments": int(ctr[0].item()),
        "node_visits": int(ctr[1].item()), "prim_tests": int(ctr[2].item())}
 tot = sum(d[2 * i] for i in (1, 3, 4))
