@@ -2929,6 +2929,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     bool qdone = false;
     f3 acc = f3{0, 0, 0};              // running End() sum of pixel jf (the same in every lane)
     uint32_t pix_slot = 0xffffffffu;   // lane l: the unit of the claimed ordinal j with j % 64 == l
+    f3 pc = f3{0, 0, 0};               // lane l: that pixel's mean, kept until its claim row is stored
     // per lane: the sample it traces
     bool busy = false;
     uint32_t g = 0, pj = 0;  // the lane's stream entry and its pixel's ordinal slot (j % 64)
@@ -2990,14 +2991,17 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 sf += e - i;
                 i = e;
                 if (sf == spp) {  // pixel jf complete: End()'s imageStores (01_BVH...glsl:652, 667-668)
-                    const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
-                    if (lane == 0) {
-                        const UnitPix p = unit_pixel(f, unit);
+                    // the lane of its ordinal slot keeps the mean; once the 8 ordinals of a claim
+                    // row are done (claims come in rows of 8: 8 adjacent pixels of one 8x8 block),
+                    // their 8 lanes store colour and depth together (128 + 32 contiguous bytes)
+                    if (lane == (jf & 63u)) pc = acc * inv;
+                    if ((jf & 7u) == 7u && lane - ((jf & 63u) & ~7u) < 8u) {
+                        const UnitPix p = unit_pixel(f, pix_slot);
                         if (p.out != (size_t)-1) {
                             reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
-                                make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
-                                            p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
-                            if (f.out_depth) f.out_depth[p.out] = pdep[jf & 63u];
+                                make_float4(p.in_image ? pc.x : 0.0f, p.in_image ? pc.y : 0.0f,
+                                            p.in_image ? pc.z : 0.0f, p.in_image ? 1.0f : 0.0f);
+                            if (f.out_depth) f.out_depth[p.out] = pdep[lane];
                         }
                     }
                     sf = 0;
@@ -3012,11 +3016,13 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         const unsigned long long fm = __ballot(!busy);
         const uint32_t nfree = (uint32_t)__popcll(fm);
         if (!qdone && nfree) {
-            // ordinals the free lanes would reach: ji + (si + nfree - 1) / spp, capped at jf + 63
+            // ordinals the free lanes would reach: ji + (si + nfree - 1) / spp, claimed in rows of
+            // 8 and at most 64 ahead of the fold's row (a slot's colour and depth wait for its row)
+            const uint32_t lim = (jf & ~7u) + 64u;
             uint32_t need = ji + (si + nfree - 1u) / spp + 1u;
-            if (need > jf + 64u) need = jf + 64u;
+            if (need > lim) need = lim;
             if (need > nclaimed) {
-                const uint32_t want = need - nclaimed;
+                const uint32_t want = (need - nclaimed + 7u) & ~7u;  // nclaimed and lim are multiples of 8
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(counter, want);
                 base = uni((uint32_t)__shfl((int)base, 0, 64));
