@@ -3280,6 +3280,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             }
         }
         if (qdone && bi == nclaimed && bmin == nclaimed && __ballot(busy) == 0) break;
+        OCC_TALLY(c, kOccSeg, busy);
         if (busy) {
             inw_segment<LIGHTS, LN, FU>(S, f, K, s, col, dep, c);
             if (f.px_rays) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
@@ -3291,6 +3292,10 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             busy = false;
         }
     }
+#ifdef RT_DIAG_OCC
+    if (f.dbg && lane == 0)
+        for (int k = 0; k < kOccSlots; k++) atomicAdd(f.dbg + 32 + k, c.occ[k]);
+#endif
     flush(f, c);
 }
 

@@ -20,3 +20,5 @@ for d in sorted(glob.glob(sys.argv[1] + "/pmc_w*")):
                 agg[r["Counter_Name"]] += float(r["Counter_Value"])
     print(os.path.basename(d), {k: round(v * 1024 / 2 / 1e9, 4) for k, v in agg.items()}, "GB per frame")
 PY
+RT_HIP_LIB=$GRAFT_REPO_ROOT/raytracing-tests_amd/librt_hip_occ.so timeout -k 10 200 python3 tools/inw_occ.py c5 64 > $O/occ_c5.json 2> $O/occ_c5.err || exit 1
+RT_HIP_LIB=$GRAFT_REPO_ROOT/raytracing-tests_amd/librt_hip_occ.so timeout -k 10 200 python3 tools/inw_occ.py c3 > $O/occ_c3.json 2> $O/occ_c3.err || exit 1
