@@ -1824,7 +1824,13 @@ __shared__ float4 g_inw_lnodes[kInwLdsNodes * kInwNodeF4];
 // same LDS (a 256-entry window costs 0.5% against 1024, 128 entries 7%; the ring
 // takes the LDS of all but the top 5 nodes, which were worth 1.5%, and saves 1% of global ring
 // traffic -- 0.57 against 42 GB of L2-to-fabric traffic per C3 frame)
-static_assert(kPmLdsNodes * kInwNodeF4 * 16 + 12 * 3 * kPmLdsRing * 4 <= kInwLdsNodes * kInwNodeF4 * 16, "LDS ring");
+#ifdef RT_INW_HYB
+constexpr uint32_t kPmFlagBytes = 12 * kPmLdsRing / 8;  // one valid bit per LDS slot and wave
+#else
+constexpr uint32_t kPmFlagBytes = 0;
+#endif
+static_assert(kPmLdsNodes * kInwNodeF4 * 16 + 12 * 3 * kPmLdsRing * 4 + kPmFlagBytes <= kInwLdsNodes * kInwNodeF4 * 16,
+              "LDS ring");
 template <bool LN>
 __device__ __forceinline__ const float4 *inw_node_ptr(const InwScene &S, int cur) {
     if (LN && (uint32_t)(cur - 1) < S.n_lnodes) return g_inw_lnodes + kInwNodeF4 * (cur - 1);
@@ -2914,7 +2920,22 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
 #endif
     FStack K{lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock), 0};
     const uint32_t lane = threadIdx.x & 63u;
+#ifdef RT_INW_HYB
+    // HYB (experiment): the LDS ring takes the entries stored less than kPmLdsRing after the
+    // fold's position; later ones go to a global ring of kPmHybGlobal entries, the issue window.
+    // A valid bit per LDS slot (set by the store, cleared by the fold) tells the fold where an
+    // entry is: a slot's valid entry is always the one being folded (a later entry of the slot
+    // goes to LDS only once this one is folded).
+    constexpr bool HYB = LR;
+    if constexpr (LR) rmask = kPmHybGlobal - 1u;
+    uint32_t *lfl = reinterpret_cast<uint32_t *>(reinterpret_cast<float *>(g_inw_lnodes + kPmLdsNodes * kInwNodeF4) +
+                                                 12u * 3u * kPmLdsRing) + uni((threadIdx.x >> 6) * (kPmLdsRing / 32u));
+    if constexpr (LR)
+        if ((threadIdx.x & 63u) < kPmLdsRing / 32u) lfl[threadIdx.x & 63u] = 0u;
+#else
+    constexpr bool HYB = false;
     if constexpr (LR) rmask = kPmLdsRing - 1u;
+#endif
     const uint32_t rsize = rmask + 1u;
     float4 *wr = ring + (size_t)uni((blockIdx.x * (SUB * kBlock) + threadIdx.x) >> 6) * rsize;
     // LR: this wave's ring, three planes (r, g, b) of kPmLdsRing floats
@@ -2962,7 +2983,22 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 n = uni(__ockl_wfred_min_u32(busy ? g - gf : 0xffffffffu));  // DPP reduction
                 if (n > gi - gf) n = gi - gf;
                 if (n > 64u) n = 64u;
-                if (lane < n) {
+                if constexpr (HYB) {
+#ifdef RT_INW_HYB
+                    const uint32_t e = k & (kPmLdsRing - 1u);
+                    bool valid = false;
+                    if (lane < n) {
+                        valid = (lfl[e >> 5] >> (e & 31u)) & 1u;
+                        if (valid) v = make_float4(lr[e], lr[kPmLdsRing + e], lr[2u * kPmLdsRing + e], 0.0f);
+                    }
+                    const bool glob = lane < n && !valid;
+                    if (__ballot(glob)) {
+                        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's global stores have landed
+                        if (glob) v = wr[k & rmask];
+                    }
+                    if (valid) atomicAnd(&lfl[e >> 5], ~(1u << (e & 31u)));
+#endif
+                } else if (lane < n) {
                     const uint32_t e = k & rmask;
                     v = make_float4(lr[e], lr[kPmLdsRing + e], lr[2u * kPmLdsRing + e], 0.0f);
                 }
@@ -3071,7 +3107,17 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                         inw_start_sample_cd(S, f, K, pcd, s, c);
                     } else {  // a padding slot: an empty sample, folded as zero
                         if ((uint32_t)s == mid) pdep[pj] = 0.0f;
-                        if constexpr (LR) {
+                        if constexpr (HYB) {
+#ifdef RT_INW_HYB
+                            if (g - gf < kPmLdsRing) {
+                                const uint32_t e = g & (kPmLdsRing - 1u);
+                                lr[e] = 0.0f; lr[kPmLdsRing + e] = 0.0f; lr[2u * kPmLdsRing + e] = 0.0f;
+                                atomicOr(&lfl[e >> 5], 1u << (e & 31u));
+                            } else {
+                                wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                            }
+#endif
+                        } else if constexpr (LR) {
                             const uint32_t e = g & rmask;
                             lr[e] = 0.0f; lr[kPmLdsRing + e] = 0.0f; lr[2u * kPmLdsRing + e] = 0.0f;
                         } else {
@@ -3112,7 +3158,18 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 parked = PK && wp.parked;
             }
             if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
-                if constexpr (LR) {
+                if constexpr (HYB) {
+#ifdef RT_INW_HYB
+                    const f3 q = f3{__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z)};
+                    if (g - gf < kPmLdsRing) {
+                        const uint32_t e = g & (kPmLdsRing - 1u);
+                        lr[e] = q.x; lr[kPmLdsRing + e] = q.y; lr[2u * kPmLdsRing + e] = q.z;
+                        atomicOr(&lfl[e >> 5], 1u << (e & 31u));
+                    } else {
+                        wr[g & rmask] = make_float4(q.x, q.y, q.z, 0.0f);
+                    }
+#endif
+                } else if constexpr (LR) {
                     const uint32_t e = g & rmask;
                     lr[e] = __builtin_sqrtf(col.x);
                     lr[kPmLdsRing + e] = __builtin_sqrtf(col.y);
