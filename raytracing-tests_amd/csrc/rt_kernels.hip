@@ -2951,6 +2951,8 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     f3 acc = f3{0, 0, 0};              // running End() sum of pixel jf (the same in every lane)
     uint32_t pix_slot = 0xffffffffu;   // lane l: the unit of the claimed ordinal j with j % 64 == l
     f3 pc = f3{0, 0, 0};               // lane l: that pixel's mean, kept until its claim row is stored
+    uint32_t jrow = 0xffffffffu;       // ordinals from jrow on are claimed and stored one at a time
+    const uint32_t tail_px = 8u * gridDim.x * (blockDim.x >> 6);  // rows stop this many pixels from the end
     // per lane: the sample it traces
     bool busy = false;
     uint32_t g = 0, pj = 0;  // the lane's stream entry and its pixel's ordinal slot (j % 64)
@@ -3027,11 +3029,14 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 sf += e - i;
                 i = e;
                 if (sf == spp) {  // pixel jf complete: End()'s imageStores (01_BVH...glsl:652, 667-668)
-                    // the lane of its ordinal slot keeps the mean; once the 8 ordinals of a claim
-                    // row are done (claims come in rows of 8: 8 adjacent pixels of one 8x8 block),
-                    // their 8 lanes store colour and depth together (128 + 32 contiguous bytes)
+                    // the lane of its ordinal slot keeps the mean; once the ordinals of a claim row
+                    // are done (claims come in rows of 8 ordinals: 8 adjacent pixels of one 8x8
+                    // block; near the queue's end single pixels, from ordinal jrow on), its lanes
+                    // store colour and depth together (128 + 32 contiguous bytes for a full row)
                     if (lane == (jf & 63u)) pc = acc * inv;
-                    if ((jf & 7u) == 7u && lane - ((jf & 63u) & ~7u) < 8u) {
+                    const bool last = jf >= jrow || (jf & 7u) == 7u || jf + 1u == jrow;
+                    const uint32_t r0 = jf >= jrow ? (jf & 63u) : ((jf & 63u) & ~7u);
+                    if (last && lane - r0 <= (jf & 63u) - r0) {
                         const UnitPix p = unit_pixel(f, pix_slot);
                         if (p.out != (size_t)-1) {
                             reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
@@ -3053,18 +3058,23 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         const uint32_t nfree = (uint32_t)__popcll(fm);
         if (!qdone && nfree) {
             // ordinals the free lanes would reach: ji + (si + nfree - 1) / spp, claimed in rows of
-            // 8 and at most 64 ahead of the fold's row (a slot's colour and depth wait for its row)
-            const uint32_t lim = (jf & ~7u) + 64u;
+            // 8 and at most 64 ahead of the fold's row (a slot's colour and depth wait for its
+            // row); from jrow on one pixel at a time, so the queue drains evenly over the waves
+            const bool rows = jrow == 0xffffffffu;
+            const uint32_t lim = (jf < jrow ? (jf & ~7u) : jf) + 64u;
             uint32_t need = ji + (si + nfree - 1u) / spp + 1u;
             if (need > lim) need = lim;
             if (need > nclaimed) {
-                const uint32_t want = (need - nclaimed + 7u) & ~7u;  // nclaimed and lim are multiples of 8
+                const uint32_t want = rows ? (need - nclaimed + 7u) & ~7u : need - nclaimed;  // rows: nclaimed, lim multiples of 8
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(counter, want);
                 base = uni((uint32_t)__shfl((int)base, 0, 64));
                 uint32_t got = want;
                 if (base >= total) { got = 0; qdone = true; }
                 else if (base + want >= total) { got = total - base; qdone = true; }
+                // the last 8 claims' worth of every wave go one pixel at a time (rows near the end
+                // left waves holding up to 8 pixels when the queue drained: 1.4% of C3)
+                if (rows && (qdone || base + want + tail_px >= total)) jrow = nclaimed + got;
 #ifdef RT_DIAG_SPLIT
                 if (qdone && t_qd == 0) t_qd = wall_clock64();
 #endif

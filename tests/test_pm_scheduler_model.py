@@ -1,5 +1,6 @@
 """A CPU model of k_inw_pm's wave scheduler (raytracing-tests_amd/csrc/rt_kernels.hip, k_inw_pm):
-claims in rows of 8 ordinals at most 64 ahead of the fold's row, issue of stream entries
+claims in rows of 8 ordinals at most 64 ahead of the fold's row (single pixels once the queue is
+within 8 claims per wave of its end), issue of stream entries
 g = (pixel ordinal, sample) to free lanes within the fold window, the LDS ring's finished-entry
 rule (every issued entry below the smallest one a busy lane holds is stored), the in-order fold
 (01_BVH...glsl:625-653's End() sum order) and the row stores (8 lanes write one claim row once
@@ -16,11 +17,13 @@ import random
 import pytest
 
 RING = 256  # kPmLdsRing
+INF = float("inf")  # jrow before the switch to single-pixel claims
 
 
 class Wave:
-    def __init__(self, spp, rng, long_frac):
-        self.spp, self.rng, self.long_frac = spp, rng, long_frac
+    def __init__(self, spp, rng, long_frac, tail_px):
+        self.spp, self.rng, self.long_frac, self.tail_px = spp, rng, long_frac, tail_px
+        self.jrow = INF
         self.gi = self.ji = self.si = 0
         self.gf = self.jf = self.sf = 0
         self.nclaimed = 0
@@ -54,9 +57,10 @@ class Wave:
                 if self.sf == spp:
                     slot = self.jf & 63
                     self.pc[slot] = (self.jf, self.acc)
-                    if (self.jf & 7) == 7:  # the row's 8 lanes store
-                        r0 = slot & ~7
-                        for l in range(r0, r0 + 8):
+                    jrow = self.jrow
+                    if self.jf >= jrow or (self.jf & 7) == 7 or self.jf + 1 == jrow:  # the row's lanes store
+                        r0 = slot if self.jf >= jrow else slot & ~7
+                        for l in range(r0, slot + 1):
                             jo, a = self.pc[l]
                             assert jo == self.jf - (slot - l), "row slot holds another pixel"
                             unit = self.pix_slot[l]
@@ -69,11 +73,12 @@ class Wave:
         # claims: rows of 8, at most 64 ahead of the fold's row
         free = [l for l in range(64) if not self.busy[l]]
         if not self.qdone and free:
-            lim = (self.jf & ~7) + 64
+            rows = self.jrow is INF
+            lim = ((self.jf & ~7) if self.jf < self.jrow else self.jf) + 64
             need = min(self.ji + (self.si + len(free) - 1) // spp + 1, lim)
             if need > self.nclaimed:
-                want = (need - self.nclaimed + 7) & ~7
-                assert self.nclaimed % 8 == 0 and self.nclaimed + want <= lim
+                want = (need - self.nclaimed + 7) & ~7 if rows else need - self.nclaimed
+                assert not rows or (self.nclaimed % 8 == 0 and self.nclaimed + want <= lim)
                 base = counter[0]
                 counter[0] += want
                 got = want
@@ -81,6 +86,8 @@ class Wave:
                     got, self.qdone = 0, True
                 elif base + want >= total:
                     got, self.qdone = total - base, True
+                if rows and (self.qdone or base + want + self.tail_px >= total):
+                    self.jrow = self.nclaimed + got
                 for r in range(got):
                     j = self.nclaimed + r
                     old = self.pix_slot[j & 63]  # the slot's previous pixel: its row is stored
@@ -121,18 +128,21 @@ def value(unit, s):
     return (unit * 7919 + s * 104729) % 1000003
 
 
-@pytest.mark.parametrize("spp,units,waves,long_frac,seed", [
-    (37, 64 * 8, 3, 0.02, 1),
-    (500, 64 * 2, 2, 0.01, 2),     # a pixel's samples span more than the ring window
-    (1, 64 * 6, 4, 0.3, 3),        # more than 64 pixels per window
-    (3, 64 * 5, 3, 0.5, 4),
-    (64, 64 * 3, 5, 0.05, 5),      # more waves than rows per wave
+@pytest.mark.parametrize("spp,units,waves,long_frac,seed,tail", [
+    (37, 64 * 8, 3, 0.02, 1, 8),
+    (500, 64 * 2, 2, 0.01, 2, 8),     # a pixel's samples span more than the ring window
+    (1, 64 * 6, 4, 0.3, 3, 8),        # more than 64 pixels per window
+    (3, 64 * 5, 3, 0.5, 4, 8),
+    (64, 64 * 3, 5, 0.05, 5, 8),      # more waves than rows per wave
+    (5, 64 * 9, 3, 0.2, 6, 0),        # rows to the end
+    (7, 64 * 9, 4, 0.2, 7, 40),       # single-pixel claims for the last 40 x waves pixels
+    (2, 64 * 4, 6, 0.1, 8, 1000),     # single-pixel claims from the start
 ])
-def test_pixel_major_scheduler_model(spp, units, waves, long_frac, seed):
+def test_pixel_major_scheduler_model(spp, units, waves, long_frac, seed, tail):
     rng = random.Random(seed)
     counter = [0]
     out = {}
-    ws = [Wave(spp, rng, long_frac) for _ in range(waves)]
+    ws = [Wave(spp, rng, long_frac, tail * waves) for _ in range(waves)]
     live = list(ws)
     for _ in range(10_000_000):
         if not live:
