@@ -1110,14 +1110,10 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // inw_ring_pm = 0: k_inw_pm's fold ring in LDS (768-lane blocks), else a global
     // ring of that many entries per wave (1024 for the 256-lane blocks)
     const bool lring = o.inw_ring_pm == 0 && blocks_ln > 0;
-    const uint32_t ring_pm = lring ? rtk::kPmLdsRing : uint32_t(o.inw_ring_pm ? o.inw_ring_pm : 1024);
+    const uint32_t ring_pm = lring ? rtk::kPmRingWin : uint32_t(o.inw_ring_pm ? o.inw_ring_pm : 1024);
     const uint32_t ring_sm = uint32_t(o.inw_ring_sm);
     const size_t waves = std::max(size_t(blocks) * (rtk::kBlock / 64), size_t(blocks_ln) * (3 * rtk::kBlock / 64));
-#ifdef RT_INW_HYB  // experiment: the LDS ring's global overflow (rtk::kPmHybGlobal entries per wave)
-    const size_t ring_bytes = waves * std::max(lring ? rtk::kPmHybGlobal : ring_pm, ring_sm) * sizeof(float4);
-#else
     const size_t ring_bytes = waves * std::max(lring ? 0u : ring_pm, ring_sm) * sizeof(float4);
-#endif
     if (s->inw_ring.bytes < ring_bytes) {
         s->inw_ring.~DevBuf();
         new (&s->inw_ring) DevBuf();

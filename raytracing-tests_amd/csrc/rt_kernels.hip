@@ -1824,13 +1824,7 @@ __shared__ float4 g_inw_lnodes[kInwLdsNodes * kInwNodeF4];
 // same LDS (a 256-entry window costs 0.5% against 1024, 128 entries 7%; the ring
 // takes the LDS of all but the top 5 nodes, which were worth 1.5%, and saves 1% of global ring
 // traffic -- 0.57 against 42 GB of L2-to-fabric traffic per C3 frame)
-#ifdef RT_INW_HYB
-constexpr uint32_t kPmFlagBytes = 12 * kPmLdsRing / 8;  // one valid bit per LDS slot and wave
-#else
-constexpr uint32_t kPmFlagBytes = 0;
-#endif
-static_assert(kPmLdsNodes * kInwNodeF4 * 16 + 12 * 3 * kPmLdsRing * 4 + kPmFlagBytes <= kInwLdsNodes * kInwNodeF4 * 16,
-              "LDS ring");
+static_assert(kPmLdsNodes * kInwNodeF4 * 16 + 12 * 3 * kPmLdsRing * 4 <= kInwLdsNodes * kInwNodeF4 * 16, "LDS ring");
 template <bool LN>
 __device__ __forceinline__ const float4 *inw_node_ptr(const InwScene &S, int cur) {
     if (LN && (uint32_t)(cur - 1) < S.n_lnodes) return g_inw_lnodes + kInwNodeF4 * (cur - 1);
@@ -2920,23 +2914,9 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
 #endif
     FStack K{lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock), 0};
     const uint32_t lane = threadIdx.x & 63u;
-#ifdef RT_INW_HYB
-    // HYB (experiment): the LDS ring takes the entries stored less than kPmLdsRing after the
-    // fold's position; later ones go to a global ring of kPmHybGlobal entries, the issue window.
-    // A valid bit per LDS slot (set by the store, cleared by the fold) tells the fold where an
-    // entry is: a slot's valid entry is always the one being folded (a later entry of the slot
-    // goes to LDS only once this one is folded).
-    constexpr bool HYB = LR;
-    if constexpr (LR) rmask = kPmHybGlobal - 1u;
-    uint32_t *lfl = reinterpret_cast<uint32_t *>(reinterpret_cast<float *>(g_inw_lnodes + kPmLdsNodes * kInwNodeF4) +
-                                                 12u * 3u * kPmLdsRing) + uni((threadIdx.x >> 6) * (kPmLdsRing / 32u));
-    if constexpr (LR)
-        if ((threadIdx.x & 63u) < kPmLdsRing / 32u) lfl[threadIdx.x & 63u] = 0u;
-#else
-    constexpr bool HYB = false;
-    if constexpr (LR) rmask = kPmLdsRing - 1u;
-#endif
-    const uint32_t rsize = rmask + 1u;
+    // LR: the window is kPmRingWin entries (slot k % kPmRingWin); the planes' last 8 slots hold
+    // the colours of the fold's current claim row until the row is stored
+    const uint32_t rsize = LR ? kPmRingWin : rmask + 1u;
     float4 *wr = ring + (size_t)uni((blockIdx.x * (SUB * kBlock) + threadIdx.x) >> 6) * rsize;
     // LR: this wave's ring, three planes (r, g, b) of kPmLdsRing floats
     float *lr = reinterpret_cast<float *>(g_inw_lnodes + kPmLdsNodes * kInwNodeF4) + uni((threadIdx.x >> 6) * (3u * kPmLdsRing));
@@ -2950,7 +2930,6 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     bool qdone = false;
     f3 acc = f3{0, 0, 0};              // running End() sum of pixel jf (the same in every lane)
     uint32_t pix_slot = 0xffffffffu;   // lane l: the unit of the claimed ordinal j with j % 64 == l
-    f3 pc = f3{0, 0, 0};               // lane l: that pixel's mean, kept until its claim row is stored
     uint32_t jrow = 0xffffffffu;       // ordinals from jrow on are claimed and stored one at a time
     const uint32_t tail_px = 8u * gridDim.x * (blockDim.x >> 6);  // rows stop this many pixels from the end
     // per lane: the sample it traces
@@ -2985,23 +2964,8 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 n = uni(__ockl_wfred_min_u32(busy ? g - gf : 0xffffffffu));  // DPP reduction
                 if (n > gi - gf) n = gi - gf;
                 if (n > 64u) n = 64u;
-                if constexpr (HYB) {
-#ifdef RT_INW_HYB
-                    const uint32_t e = k & (kPmLdsRing - 1u);
-                    bool valid = false;
-                    if (lane < n) {
-                        valid = (lfl[e >> 5] >> (e & 31u)) & 1u;
-                        if (valid) v = make_float4(lr[e], lr[kPmLdsRing + e], lr[2u * kPmLdsRing + e], 0.0f);
-                    }
-                    const bool glob = lane < n && !valid;
-                    if (__ballot(glob)) {
-                        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's global stores have landed
-                        if (glob) v = wr[k & rmask];
-                    }
-                    if (valid) atomicAnd(&lfl[e >> 5], ~(1u << (e & 31u)));
-#endif
-                } else if (lane < n) {
-                    const uint32_t e = k & rmask;
+                if (lane < n) {
+                    const uint32_t e = k % kPmRingWin;
                     v = make_float4(lr[e], lr[kPmLdsRing + e], lr[2u * kPmLdsRing + e], 0.0f);
                 }
             } else {
@@ -3029,20 +2993,37 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 sf += e - i;
                 i = e;
                 if (sf == spp) {  // pixel jf complete: End()'s imageStores (01_BVH...glsl:652, 667-668)
-                    // the lane of its ordinal slot keeps the mean; once the ordinals of a claim row
-                    // are done (claims come in rows of 8 ordinals: 8 adjacent pixels of one 8x8
-                    // block; near the queue's end single pixels, from ordinal jrow on), its lanes
-                    // store colour and depth together (128 + 32 contiguous bytes for a full row)
-                    if (lane == (jf & 63u)) pc = acc * inv;
-                    const bool last = jf >= jrow || (jf & 7u) == 7u || jf + 1u == jrow;
-                    const uint32_t r0 = jf >= jrow ? (jf & 63u) : ((jf & 63u) & ~7u);
-                    if (last && lane - r0 <= (jf & 63u) - r0) {
-                        const UnitPix p = unit_pixel(f, pix_slot);
-                        if (p.out != (size_t)-1) {
-                            reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
-                                make_float4(p.in_image ? pc.x : 0.0f, p.in_image ? pc.y : 0.0f,
-                                            p.in_image ? pc.z : 0.0f, p.in_image ? 1.0f : 0.0f);
-                            if (f.out_depth) f.out_depth[p.out] = pdep[lane];
+                    if constexpr (LR) {
+                        // the mean waits in the row's colour slot; once the ordinals of a claim row
+                        // are done (claims come in rows of 8 ordinals: 8 adjacent pixels of one 8x8
+                        // block; near the queue's end single pixels, from ordinal jrow on), its lanes
+                        // store colour and depth together (128 + 32 contiguous bytes for a full row)
+                        const uint32_t cs = kPmRingWin + (jf & 7u);
+                        if (lane == 0) {
+                            lr[cs] = acc.x * inv; lr[kPmLdsRing + cs] = acc.y * inv; lr[2u * kPmLdsRing + cs] = acc.z * inv;
+                        }
+                        const bool last = jf >= jrow || (jf & 7u) == 7u || jf + 1u == jrow;
+                        const uint32_t r0 = jf >= jrow ? (jf & 63u) : ((jf & 63u) & ~7u);
+                        if (last && lane - r0 <= (jf & 63u) - r0) {
+                            const UnitPix p = unit_pixel(f, pix_slot);
+                            if (p.out != (size_t)-1) {
+                                const uint32_t cl = kPmRingWin + (lane & 7u);
+                                reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
+                                    p.in_image ? make_float4(lr[cl], lr[kPmLdsRing + cl], lr[2u * kPmLdsRing + cl], 1.0f)
+                                               : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                                if (f.out_depth) f.out_depth[p.out] = pdep[lane];
+                            }
+                        }
+                    } else {  // one lane stores the pixel
+                        const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
+                        if (lane == 0) {
+                            const UnitPix p = unit_pixel(f, unit);
+                            if (p.out != (size_t)-1) {
+                                reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
+                                    make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
+                                                p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
+                                if (f.out_depth) f.out_depth[p.out] = pdep[jf & 63u];
+                            }
                         }
                     }
                     sf = 0;
@@ -3117,18 +3098,8 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                         inw_start_sample_cd(S, f, K, pcd, s, c);
                     } else {  // a padding slot: an empty sample, folded as zero
                         if ((uint32_t)s == mid) pdep[pj] = 0.0f;
-                        if constexpr (HYB) {
-#ifdef RT_INW_HYB
-                            if (g - gf < kPmLdsRing) {
-                                const uint32_t e = g & (kPmLdsRing - 1u);
-                                lr[e] = 0.0f; lr[kPmLdsRing + e] = 0.0f; lr[2u * kPmLdsRing + e] = 0.0f;
-                                atomicOr(&lfl[e >> 5], 1u << (e & 31u));
-                            } else {
-                                wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                            }
-#endif
-                        } else if constexpr (LR) {
-                            const uint32_t e = g & rmask;
+                        if constexpr (LR) {
+                            const uint32_t e = g % kPmRingWin;
                             lr[e] = 0.0f; lr[kPmLdsRing + e] = 0.0f; lr[2u * kPmLdsRing + e] = 0.0f;
                         } else {
                             wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(ring_tag(S, g)));
@@ -3168,19 +3139,8 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 parked = PK && wp.parked;
             }
             if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
-                if constexpr (HYB) {
-#ifdef RT_INW_HYB
-                    const f3 q = f3{__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z)};
-                    if (g - gf < kPmLdsRing) {
-                        const uint32_t e = g & (kPmLdsRing - 1u);
-                        lr[e] = q.x; lr[kPmLdsRing + e] = q.y; lr[2u * kPmLdsRing + e] = q.z;
-                        atomicOr(&lfl[e >> 5], 1u << (e & 31u));
-                    } else {
-                        wr[g & rmask] = make_float4(q.x, q.y, q.z, 0.0f);
-                    }
-#endif
-                } else if constexpr (LR) {
-                    const uint32_t e = g & rmask;
+                if constexpr (LR) {
+                    const uint32_t e = g % kPmRingWin;
                     lr[e] = __builtin_sqrtf(col.x);
                     lr[kPmLdsRing + e] = __builtin_sqrtf(col.y);
                     lr[2u * kPmLdsRing + e] = __builtin_sqrtf(col.z);

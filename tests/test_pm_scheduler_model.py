@@ -16,7 +16,7 @@ import random
 
 import pytest
 
-RING = 256  # kPmLdsRing
+RING = 248  # kPmRingWin
 INF = float("inf")  # jrow before the switch to single-pixel claims
 
 
