@@ -1199,7 +1199,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     if (epoch == 0) e = hipMemsetAsync(s->inw_ring.p, 0xff, s->inw_ring.bytes, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->first, st);
     if (e == hipSuccess)
-        e = rtk::launch_inw_fold(f, sc, s->inw_ring.as<float4>(), ring_pm, ring_sm, s->counter.as<unsigned>(),
+        e = rtk::launch_inw_fold(f, sc, s->inw_ring.as<float4>(), lring ? rtk::kPmLdsRing : ring_pm, ring_sm, s->counter.as<unsigned>(),
                                  s->inw_mode.as<uint32_t>(), force, blocks, blocks_ln, cost, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->second, st);
     if (e != hipSuccess) {
