@@ -1110,7 +1110,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // inw_ring_pm = 0: k_inw_pm's fold ring in LDS (768-lane blocks), else a global
     // ring of that many entries per wave (1024 for the 256-lane blocks)
     const bool lring = o.inw_ring_pm == 0 && blocks_ln > 0;
-    const uint32_t ring_pm = lring ? rtk::kPmRingWin : uint32_t(o.inw_ring_pm ? o.inw_ring_pm : 1024);
+    const uint32_t ring_pm = lring ? rtk::kPmLdsRing : uint32_t(o.inw_ring_pm ? o.inw_ring_pm : 1024);
     const uint32_t ring_sm = uint32_t(o.inw_ring_sm);
     const size_t waves = std::max(size_t(blocks) * (rtk::kBlock / 64), size_t(blocks_ln) * (3 * rtk::kBlock / 64));
     const size_t ring_bytes = waves * std::max(lring ? 0u : ring_pm, ring_sm) * sizeof(float4);
@@ -1199,7 +1199,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     if (epoch == 0) e = hipMemsetAsync(s->inw_ring.p, 0xff, s->inw_ring.bytes, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->first, st);
     if (e == hipSuccess)
-        e = rtk::launch_inw_fold(f, sc, s->inw_ring.as<float4>(), lring ? rtk::kPmLdsRing : ring_pm, ring_sm, s->counter.as<unsigned>(),
+        e = rtk::launch_inw_fold(f, sc, s->inw_ring.as<float4>(), ring_pm, ring_sm, s->counter.as<unsigned>(),
                                  s->inw_mode.as<uint32_t>(), force, blocks, blocks_ln, cost, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->second, st);
     if (e != hipSuccess) {

@@ -2914,9 +2914,8 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
 #endif
     FStack K{lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock), 0};
     const uint32_t lane = threadIdx.x & 63u;
-    // LR: the window is kPmRingWin entries (slot k % kPmRingWin); the planes' last 8 slots hold
-    // the colours of the fold's current claim row until the row is stored
-    const uint32_t rsize = LR ? kPmRingWin : rmask + 1u;
+    if constexpr (LR) rmask = kPmLdsRing - 1u;
+    const uint32_t rsize = rmask + 1u;
     float4 *wr = ring + (size_t)uni((blockIdx.x * (SUB * kBlock) + threadIdx.x) >> 6) * rsize;
     // LR: this wave's ring, three planes (r, g, b) of kPmLdsRing floats
     float *lr = reinterpret_cast<float *>(g_inw_lnodes + kPmLdsNodes * kInwNodeF4) + uni((threadIdx.x >> 6) * (3u * kPmLdsRing));
@@ -2930,8 +2929,6 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     bool qdone = false;
     f3 acc = f3{0, 0, 0};              // running End() sum of pixel jf (the same in every lane)
     uint32_t pix_slot = 0xffffffffu;   // lane l: the unit of the claimed ordinal j with j % 64 == l
-    uint32_t jrow = 0xffffffffu;       // ordinals from jrow on are claimed and stored one at a time
-    const uint32_t tail_px = 8u * gridDim.x * (blockDim.x >> 6);  // rows stop this many pixels from the end
     // per lane: the sample it traces
     bool busy = false;
     uint32_t g = 0, pj = 0;  // the lane's stream entry and its pixel's ordinal slot (j % 64)
@@ -2965,7 +2962,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 if (n > gi - gf) n = gi - gf;
                 if (n > 64u) n = 64u;
                 if (lane < n) {
-                    const uint32_t e = k % kPmRingWin;
+                    const uint32_t e = k & rmask;
                     v = make_float4(lr[e], lr[kPmLdsRing + e], lr[2u * kPmLdsRing + e], 0.0f);
                 }
             } else {
@@ -2993,37 +2990,14 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 sf += e - i;
                 i = e;
                 if (sf == spp) {  // pixel jf complete: End()'s imageStores (01_BVH...glsl:652, 667-668)
-                    if constexpr (LR) {
-                        // the mean waits in the row's colour slot; once the ordinals of a claim row
-                        // are done (claims come in rows of 8 ordinals: 8 adjacent pixels of one 8x8
-                        // block; near the queue's end single pixels, from ordinal jrow on), its lanes
-                        // store colour and depth together (128 + 32 contiguous bytes for a full row)
-                        const uint32_t cs = kPmRingWin + (jf & 7u);
-                        if (lane == 0) {
-                            lr[cs] = acc.x * inv; lr[kPmLdsRing + cs] = acc.y * inv; lr[2u * kPmLdsRing + cs] = acc.z * inv;
-                        }
-                        const bool last = jf >= jrow || (jf & 7u) == 7u || jf + 1u == jrow;
-                        const uint32_t r0 = jf >= jrow ? (jf & 63u) : ((jf & 63u) & ~7u);
-                        if (last && lane - r0 <= (jf & 63u) - r0) {
-                            const UnitPix p = unit_pixel(f, pix_slot);
-                            if (p.out != (size_t)-1) {
-                                const uint32_t cl = kPmRingWin + (lane & 7u);
-                                reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
-                                    p.in_image ? make_float4(lr[cl], lr[kPmLdsRing + cl], lr[2u * kPmLdsRing + cl], 1.0f)
-                                               : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                                if (f.out_depth) f.out_depth[p.out] = pdep[lane];
-                            }
-                        }
-                    } else {  // one lane stores the pixel
-                        const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
-                        if (lane == 0) {
-                            const UnitPix p = unit_pixel(f, unit);
-                            if (p.out != (size_t)-1) {
-                                reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
-                                    make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
-                                                p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
-                                if (f.out_depth) f.out_depth[p.out] = pdep[jf & 63u];
-                            }
+                    const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
+                    if (lane == 0) {
+                        const UnitPix p = unit_pixel(f, unit);
+                        if (p.out != (size_t)-1) {
+                            reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
+                                make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
+                                            p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
+                            if (f.out_depth) f.out_depth[p.out] = pdep[jf & 63u];
                         }
                     }
                     sf = 0;
@@ -3038,24 +3012,17 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         const unsigned long long fm = __ballot(!busy);
         const uint32_t nfree = (uint32_t)__popcll(fm);
         if (!qdone && nfree) {
-            // ordinals the free lanes would reach: ji + (si + nfree - 1) / spp, claimed in rows of
-            // 8 and at most 64 ahead of the fold's row (a slot's colour and depth wait for its
-            // row); from jrow on one pixel at a time, so the queue drains evenly over the waves
-            const bool rows = jrow == 0xffffffffu;
-            const uint32_t lim = (jf < jrow ? (jf & ~7u) : jf) + 64u;
+            // ordinals the free lanes would reach: ji + (si + nfree - 1) / spp, capped at jf + 63
             uint32_t need = ji + (si + nfree - 1u) / spp + 1u;
-            if (need > lim) need = lim;
+            if (need > jf + 64u) need = jf + 64u;
             if (need > nclaimed) {
-                const uint32_t want = rows ? (need - nclaimed + 7u) & ~7u : need - nclaimed;  // rows: nclaimed, lim multiples of 8
+                const uint32_t want = need - nclaimed;
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(counter, want);
                 base = uni((uint32_t)__shfl((int)base, 0, 64));
                 uint32_t got = want;
                 if (base >= total) { got = 0; qdone = true; }
                 else if (base + want >= total) { got = total - base; qdone = true; }
-                // the last 8 claims' worth of every wave go one pixel at a time (rows near the end
-                // left waves holding up to 8 pixels when the queue drained: 1.4% of C3)
-                if (rows && (qdone || base + want + tail_px >= total)) jrow = nclaimed + got;
 #ifdef RT_DIAG_SPLIT
                 if (qdone && t_qd == 0) t_qd = wall_clock64();
 #endif
@@ -3099,7 +3066,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                     } else {  // a padding slot: an empty sample, folded as zero
                         if ((uint32_t)s == mid) pdep[pj] = 0.0f;
                         if constexpr (LR) {
-                            const uint32_t e = g % kPmRingWin;
+                            const uint32_t e = g & rmask;
                             lr[e] = 0.0f; lr[kPmLdsRing + e] = 0.0f; lr[2u * kPmLdsRing + e] = 0.0f;
                         } else {
                             wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(ring_tag(S, g)));
@@ -3140,7 +3107,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             }
             if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
                 if constexpr (LR) {
-                    const uint32_t e = g % kPmRingWin;
+                    const uint32_t e = g & rmask;
                     lr[e] = __builtin_sqrtf(col.x);
                     lr[kPmLdsRing + e] = __builtin_sqrtf(col.y);
                     lr[2u * kPmLdsRing + e] = __builtin_sqrtf(col.z);

@@ -189,7 +189,6 @@ constexpr int kBlock = 256;      // threads per block of every render kernel
 constexpr int kInwLdsNodes = 236;        // wide BVH nodes the INW fold kernels stage in LDS (rt_kernels.hip)
 constexpr uint32_t kPmLdsRing = 256;     // k_inw_pm's LDS fold ring: entries per wave (InwScene::lring) ...
 constexpr uint32_t kPmLdsNodes = 5;      // ... and the nodes it leaves staged
-constexpr uint32_t kPmRingWin = kPmLdsRing - 8;  // its fold window; the last 8 slots hold a claim row's colours
 constexpr int kParkBelow = 32;    // park when fewer than half the wave's lanes are busy
 constexpr int kContSlots = 13;    // float4 per parked lane
 struct Cont {

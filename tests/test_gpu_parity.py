@@ -220,7 +220,7 @@ def test_scene_update_matches_fresh_scene(gpu, device_lbvh):
 
 def test_debug_path_reports_the_fold_ring(gpu):
     """rt_debug_path names the kernel and where its fold ring lived: k_inw_pm's ring in LDS by
-    default (248 entries per wave, 5 staged nodes), a global ring with inw_ring_pm > 0 (236 staged
+    default (256 entries per wave, 5 staged nodes), a global ring with inw_ring_pm > 0 (236 staged
     nodes); the sample-major kernel keeps its global ring."""
     import ctypes as C
 
@@ -250,7 +250,7 @@ def test_debug_path_reports_the_fold_ring(gpu):
         lib.rt_dev_scene_free(s)
     print(paths)
     p = paths["lds"]
-    assert p["kernel"].startswith("k_inw_pm") and p["ring_lds"] == 1 and p["ring_entries"] == 248
+    assert p["kernel"].startswith("k_inw_pm") and p["ring_lds"] == 1 and p["ring_entries"] == 256
     assert p["lds_nodes"] == 5
     p = paths["global"]
     assert p["kernel"].startswith("k_inw_pm") and p["ring_lds"] == 0 and p["ring_entries"] == 1024

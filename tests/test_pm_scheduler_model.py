@@ -1,36 +1,31 @@
 """A CPU model of k_inw_pm's wave scheduler (raytracing-tests_amd/csrc/rt_kernels.hip, k_inw_pm):
-claims in rows of 8 ordinals at most 64 ahead of the fold's row (single pixels once the queue is
-within 8 claims per wave of its end), issue of stream entries
-g = (pixel ordinal, sample) to free lanes within the fold window, the LDS ring's finished-entry
-rule (every issued entry below the smallest one a busy lane holds is stored), the in-order fold
-(01_BVH...glsl:625-653's End() sum order) and the row stores (8 lanes write one claim row once
-its 8 pixels are folded).
+pixel claims at most 64 ordinals ahead of the fold, issue of stream entries g = (pixel ordinal,
+sample) to free lanes within the fold window, the LDS ring's finished-entry rule (every issued
+entry below the smallest one a busy lane holds is stored), the in-order fold (01_BVH...glsl:
+625-653's End() sum order) and the pixel store when its last sample is folded.
 
 Several waves share one claim counter; sample lengths are drawn at random (mostly one segment,
 a few very long: stragglers that hold the window). The model checks what the kernel's exactness
 rests on: every pixel's samples are folded in sample order, every pixel is stored exactly once
-with the right sum, a row is stored only when its 8 pixels are folded and its slots still hold
-them, and every wave terminates with its grid drained.
+with the right sum while its ordinal slot still holds it, and every wave terminates with its grid
+drained.
 """
 import random
 
 import pytest
 
-RING = 248  # kPmRingWin
-INF = float("inf")  # jrow before the switch to single-pixel claims
+RING = 256  # kPmLdsRing
 
 
 class Wave:
-    def __init__(self, spp, rng, long_frac, tail_px):
-        self.spp, self.rng, self.long_frac, self.tail_px = spp, rng, long_frac, tail_px
-        self.jrow = INF
+    def __init__(self, spp, rng, long_frac):
+        self.spp, self.rng, self.long_frac = spp, rng, long_frac
         self.gi = self.ji = self.si = 0
         self.gf = self.jf = self.sf = 0
         self.nclaimed = 0
         self.qdone = False
         self.acc = None
         self.pix_slot = [None] * 64
-        self.pc = [None] * 64
         self.busy = [False] * 64
         self.g = [0] * 64
         self.left = [0] * 64
@@ -55,30 +50,20 @@ class Wave:
                 self.acc = v if self.sf == 0 else self.acc + v
                 self.sf += 1
                 if self.sf == spp:
-                    slot = self.jf & 63
-                    self.pc[slot] = (self.jf, self.acc)
-                    jrow = self.jrow
-                    if self.jf >= jrow or (self.jf & 7) == 7 or self.jf + 1 == jrow:  # the row's lanes store
-                        r0 = slot if self.jf >= jrow else slot & ~7
-                        for l in range(r0, slot + 1):
-                            jo, a = self.pc[l]
-                            assert jo == self.jf - (slot - l), "row slot holds another pixel"
-                            unit = self.pix_slot[l]
-                            assert unit[0] == jo
-                            assert unit[1] not in out, "pixel stored twice"
-                            out[unit[1]] = a
+                    unit = self.pix_slot[self.jf & 63]
+                    assert unit[0] == self.jf, "ordinal slot holds another pixel"
+                    assert unit[1] not in out, "pixel stored twice"
+                    out[unit[1]] = self.acc
                     self.sf = 0
                     self.jf += 1
             self.gf += n
-        # claims: rows of 8, at most 64 ahead of the fold's row
+        # claims: at most 64 ordinals ahead of the fold
         free = [l for l in range(64) if not self.busy[l]]
         if not self.qdone and free:
-            rows = self.jrow is INF
-            lim = ((self.jf & ~7) if self.jf < self.jrow else self.jf) + 64
+            lim = self.jf + 64
             need = min(self.ji + (self.si + len(free) - 1) // spp + 1, lim)
             if need > self.nclaimed:
-                want = (need - self.nclaimed + 7) & ~7 if rows else need - self.nclaimed
-                assert not rows or (self.nclaimed % 8 == 0 and self.nclaimed + want <= lim)
+                want = need - self.nclaimed
                 base = counter[0]
                 counter[0] += want
                 got = want
@@ -86,12 +71,10 @@ class Wave:
                     got, self.qdone = 0, True
                 elif base + want >= total:
                     got, self.qdone = total - base, True
-                if rows and (self.qdone or base + want + self.tail_px >= total):
-                    self.jrow = self.nclaimed + got
                 for r in range(got):
                     j = self.nclaimed + r
-                    old = self.pix_slot[j & 63]  # the slot's previous pixel: its row is stored
-                    assert old is None or (old[0] | 7) < self.jf, "slot reclaimed before its row was stored"
+                    old = self.pix_slot[j & 63]  # the slot's previous pixel is stored
+                    assert old is None or old[0] < self.jf, "slot reclaimed before its pixel was stored"
                     self.pix_slot[j & 63] = (j, base + r)
                 self.nclaimed += got
         # issue within the window
@@ -128,21 +111,19 @@ def value(unit, s):
     return (unit * 7919 + s * 104729) % 1000003
 
 
-@pytest.mark.parametrize("spp,units,waves,long_frac,seed,tail", [
-    (37, 64 * 8, 3, 0.02, 1, 8),
-    (500, 64 * 2, 2, 0.01, 2, 8),     # a pixel's samples span more than the ring window
-    (1, 64 * 6, 4, 0.3, 3, 8),        # more than 64 pixels per window
-    (3, 64 * 5, 3, 0.5, 4, 8),
-    (64, 64 * 3, 5, 0.05, 5, 8),      # more waves than rows per wave
-    (5, 64 * 9, 3, 0.2, 6, 0),        # rows to the end
-    (7, 64 * 9, 4, 0.2, 7, 40),       # single-pixel claims for the last 40 x waves pixels
-    (2, 64 * 4, 6, 0.1, 8, 1000),     # single-pixel claims from the start
+@pytest.mark.parametrize("spp,units,waves,long_frac,seed", [
+    (37, 64 * 8, 3, 0.02, 1),
+    (500, 64 * 2, 2, 0.01, 2),     # a pixel's samples span more than the ring window
+    (1, 64 * 6, 4, 0.3, 3),        # more than 64 pixels per window
+    (3, 64 * 5, 3, 0.5, 4),
+    (64, 64 * 3, 5, 0.05, 5),      # more waves than rows per wave
+    (7, 64 * 9, 4, 0.2, 7),
 ])
-def test_pixel_major_scheduler_model(spp, units, waves, long_frac, seed, tail):
+def test_pixel_major_scheduler_model(spp, units, waves, long_frac, seed):
     rng = random.Random(seed)
     counter = [0]
     out = {}
-    ws = [Wave(spp, rng, long_frac, tail * waves) for _ in range(waves)]
+    ws = [Wave(spp, rng, long_frac) for _ in range(waves)]
     live = list(ws)
     for _ in range(10_000_000):
         if not live:
