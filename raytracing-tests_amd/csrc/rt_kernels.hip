@@ -372,9 +372,6 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
         // farthest-first.
         DBG_T0(F_, t_trav);
         int sp = 0, pend = -1, cur = S.root_link;
-#ifdef RT_IOW_PEND2  // experiment: two postponed leaves per lane
-        int pend2 = -1;
-#endif
         bool walking = true, ovf = false;  // ovf: a child was dropped by a full stack
         float lim = min_t * 1.0001f + 1e-3f;  // culling limit, follows min_t
         for (;;) {
@@ -405,29 +402,15 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
                     cur = k0;
                     pop = t0 == kMiss;
                 } else {
-#ifdef RT_IOW_PEND2
-                    pop = pend < 0 || pend2 < 0;
-                    if (pend < 0) pend = -cur;
-                    else if (pend2 < 0) pend2 = -cur;
-#else
                     pop = pend < 0;  // a leaf waits while the lane still holds one
                     if (pop) pend = -cur;
-#endif
                 }
                 if (pop) {
                     if (sp == 0) walking = false;
                     else cur = bstk[(--sp) * kBlock];
                 }
             }
-#ifdef RT_IOW_PEND2
-            if (__all(!walking || pend2 >= 0) || __popcll(__ballot(pend >= 0)) >= F_.leaf_batch) {
-                if (pend >= 0) { test(pend); pend = pend2; pend2 = -1; lim = min_t * 1.0001f + 1e-3f; }
-                if (__all(!walking && pend < 0)) break;
-            }
-            if (false) {
-#else
             if (__all(!walking || pend >= 0) || __popcll(__ballot(pend >= 0)) >= F_.leaf_batch) {
-#endif
                 DBG_TALLY(F_, c, kDbgLeaf, pend >= 0);
                 DBG_T0(F_, t_leaf);
                 if (pend >= 0) { test(pend); pend = -1; lim = min_t * 1.0001f + 1e-3f; }
@@ -1960,9 +1943,6 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
     const int base = (int)K.size + (PK ? 8 : 0), cap = kFStack - 3 - base;
     const uint32_t ox = d.x < 0.0f ? 3u : 0u, oy = d.y < 0.0f ? 4u : 1u, oz = d.z < 0.0f ? 5u : 2u;
     int sp = 0, pend = -1, cur = S.wroot;
-#ifdef RT_INW_PEND2
-    int pend2 = -1;
-#endif
     bool walking = ok, ovf = false;
     float lim = bt * 1.0001f + 1e-3f;
     if constexpr (PK) {
@@ -2027,14 +2007,8 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
                 cur = k0;
                 pop = t0 == kMiss;
             } else {
-#ifdef RT_INW_PEND2  // experiment: two postponed leaves per lane
-                pop = pend2 < 0;
-                if (pend < 0) pend = -cur;
-                else if (pend2 < 0) pend2 = -cur;
-#else
                 pop = pend < 0;  // a leaf waits while the lane still holds one
                 if (pop) pend = -cur;
-#endif
             }
             if (pop) {
                 if (sp == 0) walking = false;
@@ -2042,22 +2016,11 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
             }
             if (ovf) walking = false;
         }
-#ifdef RT_INW_PEND2
-        if (__all(!walking || pend2 >= 0)) {
-            OCC_TALLY(c, kOccLeaf, pend >= 0);
-            if (pend >= 0) { leaf(pend); pend = pend2; pend2 = -1; }
-            if (__all(!walking)) {
-                if (pend >= 0) { leaf(pend); pend = -1; }
-                break;
-            }
-        }
-#else
         if (__all(!walking || pend >= 0)) {
             OCC_TALLY(c, kOccLeaf, pend >= 0);
             if (pend >= 0) { leaf(pend); pend = -1; }
             if (__all(!walking)) break;
         }
-#endif
         if constexpr (PK) {
             if (++trips >= kParkMinTrips && __popcll(__ballot(walking)) <= kParkLanes) {
                 if (__any(pend >= 0)) {  // every pending leaf is tested before the lanes part
@@ -3090,11 +3053,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         // whose next ray is a primary one; round 1 every lane with a ray left, the bounce rays those
         // primaries just pushed included, so the walk runs with the bounce rays of the whole wave.
         // INW-04 (LIGHTS) keeps one round: with its shadow walks the two-round loop spills 17 VGPRs
-#ifdef RT_INW_ONE  // A/B: one segment per lane and iteration (round 3)
-        constexpr int kRounds = 1;
-#else
         constexpr int kRounds = LIGHTS ? 1 : 2;
-#endif
 #pragma unroll 1
         for (int round = 2 - kRounds; round < 2; round++) {
             const bool prim = bu != kBeamOff && !parked && K.size >= 8u && K.at(K.size - 1u) == 0.0f;
