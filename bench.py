@@ -129,6 +129,39 @@ def lpt_deal(costs, nx: int, ny: int, world: int):
     return lists
 
 
+def refine_deal(lists, costs, times, nx: int, tol: float = 0.003):
+    """Rebalance a deal by measured rank times (the view is static, so a frame's times predict the
+    next one's).  Each rank's time per unit of tile cost k_r = time_r / load_r folds in what rays
+    alone miss (the long dependent chains of IOW-03 samples, the tail of a rank's last pixels);
+    the equal-time target T solves sum_r T / k_r = sum_r load_r.  Ranks above their share T / k_r
+    hand their cheapest tiles to the rank furthest below its share until within `tol`, so the
+    heavy tiles -- where the long chains are -- stay where they were measured.  Deterministic:
+    every rank computes the same lists from the same reduced costs and gathered times.
+    costs[ty * nx + tx] = rays per tile; times[r] = rank r's frame time."""
+    lists = [[tuple(t) for t in lst] for lst in lists]
+    cost = lambda t: float(costs[t[1] * nx + t[0]])  # noqa: E731
+    load = [sum(cost(t) for t in lst) for lst in lists]
+    if min(load) <= 0.0 or min(times) <= 0.0:
+        return lists
+    k = [float(tm) / ld for tm, ld in zip(times, load)]
+    target = sum(load) / sum(1.0 / kr for kr in k)
+    want = [target / kr for kr in k]
+    for r in sorted(range(len(lists)), key=lambda r: (want[r] - load[r], r)):
+        movable = sorted(lists[r], key=lambda t: (cost(t), t[1], t[0]))  # cheapest first
+        for t in movable:
+            if load[r] - want[r] <= tol * want[r]:
+                break
+            s = min(range(len(lists)), key=lambda q: ((load[q] - want[q]) / want[q], q))
+            c = cost(t)
+            if load[s] + c > want[s] * (1.0 + tol) or c > load[r] - want[r]:
+                continue
+            lists[r].remove(t)
+            lists[s].append(t)
+            load[r] -= c
+            load[s] += c
+    return lists
+
+
 def assemble_lists(src, lists, nx: int, ny: int):
     """src: [world, per_rank, T, T, 4] packed tiles as gathered on rank 0, where tile t of rank r
     is lists[r][t].  Returns the [ny*T, nx*T, 4] frame (crop to W x H)."""
@@ -221,6 +254,10 @@ def main():
     ap.add_argument("--balance", action="store_true",
                     help="multi-rank: deal the timed frames' tiles by LPT over the warm-up frame's tile costs "
                          "(measured neutral on the 8-way frames: their time is set by long samples, not by rays)")
+    ap.add_argument("--balance-time", action="store_true",
+                    help="multi-rank: after the warm-up frames (hashed deal), move each rank's cheapest tiles "
+                         "from ranks above the equal-time share to ranks below it, by the warm-up frame's "
+                         "measured rank times and per-tile rays (bench.refine_deal)")
     ap.add_argument("--occupancy", action="store_true", help="report per-phase lane occupancy (diagnostic)")
     ap.add_argument("--save-image", default="", help="rank 0 saves the assembled frame (.npy) for checking")
     ap.add_argument("--rebuild", action="store_true",
@@ -281,6 +318,12 @@ def main():
     nx, ny = math.ceil(W / T), math.ceil(H / T)
     allt = deal_order(nx, ny, nparts)
     lists = [allt[r::nparts] for r in range(nparts)]  # the hashed deal (first frame)
+    deal_file = os.environ.get("RT_BENCH_DEAL", "")  # diagnostic: a deal computed elsewhere (tools/gpu/shares_refined.sh)
+    if deal_file:
+        with open(deal_file) as fh:
+            lists = [[tuple(t) for t in lst] for lst in json.load(fh)]
+        if len(lists) != nparts:
+            raise SystemExit(f"RT_BENCH_DEAL holds {len(lists)} lists for {nparts} parts")
 
     if inw:
         lt = sc.lights if sc.lights is not None and len(sc.lights) else None
@@ -387,6 +430,9 @@ def main():
     # (the view is static, so a frame's costs predict the next one's).  A shard-diagnostic
     # process renders every tile in its warm-up to get them (cached in RT_BENCH_COSTS).
     balance = nparts > 1 and args.balance and args.warmup > 0
+    tbal = nparts > 1 and args.balance_time and args.warmup > 0 and not shard
+    if tbal:
+        lib.rt_debug_pixel_rays(buf["px_rays"].data_ptr())
     costs = None
     cache = os.environ.get("RT_BENCH_COSTS", "")
     if balance and shard and cache and os.path.exists(cache):
@@ -395,11 +441,30 @@ def main():
         use_tiles(allt, len(allt))
     if balance and costs is None:
         lib.rt_debug_pixel_rays(buf["px_rays"].data_ptr())
+    wt = 0.0
     for w in range(args.warmup):
-        if balance and costs is None and w == args.warmup - 1:
+        if (balance and costs is None or tbal) and w == args.warmup - 1:
             buf["px_rays"].zero_()
-        step()
+        if tbal and w == args.warmup - 1:
+            torch.cuda.synchronize()
+            tw = time.perf_counter()
+            step()
+            torch.cuda.synchronize()
+            wt = time.perf_counter() - tw
+        else:
+            step()
     barrier()
+    if tbal:  # refine the hashed deal by the last warm-up frame's rank times
+        tcosts = tile_costs()
+        lib.rt_debug_pixel_rays(None)
+        tt = torch.tensor([wt], dtype=torch.float64, device="cpu" if host_coll else dev)
+        gl = [torch.zeros_like(tt) for _ in range(world)]
+        dist.all_gather(gl, tt)
+        lists = refine_deal(lists, tcosts, [float(x.item()) for x in gl], nx)
+        per_rank = max(len(v) for v in lists)
+        use_tiles(lists[part], per_rank)
+        step()  # one frame on the final partition (first use of its buffers)
+        barrier()
     if balance:
         if costs is None:
             costs = tile_costs()
@@ -537,7 +602,8 @@ def main():
             "data": data,
             "config": {"workload": wl1 if world == 1 else wln.format(n=world), "width": W, "height": H,
                        "spp": spp, "max_bounces": sc.params.max_bounces, "objects": sc.n, "tile": T,
-                       "parallelism": f"tiles_rr{world}" + ("+rccl_gather" if world > 1 else "")},
+                       "parallelism": f"tiles_rr{world}" + ("+rccl_gather" if world > 1 else ""),
+                       "deal": ("lpt_rays" if balance else "time_refined" if tbal else "hashed") if world > 1 else None},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                          "traffic": traffic, "lane_issue_frac": round(lane_issue, 4) if lane_issue else None,

@@ -63,3 +63,25 @@ def test_block_parity_bits_and_nans():
     assert 0.0 < p["max_abs"] < 1e-6
     dep[2, 3] = 0.0
     assert bench.block_parity(rect, ref, ref_d, img, dep)["nan_mismatch"] == 1
+
+
+def test_refine_deal_moves_cheap_tiles_off_slow_ranks():
+    rng = np.random.default_rng(5)
+    nx, ny, world = 24, 12, 4
+    costs = rng.uniform(1.0, 2.0, nx * ny)
+    costs[5 * nx + 7] = 80.0  # one heavy tile (a long chain) on whichever rank holds it
+    order = bench.deal_order(nx, ny, world)
+    lists = [order[r::world] for r in range(world)]
+    heavy = (7, 5)
+    hr = next(r for r in range(world) if heavy in lists[r])
+    load = [sum(costs[ty * nx + tx] for tx, ty in lst) for lst in lists]
+    times = [ld * (1.3 if r == hr else 1.0) for r, ld in enumerate(load)]  # the heavy rank runs slower per ray
+    new = bench.refine_deal(lists, costs, times, nx)
+    flat = sorted(t for lst in new for t in lst)
+    assert flat == sorted(order)
+    assert heavy in new[hr]  # the heavy tile stays where it was measured
+    k = [tm / ld for tm, ld in zip(times, load)]
+    pred = [k[r] * sum(costs[ty * nx + tx] for tx, ty in new[r]) for r in range(world)]
+    assert max(pred) / min(pred) < 1.05 < max(times) / min(times)  # 2.3x apart before
+    # deterministic: the same inputs give the same lists on every rank
+    assert bench.refine_deal(lists, costs, times, nx) == new
