@@ -127,7 +127,8 @@ typedef struct rt_options {
     int park_min;           /* park lanes only while at least this many units remain (-1: resident lanes / 8) */
     int spec_iters;         /* resolve + re-run passes */
     int spec_probe;         /* heavy-first: every spec_probe-th pixel probes all sample indices */
-    int spec_heavy;         /* heavy-first: costliest sample indices run first (-1: (spp - 1) / 20) */
+    int spec_heavy;         /* heavy-first: costliest sample indices run first (-1: (spp - 1) / 20,
+                               (spp - 1) / 10 for a render of at most half the frame) */
     int spec_rounds;        /* checkpoint rounds of the speculative pass (0 = one launch) */
     int spec_tail_rounds;   /* budgeted tail rounds */
     int spec_tail_budget;   /* segments per unit and budgeted tail round */
@@ -135,7 +136,8 @@ typedef struct rt_options {
     int spec_chain;         /* exact restarts follow their pixel's chain */
     int spec_alt;           /* alternative runs for long samples that read one stale entry */
     int spec_alt_cap;       /* alternative-run records */
-    int spec_alt_seg;       /* segments that make a sample long enough for alternatives */
+    int spec_alt_seg;       /* segments that make a sample long enough for alternatives (0: 16384,
+                               2048 for a render of at most half the frame) */
     int spec_alt_every;     /* also spawn alternatives after every k-th budgeted tail round (0 = once) */
     int spec_spread;        /* the last round of a pass gives long samples a wave each */
     int spec_prior_from;    /* first sample whose stale entries are guessed as the scene's RI prior */

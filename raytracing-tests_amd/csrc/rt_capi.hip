@@ -38,7 +38,7 @@ rt_options default_options() {
     o.rounds_seq = 6; o.rounds_spec = 1; o.park_min = -1;
     o.spec_iters = 1; o.spec_probe = 64; o.spec_heavy = -1; o.spec_rounds = 24; o.spec_tail_rounds = 60;
     o.spec_tail_budget = 3072; o.spec_scan = 128; o.spec_chain = 1; o.spec_alt = 1; o.spec_alt_cap = 1 << 17;
-    o.spec_alt_seg = 16384; o.spec_alt_every = 0; o.spec_spread = 1; o.spec_prior_from = 2; o.spec_sort = 1;
+    o.spec_alt_seg = 0; o.spec_alt_every = 0; o.spec_spread = 1; o.spec_prior_from = 2; o.spec_sort = 1;
     o.spec_solo = 4096; o.spec_validate = 1; o.spec_max_gb = 96.0;
     return o;
 }
@@ -49,7 +49,7 @@ bool options_ok(const rt_options *o) {
            o->rounds_seq >= 0 && o->rounds_seq <= 14 && o->rounds_spec >= 0 && o->rounds_spec <= 14 &&
            o->park_min >= -1 && o->spec_iters >= 0 && o->spec_probe >= 1 && o->spec_heavy >= -1 &&
            o->spec_rounds >= 0 && o->spec_tail_rounds >= 0 && o->spec_tail_budget >= 1 && o->spec_scan >= 0 &&
-           o->spec_alt_cap >= 1024 && o->spec_alt_cap <= (1 << 24) && o->spec_alt_seg >= 1 && o->spec_alt_every >= 0 &&
+           o->spec_alt_cap >= 1024 && o->spec_alt_cap <= (1 << 24) && o->spec_alt_seg >= 0 && o->spec_alt_every >= 0 &&
            o->spec_prior_from >= 1 && o->spec_solo >= 0 && o->spec_max_gb > 0.0;
 }
 rt_options g_opt = default_options();
@@ -733,6 +733,14 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const int rounds = o.rounds_spec;
     const int iters = o.spec_iters;
     const int groups = 1;  // one pipeline (per-group streams measured slower: 8.8 s with 4 groups)
+    // A render of at most half the frame (one rank's tiles of a partition) has less parallel work
+    // per sample chain, and its time becomes the longest dependent chain of its heaviest pixel
+    // (north star): the automatic settings then spend more on the long samples,
+    // twice the heavy-first indices and alternative runs from 2048 segments on (north-star 8-way
+    // shares 5.87x -> 6.09x; whole frames keep (S - 1) / 20 and 16384: C2 +2.3% otherwise).
+    const bool partial = uint64_t(P) * 2u <= uint64_t((f.W + 7) / 8 * 8) * uint64_t((f.H + 7) / 8 * 8);
+    const int heavy_auto = int(S - 1) / (partial ? 10 : 20);
+    const int alt_seg = o.spec_alt_seg > 0 ? o.spec_alt_seg : (partial ? 2048 : 16384);
     const size_t gmax = size_t(P + groups - 1) / groups + 1;  // pixels in the largest group
     if ((rc = ensure_cont(s)) != RT_OK) return rc;
     if ((rc = ensure_lanes(s, groups, rtk::sort_pairs_temp_bytes(gmax * S, 24))) != RT_OK) return rc;
@@ -743,7 +751,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                           s->sp_front.as<uint4>(), s->sp_sorder.as<uint32_t>(),
                           uint32_t(o.spec_probe),
                           S > 2 && groups == 1 ? uint32_t(std::min(int(S) - 2, o.spec_heavy >= 0 ? o.spec_heavy
-                                                                                                : int(S - 1) / 20))
+                                                                                                : heavy_auto))
                                                : 0u};
     s->launch_seq = 0;
 #ifdef RT_DIAG
@@ -778,7 +786,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         R.alt_count = s->sp_alt_count.as<unsigned>();
         R.alt_cap = cap;
         R.alt_hcap = cap * 2;
-        R.alt_min_seg = uint32_t(o.spec_alt_seg);
+        R.alt_min_seg = uint32_t(alt_seg);
         for (int v = 0; v < 8; v++) R.alt_vals[v] = s->alt_vals[v];
         R.n_alt_vals = s->n_alt_vals;
     }
