@@ -293,9 +293,13 @@ def main():
     lib = R.load()
     if args.opt:
         o = R.get_options()
+        fields = dict(R.RtOptions._fields_)
         for kv in args.opt:
-            k, v = kv.split("=", 1)
-            setattr(o, k, type(getattr(o, k))(float(v)) if k == "spec_max_gb" else int(v))
+            k, sep, v = kv.partition("=")
+            if not sep or k not in fields or k == "size":  # a ctypes Structure would accept any name
+                raise SystemExit(f"--opt {kv!r}: not FIELD=VALUE with an rt_options field "
+                                 f"({', '.join(f for f in fields if f != 'size')})")
+            setattr(o, k, float(v) if k == "spec_max_gb" else int(v))
         R.set_options(o)
     over = {}
     if args.spp:
@@ -374,14 +378,18 @@ def main():
         if rb_on[0]:
             rb_ms[:5] += [(t1 - t0) * 1e3, tm[0], tm[1], tm[2], tm[3]]
 
-    def step(i=None):
+    def step(i=None, evp=None):
+        """One frame; `i`: timed step i (events ev[i]); `evp`: an event pair around the render alone
+        (the --balance-time warm-up frame: the gather below would make every rank wait for the slowest)."""
         mine, d_tiles, packed, depth = buf["mine"], buf["d_tiles"], buf["packed"], buf["depth"]
         gathered = buf["gathered"]
         stream = torch.cuda.current_stream()
         if args.rebuild:
             rebuild()
-        if i is not None:
-            ev[i][0].record(stream)
+        if evp is None and i is not None:
+            evp = ev[i]
+        if evp is not None:
+            evp[0].record(stream)
         if mine:
             rc = lib.rt_render_tiles_async(scene, C.byref(sc.camera), C.byref(sc.params), d_tiles.data_ptr(),
                                            len(mine), T, packed.data_ptr(),
@@ -389,8 +397,8 @@ def main():
                                            stream.cuda_stream)
             if rc != 0:
                 raise RuntimeError(f"rt_render_tiles_async -> {rc}")
-        if i is not None:
-            ev[i][1].record(stream)
+        if evp is not None:
+            evp[1].record(stream)
         if world > 1 and not host_coll:  # the one exchange step: RCCL gather of the packed tiles to rank 0
             dist.gather(packed, gathered, dst=0)
         elif world > 1:
@@ -442,18 +450,16 @@ def main():
     if balance and costs is None:
         lib.rt_debug_pixel_rays(buf["px_rays"].data_ptr())
     wt = 0.0
+    wev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     for w in range(args.warmup):
         if (balance and costs is None or tbal) and w == args.warmup - 1:
             buf["px_rays"].zero_()
-        if tbal and w == args.warmup - 1:
-            torch.cuda.synchronize()
-            tw = time.perf_counter()
-            step()
-            torch.cuda.synchronize()
-            wt = time.perf_counter() - tw
-        else:
-            step()
+        # --balance-time: this rank's own render time of the last warm-up frame (HIP events on the
+        # render stream, before the gather, which would make every rank wait for the slowest)
+        step(evp=wev if tbal and w == args.warmup - 1 else None)
     barrier()
+    if tbal:
+        wt = wev[0].elapsed_time(wev[1]) * 1e-3
     if tbal:  # refine the hashed deal by the last warm-up frame's rank times
         tcosts = tile_costs()
         lib.rt_debug_pixel_rays(None)

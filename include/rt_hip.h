@@ -114,6 +114,9 @@ typedef struct rt_options {
                                5 staged nodes; else a global ring of that many entries per wave
                                (power of two >= 64) beside 236 staged nodes */
     int inw_ring_sm;        /* ... of the sample-major kernel */
+    int inw_stackless;      /* the reference's LBVH walks (closest hit, surrounding RI) without their stack, by
+                               the node buffer's parent links, wherever no push could drop; their top
+                               nodes staged in LDS when there is no wide walk (DESIGN.md "Stackless") */
     /* IOW-03 (In-One-Weekend 03) */
     int iow_spec;           /* sample-parallel speculation (0: the sequential per-pixel kernel) */
     int iow_linear;         /* [build] the shader's linear object loop instead of the culling BVH */
@@ -284,7 +287,9 @@ void rt_dev_scene_free(rt_dev_scene *s);
  * swept boxes rt_pack_inw writes) with rt_lbvh_build_async; lights: the layout-4 light SSBO.
  * The wide walk's structures and the RI grid are rebuilt on the host.  Synchronises the device
  * first.  timing_ms (may be NULL) receives the host time of {records, LBVH (upload + device
- * build + read-back), host structures, their upload}. */
+ * build + read-back), host structures, their upload}.  If any step fails the scene keeps its
+ * previous object count but its buffers may be partly replaced: every render of it then returns
+ * RT_E_ARG until a later update succeeds. */
 int rt_dev_scene_inw_update(rt_dev_scene *s, const float *geom, uint32_t n, const float *nodes, const float *aabbs,
                             const float *lights, uint32_t n_lights, double timing_ms[4]);
 /* Replace the scene's options (the [build] ones keep the values the scene was built with). */
@@ -306,6 +311,8 @@ typedef struct rt_path_info {
     int ring_entries;     /* fold window of the kernel that ran */
     int iow_bvh;          /* IOW-03: 0 linear loop, 1 culling BVH, 2 culling BVH in LDS */
     int ring_lds;         /* 1: the fold ring was in LDS (k_inw_pm, inw_ring_pm = 0) */
+    int stackless;        /* 1: the reference LBVH walks ran stackless where no push could drop */
+    int lbvh_lds_nodes;   /* LBVH nodes the stackless walks read from LDS (no wide walk) */
 } rt_path_info;
 int rt_debug_path(rt_dev_scene *s, rt_path_info *out);
 
@@ -320,6 +327,37 @@ int rt_render_tiles_async(rt_dev_scene *s, const rt_camera *cam, const rt_params
 /* Render the rectangle in p->tile_* into a full W*H image resident on the device. */
 int rt_render_image_async(rt_dev_scene *s, const rt_camera *cam, const rt_params *p,
                           float *d_rgba, float *d_depth, uint64_t *d_counters, void *stream);
+
+/* ---- multi-GPU partition (BASELINE configs[3]) -----------------------------
+ * One host thread drives several devices of this process: the frame's tiles are dealt
+ * across the devices, each renders its share with rt_render_tiles_async on a stream of its own,
+ * and one RCCL exchange over xGMI (grouped ncclSend / ncclRecv) brings the packed tiles to device
+ * 0, which unpacks them into the W x H image.  This generalises the reference's per-tile
+ * dispatch (In-One-Weekend/03_Shadows_and_Materials/materials.cpp:98-152) to devices, for the
+ * host that replaces RT_Base<>::OnUpdateBase (In-Next-Week/base.h:148-173).
+ *
+ * rt_tile_deal: the frame's ceil(W/T) x ceil(H/T) tiles in deal order as (tx, ty) int pairs,
+ * row-major for one device, else row-major permuted by the multiplicative hash
+ * i * 2654435761 mod 2^32 (ties by i); entry k goes to device k % n_dev.  Writes up to cap pairs
+ * to order_out (may be NULL) and returns the tile count. */
+int rt_tile_deal(int width, int height, int tile_size, int n_dev, int *order_out, int cap);
+/* A group of distinct devices with one RCCL communicator each (ncclCommInitAll) and a stream per
+ * device.  NULL when a device is missing, not gfx950, repeated, or RCCL fails. */
+typedef struct rt_group rt_group;
+rt_group *rt_group_create(const int *devices, int n_dev);
+void rt_group_free(rt_group *g);   /* synchronises the group's devices first */
+/* Render the whole frame p->width x p->height (p->tile_* ignored) of scenes[r] (one device scene
+ * per group device r, built from the same records and spp) in tile_size^2 tiles (a multiple of
+ * 16) dealt by rt_tile_deal.  d_rgba (W*H*4 floats), d_depth (W*H, may be NULL) and d_counters
+ * (6 x u64, added to; may be NULL) are device-0 pointers; stream is device 0's stream (the other
+ * devices use the group's).  The first call for a frame size allocates the group's buffers. */
+int rt_render_multi_async(rt_group *g, rt_dev_scene *const *scenes, const rt_camera *cam, const rt_params *p,
+                          int tile_size, float *d_rgba, float *d_depth, uint64_t *d_counters, void *stream);
+/* Blocking form of rt_render_inw over devices[0..n_dev): the scene replicated on every device, a
+ * group, one partitioned frame, the image copied back (st->ms: device-0 time of the render). */
+int rt_render_inw_multi(const float *geom, uint32_t n, int layout, const float *nodes, const float *lights,
+                        uint32_t n_lights, const rt_camera *cam, const rt_params *p, const int *devices, int n_dev,
+                        int tile_size, float *rgba, float *depth, rt_stats *st);
 
 /* ---- progressive display -------------------------------------------------
  * Tile order <- Adding_Materials::OnUpdate  In-One-Weekend/03_Shadows_and_Materials/materials.cpp:84-152:

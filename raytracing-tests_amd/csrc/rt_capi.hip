@@ -31,7 +31,7 @@ rt_options default_options() {
     std::memset(&o, 0, sizeof(o));
     o.size = sizeof(rt_options);
     o.inw_wide_walk = 1; o.inw_order = 0; o.inw_beams = 1; o.inw_ri_grid = 1; o.inw_lds_nodes = 1;
-    o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 0; o.inw_ring_sm = 256;
+    o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 0; o.inw_ring_sm = 256; o.inw_stackless = 1;
     o.iow_spec = 1; o.iow_linear = 0; o.iow_narrow = 0; o.iow_lds_bvh = 1;
     o.iow_leaf_batch = 32;  // 32 measured 2.5% faster on the bench frame than 65 (round 2)
     o.iow_coop_max = 4; o.iow_chunks_lpt = 0;
@@ -178,9 +178,11 @@ struct rt_dev_scene {
     char kname[64] = {0};         // the fold kernel's instance name (rt_debug_launches)
     uint32_t last_ring[2] = {0, 0};  // ... its fold windows (pixel-major, sample-major)
     uint32_t ring_frame = 0;         // frames rendered with the current fold rings (their tag epoch)
+    bool broken = false;             // a failed rt_dev_scene_inw_update left the buffers inconsistent: no renders
     rt_path_info last_path{};     // rt_debug_path: what the last render ran
     float wbound = 0.0f;          // largest |coordinate| of the INW culling boxes (the fused cull's condition)
-    uint32_t dfs_high = 0;
+    uint32_t dfs_high = 0;        // the reference walk's stack high-water mark (0: no walkable LBVH)
+    bool sl_ok = false;           // the node buffer has the stackless walks' layout (lbvh_walk_info)
     uint32_t n_tex = 0;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
     uint32_t ws_units = 0;
@@ -338,6 +340,9 @@ int upload_textures(rt_dev_scene *s, const rt_texture *tex, int n_tex);
 // stack high-water mark, and the kernels use the wide walk only while size + dfs_high <= 40.
 void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     if (!s->dfs_high) return;
+    sc.dfs_high = s->dfs_high;
+    sc.sl = s->sl_ok && s->opt.inw_stackless ? 1u : 0u;  // stackless LBVH walks (rt_options.inw_stackless)
+    if (!s->n_wnodes) return;  // no wide walk
     sc.wnodes = s->wnodes.as<float4>();
     sc.wroot = 1;
     sc.rank = s->wrank.as<uint32_t>();
@@ -358,17 +363,24 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
 // ms (may be null): host time of the builds, then of the uploads
 int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n, double *ms = nullptr) {
     s->dfs_high = 0;
+    s->sl_ok = false;
+    s->n_wnodes = 0;
     s->ri_ok = false;
     const auto t0 = std::chrono::steady_clock::now();
+    uint32_t high = 0;
+    bool sl = false;
+    const bool walkable = rtamd::lbvh_walk_info(nodes, n, high, sl);
     rtamd::InwWide w;
     rtamd::RiGrid g;
-    const bool ok = s->opt.inw_wide_walk && rtamd::inw_wide_build(nodes, n, w);
+    const bool ok = walkable && s->opt.inw_wide_walk && rtamd::inw_wide_build(nodes, n, w);
     if (ok) g = rtamd::ri_grid_build(w.leafbox.data(), n);
     const auto t1 = std::chrono::steady_clock::now();
     if (ms) ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    if (!ok) return RT_OK;
+    if (!ok) {  // the reference walk only (stackless where it cannot drop a push)
+        if (walkable) { s->dfs_high = high; s->sl_ok = sl; }
+        return RT_OK;
+    }
     HIP_OK(s->wnodes.store(w.wnodes.data(), w.wnodes.size() * sizeof(float)));
-    s->n_wnodes = uint32_t(w.wnodes.size() / 40);
     HIP_OK(s->wrank.store(w.rank.data(), w.rank.size() * sizeof(uint32_t)));
     HIP_OK(s->wleaf.store(w.leafbox.data(), w.leafbox.size() * sizeof(float)));
     if (g.ok) {
@@ -379,7 +391,9 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n, double *ms = 
             s->ri_lo[a] = g.lo[a]; s->ri_hi[a] = g.hi[a]; s->ri_inv[a] = g.inv[a]; s->ri_dim[a] = g.dim[a];
         }
     }
+    s->n_wnodes = uint32_t(w.wnodes.size() / 40);
     s->dfs_high = w.dfs_high;
+    s->sl_ok = sl;
     s->wdepth = w.depth;
     s->wbound = w.wbound;
     if (ms) ms[1] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
@@ -445,18 +459,21 @@ int update_inw(rt_dev_scene *s, const float *geom, uint32_t n, const float *node
         if (ms) ms[k] = std::chrono::duration<double, std::milli>(now - t).count();
         t = now;
     };
+    if (n > (1u << 24)) return RT_E_UNSUPPORTED;  // node / object ids are stored as floats (exact to 2^24)
+    // Until every step below has succeeded the buffers may hold a mix of the old and the new
+    // scene (sizes included): the scene refuses renders (launch_scene) and keeps its old n and
+    // counts, so nothing indexes past a buffer.  The new sizes are committed at the end.
+    s->broken = true;
     std::vector<float> hot, cold;
     inw_records(geom, n, s->layout, hot, cold);
-    s->n = n;
-    s->n_lights = s->layout == 4 ? n_lights : 0;
+    const uint32_t nl = s->layout == 4 ? n_lights : 0;
     HIP_OK(s->hot.store(hot.data(), hot.size() * sizeof(float)));
     HIP_OK(s->cold.store(cold.data(), cold.size() * sizeof(float)));
-    if (s->n_lights) HIP_OK(s->lights.store(lights, size_t(s->n_lights) * 7 * sizeof(float)));
+    if (nl) HIP_OK(s->lights.store(lights, size_t(nl) * 7 * sizeof(float)));
     lap(0);
     const size_t nbytes = size_t(2 * n - 1) * 8 * sizeof(float);
     std::vector<float> host_nodes;
     if (!nodes) {  // ConstructLBVH_Buff on the device (rt_lbvh_build_async), read back for the host builders
-        if (n > (1u << 24)) return RT_E_UNSUPPORTED;
         if (s->nodes.bytes < nbytes) {
             s->nodes.~DevBuf();
             new (&s->nodes) DevBuf();
@@ -477,6 +494,9 @@ int update_inw(rt_dev_scene *s, const float *geom, uint32_t n, const float *node
     double w[2] = {0.0, 0.0};
     if (int rc = make_inw_wide(s, nodes, n, w); rc != RT_OK) return rc;
     if (ms) { ms[2] = w[0]; ms[3] = w[1]; }
+    s->n = n;
+    s->n_lights = nl;
+    s->broken = false;
     return RT_OK;
 }
 
@@ -601,6 +621,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st);
 int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st);
 
 int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
+    if (s->broken) return RT_E_ARG;  // a failed rt_dev_scene_inw_update (update_inw)
     f.n_focus = (s->kind != 3 && s->layout == 1) ? s->n_focus : 0;
     std::memcpy(f.focus_list, s->focus, sizeof(f.focus_list));
     f.leaf_batch = s->opt.iow_leaf_batch;
@@ -618,7 +639,8 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     s->last_kernel = s->kind == 3 ? (rtk::iow_narrow(f) ? "k_iow03n" : "k_iow03") : (s->layout == 4 ? "k_inw<true>" : "k_inw<false>");
     s->last_launches = int(plan.size()) * (1 + s->opt.rounds_seq);
     s->last_path.order = s->kind == 3 ? 5 : 3;
-    s->last_path.wide_walk = s->kind != 3 && s->dfs_high != 0;
+    s->last_path.wide_walk = s->kind != 3 && s->n_wnodes != 0;
+    s->last_path.stackless = s->kind != 3 && s->dfs_high != 0 && s->sl_ok && s->opt.inw_stackless;
     s->last_chunks = int(plan.size());
     if (plan.size() > 1) {
         int rc = ensure_workspace(s, units);
@@ -1113,7 +1135,8 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const int blocks = s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 16 : 15);
     // the top of the wide BVH staged in LDS (768-lane blocks, 3 waves per SIMD);
     // inw_lds_nodes = 0: 256-lane blocks reading every node from L1 / L2 (A/B)
-    const int blocks_ln = o.inw_lds_nodes && s->dfs_high
+    // (without the wide walk the stackless LBVH walks read the top of the LBVH from that LDS)
+    const int blocks_ln = o.inw_lds_nodes && (s->n_wnodes || (s->dfs_high && s->sl_ok && o.inw_stackless))
                               ? s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 18 : 17) : 0;
     // inw_ring_pm = 0: k_inw_pm's fold ring in LDS (768-lane blocks), else a global
     // ring of that many entries per wave (1024 for the 256-lane blocks)
@@ -1128,9 +1151,11 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         if (s->inw_ring.alloc(ring_bytes) != hipSuccess) return RT_E_HIP;
         s->ring_frame = 0;  // fresh memory: clear it before the first frame
     }
-    // ring tags carry the frame's epoch (rtk::ring_tag); the rings are cleared only when it wraps
+    // ring tags carry the frame's epoch (rtk::ring_tag); the rings are cleared only when it wraps.
+    // ring_frame advances only once this frame's clear (epoch 0) is enqueued, and any failure
+    // below resets it, so the next frame clears the rings before it uses them
     const uint32_t epoch = s->ring_frame % 63u;
-    s->ring_frame++;
+    s->ring_frame = 0;
     rtk::InwScene sc{s->hot.as<float4>(), s->cold.as<float4>(), s->nodes.as<float4>(),
                      s->lights.as<float>(), s->n, s->n_lights, s->layout, s->sunflower.as<float>(),
                      s->tex.as<float4>(), s->tex_info.as<int4>(), s->n_tex};
@@ -1202,15 +1227,21 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         P.ri_grid = sc.ri_cells != nullptr;
         P.fused_cull = s->last_fu ? 1 : 0;
         P.lds_nodes = s->last_ln ? int(std::min<uint32_t>(s->n_wnodes, uint32_t(rtk::kInwLdsNodes))) : 0;
+        P.stackless = sc.sl ? 1 : 0;
+        // the LBVH nodes the stackless walks read from LDS (LN kernels without the wide walk)
+        P.lbvh_lds_nodes = s->last_ln && sc.sl && !sc.wnodes
+                               ? int(std::min<uint32_t>(2 * s->n - 1, uint32_t(rtk::kInwLdsNodes * 10 / 2))) : 0;
         P.claim_order = cost != nullptr;
     }
     if (epoch == 0) e = hipMemsetAsync(s->inw_ring.p, 0xff, s->inw_ring.bytes, st);
+    if (e == hipSuccess) s->ring_frame = epoch + 1;
     if (e == hipSuccess && ev) e = hipEventRecord(ev->first, st);
     if (e == hipSuccess)
         e = rtk::launch_inw_fold(f, sc, s->inw_ring.as<float4>(), ring_pm, ring_sm, s->counter.as<unsigned>(),
                                  s->inw_mode.as<uint32_t>(), force, blocks, blocks_ln, cost, st);
     if (e == hipSuccess && ev) e = hipEventRecord(ev->second, st);
     if (e != hipSuccess) {
+        s->ring_frame = 0;
         std::fprintf(stderr, "[rt_hip] launch failed: %s\n", hipGetErrorString(e));
         return RT_E_HIP;
     }
@@ -1366,7 +1397,12 @@ int rt_dev_scene_inw_update(rt_dev_scene *s, const float *geom, uint32_t n, cons
     if (s->n_tex == 0 && inw_textured(geom, n, s->layout)) return RT_E_UNSUPPORTED;
     HIP_OK(hipSetDevice(s->device));
     HIP_OK(hipDeviceSynchronize());  // the scene's last frame may still read the buffers being replaced
-    return update_inw(s, geom, n, nodes, aabbs, lights, n_lights, timing_ms);
+    try {  // the host builders allocate: no exception crosses the ABI
+        return update_inw(s, geom, n, nodes, aabbs, lights, n_lights, timing_ms);
+    } catch (...) {
+        s->broken = true;
+        return RT_E_ARG;
+    }
 }
 
 int rt_dev_scene_set_options(rt_dev_scene *s, const rt_options *o) {
@@ -1391,6 +1427,7 @@ int rt_debug_path(rt_dev_scene *s, rt_path_info *out) {
         P.ring_entries = int(s->last_ring[0]);
         P.ring_lds = s->last_lring ? 1 : 0;
         if (s->last_lring) P.lds_nodes = std::min(P.lds_nodes, int(rtk::kPmLdsNodes));
+        if (s->last_lring) P.lbvh_lds_nodes = std::min(P.lbvh_lds_nodes, int(rtk::kPmLdsNodes * 10 / 2));
     }
     else if (std::strncmp(name, "k_inw_sm", 8) == 0) { P.order = 2; P.ring_entries = int(s->last_ring[1]); }
     if (P.order != 1) { P.beams = 0; P.claim_order = 0; }  // both serve the pixel-major kernel only

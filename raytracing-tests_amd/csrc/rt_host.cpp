@@ -807,6 +807,44 @@ bool inw_wide_build(const float *nodes, uint32_t n, InwWide &out) {
     return true;
 }
 
+bool lbvh_walk_info(const float *nodes, uint32_t n, uint32_t &high, bool &stackless) {
+    high = 0;
+    stackless = false;
+    if (n == 0 || n > (1u << 24)) return false;
+    const uint32_t nn = 2 * n - 1;
+    bool lay = true;
+    for (uint32_t i = 0; i < nn && lay; i++) {
+        const float left = nodes[size_t(i) * 8 + 6];
+        if (left > 0.1f) {
+            const uint32_t L = uint32_t(left);
+            lay = float(L) == left && (L & 1u) && L + 1 < nn && nodes[size_t(L) * 8 + 7] == float(i) &&
+                  nodes[size_t(L + 1) * 8 + 7] == float(i);
+        } else {
+            lay = -left >= 0.0f && -left < float(n) && float(uint32_t(-left)) == -left;
+        }
+    }
+    for (int inv = 0; inv < 2; inv++) {  // 01_BVH...glsl:456-460 push order
+        std::vector<uint32_t> st{0};
+        uint32_t pops = 0;
+        high = std::max<uint32_t>(high, 1);
+        while (!st.empty()) {
+            const uint32_t i = st.back();
+            st.pop_back();
+            if (++pops > nn) return false;  // a cycle: not a tree
+            const float left = nodes[size_t(i) * 8 + 6];
+            if (left > 0.1f) {
+                const uint32_t l = uint32_t(left), r = l + 1;
+                if (r >= nn) return false;
+                st.push_back(inv ? r : l);
+                st.push_back(inv ? l : r);
+                high = std::max<uint32_t>(high, uint32_t(st.size()));
+            }
+        }
+    }
+    stackless = lay;
+    return true;
+}
+
 RiGrid ri_grid_build(const float *lbox, uint32_t n) {
     RiGrid G;
     double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
@@ -866,6 +904,21 @@ RiGrid ri_grid_build(const float *lbox, uint32_t n) {
     G.ids = std::move(ids);
     G.ok = true;
     return G;
+}
+
+std::vector<std::pair<int, int>> tile_deal(int W, int H, int T, int n_dev) {
+    const int nx = (W + T - 1) / T, ny = (H + T - 1) / T;
+    std::vector<uint32_t> idx(size_t(nx) * size_t(ny));
+    for (size_t i = 0; i < idx.size(); i++) idx[i] = uint32_t(i);
+    if (n_dev > 1)  // key (i * 2654435761 mod 2^32, i): Knuth's multiplicative hash, ties by index
+        std::sort(idx.begin(), idx.end(), [](uint32_t a, uint32_t b) {
+            const uint32_t ha = a * 2654435761u, hb = b * 2654435761u;
+            return ha < hb || (ha == hb && a < b);
+        });
+    std::vector<std::pair<int, int>> out;
+    out.reserve(idx.size());
+    for (uint32_t i : idx) out.push_back({int(i % uint32_t(nx)), int(i / uint32_t(nx))});
+    return out;
 }
 
 }  // namespace rtamd

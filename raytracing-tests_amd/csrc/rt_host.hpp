@@ -132,6 +132,11 @@ struct InwWide {
     std::vector<float> leafbox;    // 8n: object g's LBVH leaf node
 };
 bool inw_wide_build(const float *nodes, uint32_t n, InwWide &out);
+// The reference walk's stack high-water mark over both child orders (high; its pushes can only
+// drop while size + high > 40) and whether the node buffer has the layout the stackless LBVH walks
+// rely on (stackless: every internal node's children at L (odd), L + 1 with rightData = the node,
+// leaf ids < n; lbvh.h:236-269 writes it so).  false: not a walkable LBVH (no shortcut applies).
+bool lbvh_walk_info(const float *nodes, uint32_t n, uint32_t &high, bool &stackless);
 
 // The surrounding-RI grid (DESIGN.md §5 "RI grid") over the leaf boxes: about two cells per
 // object, every object entered in each cell its leaf box overlaps once widened by a thousandth of
@@ -158,5 +163,12 @@ std::vector<SpiralTile> tile_spiral(int W, int H, int tw, int th);
 // ---- presets ----------------------------------------------------------------------------
 int scene_preset(int preset, uint32_t seed, int n_hint, std::vector<rt_geom_desc> &out,
                  rt_cam_desc &cam, rt_params &params);
+
+// The tile deal of the multi-GPU partition: the frame's ceil(W/T) x ceil(H/T) tiles
+// in row-major order, permuted for n_dev > 1 by a multiplicative hash of their index (a plain
+// round robin over rows hands a rank whole tile columns when the row length is a multiple of
+// n_dev, and a glass sphere's columns to a few ranks); entry k goes to device k % n_dev.
+// bench.py deal_order is the same function.
+std::vector<std::pair<int, int>> tile_deal(int W, int H, int T, int n_dev);
 
 }  // namespace rtamd

@@ -2248,6 +2248,126 @@ __device__ float inw_ri_grid(const InwScene &S, f3 hp, float ratio, Ctr &c, bool
     return acc;
 }
 
+// ---------------------------------------------------------------- stackless LBVH walks
+// The reference walks its LBVH depth first with the shared 40-float stack (01_BVH...glsl:431-476;
+// RI: 486-502, 272-345).  Its node buffer is written breadth first with the two children of a node
+// next to each other and rightData = the parent (lbvh.h:236-269), so the left children sit at odd
+// indices and their right siblings at the next one; the host checks that layout (InwScene::sl).
+// The same depth-first order then needs no stack: the closest-hit walk pops (invert ? left :
+// right) first (it pushes the other one first, :456-460), so after the first child's subtree
+// comes its sibling, and after the second child's subtree the walk climbs to the parent and on.
+// Every node the reference pops is visited once, in the same order, with the same running limit:
+// the same box tests, leaves, hit, node and primitive counts.  Where a reference push could drop
+// (size + dfs_high > 40) the result depends on the stack, and the caller runs the stack walk.
+// Climbing past a second child reads one float, the parent's own parent link.
+template <bool LN>
+__device__ __forceinline__ void lbvh_node(const InwScene &S, uint32_t i, float4 &n0, float4 &n1) {
+    if (LN && i < S.n_blds) {  // LDS-staged top of the LBVH (ds_read_b128)
+        n0 = g_inw_lnodes[2 * i];
+        n1 = g_inw_lnodes[2 * i + 1];
+        return;
+    }
+    n0 = S.nodes[2 * i];
+    n1 = S.nodes[2 * i + 1];
+}
+template <bool LN>
+__device__ __forceinline__ float lbvh_parent(const InwScene &S, uint32_t i) {
+    if (LN && i < S.n_blds) return g_inw_lnodes[2 * i + 1].w;
+    return reinterpret_cast<const float *>(S.nodes)[8 * (size_t)i + 7];
+}
+// The node after the subtree of `cur` in depth-first order (0 = the walk is over).  first_odd:
+// the first-visited child of a node has an odd index (invert) or an even one.  par: cur's parent.
+template <bool LN>
+__device__ __forceinline__ uint32_t lbvh_next(const InwScene &S, uint32_t cur, float par, uint32_t first_odd) {
+    for (;;) {
+        if (cur == 0u) return 0u;
+        if ((cur & 1u) == first_odd) return first_odd ? cur + 1u : cur - 1u;  // its sibling comes next
+        cur = (uint32_t)par;  // a second child: its parent's subtree is done
+        if (cur == 0u) return 0u;
+        par = lbvh_parent<LN>(S, cur);
+    }
+}
+
+template <bool WANT_NORMAL, bool LN = false>
+__device__ float inw_traverse_sl(const InwScene &S, f3 o, f3 d, float ratio, bool invert, float &tlim, f3 &normal,
+                                 float &extra, float init_geom, Ctr &c) {
+    float final_geom = init_geom;
+    const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};
+    const uint32_t first_odd = invert ? 1u : 0u;
+    uint32_t cur = 0u;
+    for (;;) {
+        float4 n0, n1;
+        lbvh_node<LN>(S, cur, n0, n1);
+        c.nodes++;
+        if (test_aabb(n0, n1, o, id, tlim)) {
+            const float left = n1.z;
+            if (left > 0.1f) {  // descend: the child the reference pops first
+                const uint32_t L = (uint32_t)left;
+                cur = invert ? L : L + 1u;
+                continue;
+            }
+            c.prims++;  // IntersectRay / IntersectRayMinimal (as inw_traverse)
+            const float geom = -left;
+            const Xf x = load_xf(S, (int)geom);
+            f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+            f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+            float t = -1.0f;
+            if (x.type == 1) t = t_ellipsoid(to, td, x.is);
+            else if (x.type == 2) t = t_cuboid(to, td, x.scale);
+            if (t > 0.0f && t < tlim) {
+                tlim = t;
+                final_geom = geom;
+                if (WANT_NORMAL) {
+                    f3 h = to + td * t, nl;
+                    if (x.type == 1) nl = normalize(f3{h.x * x.is2.x, h.y * x.is2.y, h.z * x.is2.z});
+                    else if (x.type == 2) nl = cuboid_normal(h, x.scale);
+                    else nl = f3{0, 0, 0};
+                    normal = mul(x.R, nl);
+                    extra = x.extra;
+                }
+            }
+        }
+        cur = lbvh_next<LN>(S, cur, n1.w, first_odd);
+        if (cur == 0u) break;
+    }
+    return final_geom;
+}
+
+// the surrounding-RI point walk (01_BVH...glsl:486-502): pushes left, then left + 1, so it pops
+// the right (even) child first
+template <bool LN = false>
+__device__ float inw_surrounding_ri_sl(const InwScene &S, f3 hp, float ratio, Ctr &c) {
+    float acc = 0.0f;
+    uint32_t cnt = 0, cur = 0u;
+    for (;;) {
+        float4 n0, n1;
+        lbvh_node<LN>(S, cur, n0, n1);
+        c.nodes++;
+        if (hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z) {
+            const float left = n1.z;
+            if (!(left < 0.1f)) {
+                cur = (uint32_t)left + 1u;
+                continue;
+            }
+            c.prims++;
+            const Xf x = load_xf(S, (int)(-left));
+            f3 v = (hp - x.pos) + x.delta * (1.0f - ratio);
+            v = tmul(x.R, v);
+            v.x *= x.is.x; v.y *= x.is.y; v.z *= x.is.z;
+            bool inside;
+            if (x.type == 1) inside = dot(v, v) <= 1.0f;
+            else if (x.type == 2) inside = fabsf(v.x) <= 0.5f && fabsf(v.y) <= 0.5f && fabsf(v.z) <= 0.5f;
+            else inside = false;
+            if (inside) { acc += x.ri_acc; cnt++; }
+        }
+        cur = lbvh_next<LN>(S, cur, n1.w, 0u);
+        if (cur == 0u) break;
+    }
+    if (acc > 1.0f) acc *= rcp((float)cnt);
+    else acc = 1.0f;
+    return acc;
+}
+
 template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false>
 __device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
                                              float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c,
@@ -2258,6 +2378,8 @@ __device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o,
     if (PK && wp->parked) return g;
     OCC_TALLY(c, kOccRef, !ok);
     if (ok) return g;
+    if (S.sl && K.size + S.dfs_high <= (uint32_t)kFStack)  // no push of the reference walk could drop
+        return inw_traverse_sl<WANT_NORMAL, LN>(S, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
     return inw_traverse<WANT_NORMAL>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
 }
 template <bool LN = false>
@@ -2269,6 +2391,7 @@ __device__ __forceinline__ float inw_ri(const InwScene &S, FStack &K, f3 hp, flo
     }
     const float r = inw_surrounding_ri_wide<LN>(S, K, hp, ratio, c, ok);
     if (ok) return r;
+    if (S.sl && K.size + S.dfs_high <= (uint32_t)kFStack) return inw_surrounding_ri_sl<LN>(S, hp, ratio, c);
     return inw_surrounding_ri(S, K, hp, ratio, c);
 }
 
@@ -2867,8 +2990,12 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         const uint32_t cap = LR ? (uint32_t)kPmLdsNodes : (uint32_t)kInwLdsNodes;
         const uint32_t n = S.wnodes ? (S.n_wnodes < cap ? S.n_wnodes : cap) : 0u;
         for (uint32_t i = threadIdx.x; i < n * (uint32_t)kInwNodeF4; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
+        // no wide walk: the stackless LBVH walks read the top of the LBVH (2 float4 per node) there
+        const uint32_t nb = (!S.wnodes && S.sl) ? min(2u * S.n - 1u, cap * (uint32_t)kInwNodeF4 / 2u) : 0u;
+        for (uint32_t i = threadIdx.x; i < 2u * nb; i += SUB * kBlock) g_inw_lnodes[i] = S.nodes[i];
         __syncthreads();
         S.n_lnodes = n;
+        S.n_blds = nb;
     }
     Ctr c;
 #ifdef RT_DIAG_SPLIT
@@ -3114,8 +3241,11 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     if constexpr (LN) {
         const uint32_t n = S.wnodes ? (S.n_wnodes < (uint32_t)kInwLdsNodes ? S.n_wnodes : (uint32_t)kInwLdsNodes) : 0u;
         for (uint32_t i = threadIdx.x; i < n * (uint32_t)kInwNodeF4; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
+        const uint32_t nb = (!S.wnodes && S.sl) ? min(2u * S.n - 1u, (uint32_t)(kInwLdsNodes * kInwNodeF4 / 2)) : 0u;
+        for (uint32_t i = threadIdx.x; i < 2u * nb; i += SUB * kBlock) g_inw_lnodes[i] = S.nodes[i];
         __syncthreads();
         S.n_lnodes = n;
+        S.n_blds = nb;
     }
     Ctr c;
     FStack K{lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock), 0};

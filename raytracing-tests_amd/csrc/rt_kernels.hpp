@@ -82,6 +82,12 @@ struct InwScene {
     uint32_t dfs_high = 0;
     uint32_t n_wnodes = 0;  // wide nodes
     uint32_t n_lnodes = 0;  // the first n_lnodes wide nodes are staged in LDS (LN kernels only)
+    // Stackless LBVH walks (rt_options.inw_stackless; DESIGN.md §5 "Stackless LBVH
+    // walk"): the reference's depth-first walks without their stack, by parent links, wherever no
+    // push of the reference walk could drop (size + dfs_high <= 40).  sl = 0: off (or the node
+    // buffer lacks the layout: left children at odd indices, right = left + 1, rightData = parent)
+    uint32_t sl = 0;
+    uint32_t n_blds = 0;    // LN kernels without the wide walk: the first n_blds LBVH nodes staged in LDS
     int fused = 0;          // the wide walk culls with one fma per plane (cull4nf<true>; set per frame)
     uint32_t lring = 0;       // k_inw_pm (768-lane instances): the fold ring in LDS (kPmLdsRing entries per wave)
     uint32_t ring_epoch = 0;  // fold-ring tags: the frame's epoch (0..62) << 26 (ring_tag, rt_kernels.hip)

@@ -74,7 +74,7 @@ class RtOptions(C.Structure):
     """rt_options (include/rt_hip.h): the exact strategy switches of the render path."""
     _fields_ = [("size", C.c_uint32)] + [(n, C.c_int) for n in (
         "inw_wide_walk", "inw_order", "inw_beams", "inw_ri_grid", "inw_lds_nodes", "inw_fused_cull",
-        "inw_claim_order", "inw_ring_pm", "inw_ring_sm",
+        "inw_claim_order", "inw_ring_pm", "inw_ring_sm", "inw_stackless",
         "iow_spec", "iow_linear", "iow_narrow", "iow_lds_bvh", "iow_leaf_batch", "iow_coop_max", "iow_chunks_lpt",
         "rounds_seq", "rounds_spec", "park_min",
         "spec_iters", "spec_probe", "spec_heavy", "spec_rounds", "spec_tail_rounds", "spec_tail_budget", "spec_scan",
@@ -90,7 +90,7 @@ class RtPathInfo(C.Structure):
     _fields_ = [("kernel", C.c_char * 64), ("launches", C.c_int), ("order", C.c_int), ("order_forced", C.c_int),
                 ("wide_walk", C.c_int), ("beams", C.c_int), ("ri_grid", C.c_int), ("fused_cull", C.c_int),
                 ("lds_nodes", C.c_int), ("claim_order", C.c_int), ("ring_entries", C.c_int), ("iow_bvh", C.c_int),
-                ("ring_lds", C.c_int)]
+                ("ring_lds", C.c_int), ("stackless", C.c_int), ("lbvh_lds_nodes", C.c_int)]
 
     ORDERS = {0: None, 1: "pixel-major", 2: "sample-major", 3: "per-pixel", 4: "sample-parallel", 5: "sequential"}
 
@@ -180,6 +180,13 @@ SIGNATURES = {
     "rt_dev_scene_inw_update": (C.c_int, [C.c_void_p, _FP, C.c_uint32, _FP, _FP, _FP, C.c_uint32,
                                           C.POINTER(C.c_double)]),
     "rt_debug_path": (C.c_int, [C.c_void_p, C.POINTER(RtPathInfo)]),
+    "rt_tile_deal": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _IP, C.c_int]),
+    "rt_group_create": (C.c_void_p, [_IP, C.c_int]),
+    "rt_group_free": (None, [C.c_void_p]),
+    "rt_render_multi_async": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(RtCamera), C.POINTER(RtParams), C.c_int,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_render_inw_multi": (C.c_int, [_FP, C.c_uint32, C.c_int, _FP, _FP, C.c_uint32, C.POINTER(RtCamera),
+                                      C.POINTER(RtParams), _IP, C.c_int, C.c_int, _FP, _FP, C.POINTER(RtStats)]),
 }
 
 _lib = None
@@ -388,6 +395,32 @@ def tile_spiral(width: int, height: int, tile_w: int = 100, tile_h: int = 100) -
     out = np.zeros((max(n, 1), 4), np.int32)
     lib.rt_tile_spiral(width, height, tile_w, tile_h, out.ctypes.data_as(_IP), n)
     return out[:n]
+
+
+def tile_deal(width: int, height: int, tile: int, n_dev: int) -> list:
+    """rt_tile_deal: the multi-GPU deal order of the frame's tiles, [(tx, ty), ...]; entry k goes to
+    device k % n_dev."""
+    lib = load()
+    n = lib.rt_tile_deal(width, height, tile, n_dev, None, 0)
+    check(min(n, 0), "rt_tile_deal")
+    out = np.zeros((max(n, 1), 2), np.int32)
+    lib.rt_tile_deal(width, height, tile, n_dev, out.ctypes.data_as(_IP), n)
+    return [tuple(int(v) for v in row) for row in out[:n]]
+
+
+def render_inw_multi(sc: "Scene", devices, params: RtParams | None = None, tile: int = 16):
+    """rt_render_inw_multi: the INW frame tile-partitioned over `devices` with the RCCL gather to
+    devices[0]; returns (rgba, depth, stats) like render()."""
+    p = params or sc.params
+    devs = (C.c_int * len(devices))(*devices)
+    rgba = np.zeros((p.height, p.width, 4), np.float32)
+    depth = np.zeros((p.height, p.width), np.float32)
+    st = RtStats()
+    lights = sc.lights if sc.lights is not None and len(sc.lights) else None
+    check(load().rt_render_inw_multi(fptr(sc.geom), sc.n, sc.layout, fptr(sc.nodes), fptr(lights), sc.n_lights,
+                                     C.byref(sc.camera), C.byref(p), devs, len(devices), tile, fptr(rgba), fptr(depth),
+                                     C.byref(st)), "rt_render_inw_multi")
+    return rgba, depth, st.as_dict()
 
 
 def lbvh_build_gpu(aabbs, device: int = -1):

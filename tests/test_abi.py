@@ -17,7 +17,7 @@ def _declared():
     for h in ("rt_hip.h", "rt_scene.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        for m in re.finditer(r"^\s*(?:int|void|size_t|rt_dev_scene\s*\*)\s*\*?\s*(rt_\w+)\s*\(", src, re.M):
+        for m in re.finditer(r"^\s*(?:int|void|size_t|rt_dev_scene\s*\*|rt_group\s*\*)\s*\*?\s*(rt_\w+)\s*\(", src, re.M):
             names.add(m.group(1))
     return names
 

@@ -85,3 +85,32 @@ def test_refine_deal_moves_cheap_tiles_off_slow_ranks():
     assert max(pred) / min(pred) < 1.05 < max(times) / min(times)  # 2.3x apart before
     # deterministic: the same inputs give the same lists on every rank
     assert bench.refine_deal(lists, costs, times, nx) == new
+    assert new != lists  # unbalanced shares: the refined deal differs from the hashed one
+
+
+def test_refine_deal_keeps_a_balanced_deal():
+    nx, ny, world = 24, 12, 4
+    costs = np.ones(nx * ny)
+    order = bench.deal_order(nx, ny, world)
+    lists = [order[r::world] for r in range(world)]
+    times = [float(len(lst)) for lst in lists]  # every rank at the same time per ray
+    assert bench.refine_deal(lists, costs, times, nx) == [list(lst) for lst in lists]
+
+
+def test_opt_rejects_unknown_fields(monkeypatch):
+    """bench.py --opt names an rt_options field or exits (a ctypes Structure accepts any name)."""
+    import pytest
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--opt", "inw_wide_wlak=0", "--steps", "1"])
+    monkeypatch.setenv("WORLD_SIZE", "1")
+
+    class Stop(Exception):
+        pass
+
+    def no_device(*a, **k):
+        raise Stop()
+    monkeypatch.setattr(bench.torch.cuda, "set_device", lambda *a: None)
+    monkeypatch.setattr(bench.R, "get_options", lambda: bench.R.RtOptions())
+    monkeypatch.setattr(bench.R, "load", lambda *a: None)
+    monkeypatch.setattr(bench.R, "set_options", no_device)
+    with pytest.raises(SystemExit, match="inw_wide_wlak"):
+        bench.main()

@@ -174,3 +174,49 @@ def test_inw_strategies_bit_identical(gpu, over, scene, w, h, spp):
     # leaves are tested together), so only the ray-level counters must agree
     for k in ("segments", "shadow_queries", "stack_drops", "nan_drops"):
         assert sa[k] == sb[k], k
+
+
+@pytest.mark.parametrize("over,scene,w,h,spp", [
+    ({}, INW1, 160, 90, 12),                       # pixel-major fold (k_inw_pm, LDS ring: 25 LBVH nodes in LDS)
+    ({"inw_order": 2}, INW1, 160, 90, 12),          # sample-major fold (1,180 LBVH nodes in LDS)
+    ({"inw_order": -1}, INW1, 160, 90, 12),         # the per-pixel kernel (no LDS staging)
+    ({"inw_lds_nodes": 0}, INW1, 160, 90, 12),      # 256-lane instances, every node from global memory
+    ({"inw_order": 1}, INW4, 96, 96, 10),           # INW-04: shadow rays, RI walks
+    ({"inw_order": 2}, INW4, 96, 96, 10),
+])
+def test_stackless_walk_equals_stack_walk(gpu, over, scene, w, h, spp):
+    """The stackless LBVH walks (rt_options.inw_stackless) against the reference's
+    stack walks with the wide walk off: the same image and depth, and -- since they visit the
+    same nodes in the same order -- the same node visits and object tests as well as the ray
+    counters, all equal to the oracle's."""
+    from oracle import oracle as O
+    base = {"inw_wide_walk": 0, **over}
+    a, sa = _render({**base, "inw_stackless": 0}, w, h, spp, scene)
+    b, sb = _render({**base, "inw_stackless": 1}, w, h, spp, scene)
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), np.argwhere(~same.all(axis=2))[:10].tolist()
+    sc = _scene(scene[0], scene[1], scene[2], w, h, spp)
+    _, _, so = O.render(sc)
+    for k in ("segments", "node_visits", "prim_tests", "shadow_queries", "stack_drops", "nan_drops"):
+        assert sa[k] == sb[k] == so[k], (k, sa[k], sb[k], so[k])
+    # the path report of a device scene built with those options (inw_wide_walk is a [build] option)
+    import ctypes as C
+
+    import torch
+    sc = _scene(scene[0], scene[1], scene[2], w, h, spp)
+    lib = R.load()
+    with R.options(**{**R.default_options().as_dict(), **base, "inw_stackless": 1}):
+        s = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, sc.layout, R.fptr(sc.nodes),
+                                 R.fptr(sc.lights if sc.n_lights else None), sc.n_lights, spp, -1)
+    assert s
+    try:
+        img = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+        ctr = torch.zeros(6, dtype=torch.int64, device="cuda")
+        assert lib.rt_render_image_async(s, C.byref(sc.camera), C.byref(sc.params), img.data_ptr(), None,
+                                         ctr.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        path = R.debug_path(s)
+    finally:
+        lib.rt_dev_scene_free(s)
+    print(over, path)
+    assert path["stackless"] == 1 and path["wide_walk"] == 0

@@ -1,0 +1,85 @@
+"""The multi-GPU partition behind the C ABI (BASELINE configs[3]): rt_group_create
+(one RCCL communicator per device, ncclCommInitAll), rt_render_multi_async (every device renders
+its tile share, grouped ncclSend / ncclRecv to device 0, unpack there) and the blocking
+rt_render_inw_multi a C++ host calls in place of RT_Base<>::OnUpdateBase's dispatch
+(In-Next-Week/base.h:148-173).  The box has one GPU, so the group holds one device: its tiles
+still travel through RCCL (device 0 sends to itself), and the frame must be bit-identical to the
+single-device render, with the same ray counts.  The deal itself is checked on the CPU
+(tests/test_host_logic.py::test_tile_deal_matches_bench)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import rt_amd as R
+from cases import compare
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("preset,n,w,h,spp,tile", [
+    (R.PRESET_INW01_RANDOM, 2000, 100, 60, 12, 16),   # ragged: 100 x 60 is not a multiple of 16
+    (R.PRESET_INW01_RANDOM, 3000, 96, 64, 7, 64),     # one ragged 64 x 64 tile row
+    (R.PRESET_INW04_CORNELL, 0, 64, 48, 9, 32),       # INW-04: lights, shadow queries
+])
+def test_blocking_multi_matches_single_device(gpu, preset, n, w, h, spp, tile):
+    sc = R.make_scene(preset, 7 if preset == R.PRESET_INW04_CORNELL else 1234, n, width=w, height=h, spp=spp)
+    g, gd, gst = R.render(sc)
+    m, md, mst = R.render_inw_multi(sc, [0], tile=tile)
+    assert compare(m, g)["exact_frac"] == 1.0
+    assert compare(md, gd)["exact_frac"] == 1.0
+    for k in ("segments", "node_visits", "prim_tests", "shadow_queries", "stack_drops", "nan_drops"):
+        assert mst[k] == gst[k], (k, mst[k], gst[k])
+
+
+def test_group_async_frames_match_image_render(gpu):
+    """A persistent group renders frame after frame (two cameras alternating) into device-0
+    buffers: each frame equals rt_render_image_async of the same camera, counters included."""
+    import copy
+
+    import torch
+
+    sc = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 2500, width=80, height=48, spp=10)
+    sc2 = copy.copy(sc)
+    sc2.camera = R.RtCamera.from_buffer_copy(sc.camera)
+    sc2.camera.pos[2] += 4.0
+    lib = R.load()
+    dev = torch.device("cuda")
+    s = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, 1, R.fptr(sc.nodes), None, 0, sc.params.spp, 0)
+    assert s
+    devs = (C.c_int * 1)(0)
+    grp = lib.rt_group_create(devs, 1)
+    assert grp
+    scenes = (C.c_void_p * 1)(s)
+    stream = torch.cuda.current_stream().cuda_stream
+    try:
+        for i in range(4):
+            cam = (sc.camera, sc2.camera)[i % 2]
+            out = []
+            for multi in (True, False):
+                img = torch.zeros((48, 80, 4), dtype=torch.float32, device=dev)
+                dep = torch.zeros((48, 80), dtype=torch.float32, device=dev)
+                ctr = torch.zeros(6, dtype=torch.int64, device=dev)
+                if multi:
+                    rc = lib.rt_render_multi_async(grp, scenes, C.byref(cam), C.byref(sc.params), 16, img.data_ptr(),
+                                                   dep.data_ptr(), ctr.data_ptr(), stream)
+                else:
+                    rc = lib.rt_render_image_async(s, C.byref(cam), C.byref(sc.params), img.data_ptr(),
+                                                   dep.data_ptr(), ctr.data_ptr(), stream)
+                assert rc == 0
+                torch.cuda.synchronize()
+                out.append((img.cpu().numpy(), dep.cpu().numpy(), ctr.cpu().numpy()))
+            (a, ad, ac), (b, bd, bc) = out
+            assert compare(a, b)["exact_frac"] == 1.0, i
+            assert compare(ad, bd)["exact_frac"] == 1.0, i
+            assert np.array_equal(ac, bc), (i, ac, bc)
+    finally:
+        lib.rt_group_free(grp)
+        lib.rt_dev_scene_free(s)
+
+
+def test_group_rejects_bad_device_lists(gpu):
+    lib = R.load()
+    assert not lib.rt_group_create((C.c_int * 2)(0, 0), 2)   # one rank per device
+    assert not lib.rt_group_create((C.c_int * 1)(4096), 1)   # no such device
+    assert not lib.rt_group_create(None, 1)

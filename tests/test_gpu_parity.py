@@ -129,14 +129,20 @@ def test_unsupported_texture_index_fails_loudly(gpu):
 
 def test_repeated_frames_on_one_device_scene(gpu):
     """A device scene renders frame after frame with its fold rings kept (their tags carry a
-    frame epoch; they are cleared only when it wraps every 63 frames): 70 frames, alternating the
-    fold windows (global rings, k_inw_pm's LDS ring) and the fold order between them, all bit-identical to the first, colour and depth,
-    with the same ray counts."""
+    frame epoch; they are cleared only when it wraps every 63 frames): 70 frames, alternating two
+    cameras (so a stale ring entry of the other view would change the image), the fold windows
+    (global rings, k_inw_pm's LDS ring) and the fold order between them; every frame is
+    bit-identical to the oracle's render of its camera, colour and depth, with the same ray counts."""
+    import copy
     import ctypes as C
 
     import torch
 
     sc = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 3000, width=64, height=40, spp=37)
+    sc2 = copy.copy(sc)
+    sc2.camera = R.RtCamera.from_buffer_copy(sc.camera)
+    sc2.camera.pos[0] += 3.0
+    sc2.camera.pos[1] -= 1.5
     lib = R.load()
     dev = torch.device("cuda")
     s = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, 1, R.fptr(sc.nodes), None, 0, sc.params.spp, -1)
@@ -149,37 +155,38 @@ def test_repeated_frames_on_one_device_scene(gpu):
             o.inw_ring_pm, o.inw_ring_sm = ((64, 128), (0, 256), (1024, 256), (0, 64))[i % 4]
             o.inw_order = (0, 1, 2)[i % 3]
             assert lib.rt_dev_scene_set_options(s, C.byref(o)) == 0
+            cam = (sc.camera, sc2.camera)[i % 2]
             img = torch.zeros((40, 64, 4), dtype=torch.float32, device=dev)
             dep = torch.zeros((40, 64), dtype=torch.float32, device=dev)
             ctr = torch.zeros(6, dtype=torch.int64, device=dev)
-            rc = lib.rt_render_image_async(s, C.byref(sc.camera), C.byref(sc.params), img.data_ptr(), dep.data_ptr(),
+            rc = lib.rt_render_image_async(s, C.byref(cam), C.byref(sc.params), img.data_ptr(), dep.data_ptr(),
                                            ctr.data_ptr(), torch.cuda.current_stream().cuda_stream)
             assert rc == 0
             torch.cuda.synchronize()
             frames.append((img.cpu().numpy(), dep.cpu().numpy(), int(ctr[0].item())))
     finally:
         lib.rt_dev_scene_free(s)
-    g, gd, gs = frames[0]
-    o, od, ost = O.render(sc)
-    assert compare(g, o)["exact_frac"] == 1.0 and compare(gd, od)["exact_frac"] == 1.0 and gs == ost["segments"]
-    for i, (a, d, n) in enumerate(frames[1:], 1):
-        assert compare(a, g)["exact_frac"] == 1.0, i
-        assert compare(d, gd)["exact_frac"] == 1.0, i
-        assert n == gs, i
+    refs = [O.render(x) for x in (sc, sc2)]
+    assert compare(refs[0][0], refs[1][0])["exact_frac"] < 0.5  # the two views differ
+    for i, (a, d, n) in enumerate(frames):
+        o, od, ost = refs[i % 2]
+        assert compare(a, o)["exact_frac"] == 1.0, i
+        assert compare(d, od)["exact_frac"] == 1.0, i
+        assert n == ost["segments"], i
 
 
-@pytest.mark.parametrize("device_lbvh", [False, True])
-def test_scene_update_matches_fresh_scene(gpu, device_lbvh):
+@pytest.mark.parametrize("device_lbvh,n_new", [(False, 3000), (True, 3000), (True, 3600), (False, 2200)])
+def test_scene_update_matches_fresh_scene(gpu, device_lbvh, n_new):
     """rt_dev_scene_inw_update (the per-redraw work of RT_Base::OnUpdateBase, In-Next-Week/base.h:
-    96-175) on an existing device scene: moved objects, the LBVH given or built on the device,
-    then a frame -- bit-identical to a scene built from scratch for the moved objects, and to the
-    oracle."""
+    96-175) on an existing device scene: moved objects (n_new of them: the same count, more or
+    fewer), the LBVH given or built on the device, then a frame -- bit-identical to a scene built
+    from scratch for the moved objects, and to the oracle."""
     import ctypes as C
 
     import torch
 
     a = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 3000, width=64, height=36, spp=12)
-    b = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 3000, width=64, height=36, spp=12)
+    b = R.make_scene(R.PRESET_INW01_RANDOM, 1234, n_new, width=64, height=36, spp=12)
     for i in range(b.n):  # every object moves
         for k in range(3):
             b.desc[i].position[k] += 0.25 * ((i + k) % 3 - 1)

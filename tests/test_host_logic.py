@@ -150,3 +150,20 @@ def test_iow_host_structures():
     info = R.iow_host_build(sc.types, sc.records, sc.n)
     assert 1 <= info["wide_nodes"] < sc.n
     assert R.iow_host_build(sc.types[:1], sc.records[:1], 1)["wide_nodes"] == 0
+
+
+def test_tile_deal_matches_bench():
+    """rt_tile_deal (the C ABI's multi-GPU deal, rt_multi.hip) is bench.py's deal_order: every
+    tile once, row-major on one device, the multiplicative-hash permutation across devices; device
+    r's share is entries r, r + n, ... (bench.tiles_for_rank)."""
+    import bench
+    for (W, H, T) in ((1920, 1080, 16), (1920, 1080, 64), (100, 60, 16), (4096, 4096, 32), (17, 9, 16)):
+        nx, ny = -(-W // T), -(-H // T)
+        for n in (1, 2, 3, 8):
+            got = R.tile_deal(W, H, T, n)
+            assert got == bench.deal_order(nx, ny, n), (W, H, T, n)
+            assert sorted(got) == sorted((tx, ty) for ty in range(ny) for tx in range(nx))
+            for r in range(n):
+                assert got[r::n] == bench.tiles_for_rank(W, H, n, r, T)[1]
+    assert R.load().rt_tile_deal(0, 10, 16, 1, None, 0) < 0
+    assert R.load().rt_tile_deal(10, 10, 16, 0, None, 0) < 0
