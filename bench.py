@@ -354,7 +354,7 @@ def main():
     use_tiles(lists[part], per_rank)
     if args.rebuild and not inw:
         raise SystemExit("--rebuild: INW configs only (c3 / c4)")
-    rb_ms = np.zeros(6)  # per timed step: pack, records, LBVH, host structures, their upload, (unused)
+    rb_ms = np.zeros(6)  # per timed step: pack, records, LBVH, walk structures, their upload, (unused)
     rb_on = [False]
     lib.rt_debug_time_kernels(1)
     if args.occupancy:
@@ -365,7 +365,8 @@ def main():
     def rebuild():
         """RT_Base<>::OnUpdateBase's per-redraw scene work on the device scene: FillBuffer and the
         swept boxes (rt_pack_inw), the records, the LBVH on the device (ConstructLBVH_Buff,
-        base.h:135-142), the wide walk and RI grid on the host, every upload."""
+        base.h:135-142), the wide walk and RI grid on the device (rt_options.inw_device_build;
+        0: on the host from the read-back LBVH, then uploaded)."""
         t0 = time.perf_counter()
         pk = R.pack(sc.desc, sc.n, sc.stage, build_lbvh=False)
         t1 = time.perf_counter()
@@ -654,9 +655,11 @@ def main():
                              "frame are outside it (bench.py --rebuild times them per step)"),
         }
         if args.rebuild:
-            out["rebuild_ms_per_step"] = dict(zip(("pack", "records", "lbvh_device", "host_structures", "upload"),
+            out["rebuild_ms_per_step"] = dict(zip(("pack", "records", "lbvh_device", "walk_structures", "upload"),
                                                   [round(v / args.steps, 3) for v in rb_ms[:5]]))
             out["rebuild_ms_per_step"]["render_events"] = round(kernel_ms, 3)
+            out["rebuild_ms_per_step"]["walk_structures_on"] = ("device" if R.get_options().inw_device_build
+                                                                else "host")
             out["blocking_rt_render_inw_ms"] = round(blocking_ms, 1) if blocking_ms is not None else None
             out["config"]["workload"] += " + per-step scene rebuild (--rebuild)"
         if args.occupancy:

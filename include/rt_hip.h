@@ -117,6 +117,9 @@ typedef struct rt_options {
     int inw_stackless;      /* the reference's LBVH walks (closest hit, surrounding RI) without their stack, by
                                the node buffer's parent links, wherever no push could drop; their top
                                nodes staged in LDS when there is no wide walk (DESIGN.md "Stackless") */
+    int inw_device_build;   /* rt_dev_scene_inw_update with the LBVH built on the device: the wide walk's
+                               4-wide BVH (binned SAH), ranks and RI grid built on the device too (0: on
+                               the host from the read-back LBVH, as rt_dev_scene_inw does) */
     /* IOW-03 (In-One-Weekend 03) */
     int iow_spec;           /* sample-parallel speculation (0: the sequential per-pixel kernel) */
     int iow_linear;         /* [build] the shader's linear object loop instead of the culling BVH */
@@ -285,9 +288,11 @@ void rt_dev_scene_free(rt_dev_scene *s);
  * uploads) on the scene's existing device buffers.  geom: N*28 records of the scene's layout;
  * nodes: the caller's LBVH ((2N-1)*8), or NULL to build it on the device from aabbs (N*6, the
  * swept boxes rt_pack_inw writes) with rt_lbvh_build_async; lights: the layout-4 light SSBO.
- * The wide walk's structures and the RI grid are rebuilt on the host.  Synchronises the device
- * first.  timing_ms (may be NULL) receives the host time of {records, LBVH (upload + device
- * build + read-back), host structures, their upload}.  If any step fails the scene keeps its
+ * The wide walk's structures and the RI grid are rebuilt on the device from a device-built LBVH
+ * (rt_options.inw_device_build, the default), else on the host.  Synchronises the device first.
+ * timing_ms (may be NULL) receives the host time of {records, LBVH (upload + device build, +
+ * read-back for the host builders), the wide walk's structures (device or host build), their
+ * upload (0 for the device build)}.  If any step fails the scene keeps its
  * previous object count but its buffers may be partly replaced: every render of it then returns
  * RT_E_ARG until a later update succeeds. */
 int rt_dev_scene_inw_update(rt_dev_scene *s, const float *geom, uint32_t n, const float *nodes, const float *aabbs,
@@ -439,6 +444,11 @@ int rt_debug_time_kernels(int on);
  * Writes the mismatch count and the lowest mismatching x (0xffffffff if none); synchronous. */
 int rt_debug_check_fastmath(int which, uint64_t *mismatches, uint32_t *first_bad);
 int rt_debug_kernel_time(rt_dev_scene *s, double *ms_total, int *launches);
+/* The INW scene's walk structures (synchronises): info = {wide nodes, dfs_high, wide depth, RI grid
+ * built, RI cells, stackless layout, objects, 0}; rank_out (2n, may be NULL) receives the objects'
+ * depth-first ranks (invert 0, then 1) when the wide walk is built.  Lets the tests compare the
+ * device build (rt_dev_scene_inw_update) with the host build of a fresh scene. */
+int rt_debug_wide_info(rt_dev_scene *s, uint32_t info[8], uint32_t *rank_out);
 
 #ifdef __cplusplus
 }

@@ -32,6 +32,7 @@ rt_options default_options() {
     o.size = sizeof(rt_options);
     o.inw_wide_walk = 1; o.inw_order = 0; o.inw_beams = 1; o.inw_ri_grid = 1; o.inw_lds_nodes = 1;
     o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 0; o.inw_ring_sm = 256; o.inw_stackless = 1;
+    o.inw_device_build = 1;
     o.iow_spec = 1; o.iow_linear = 0; o.iow_narrow = 0; o.iow_lds_bvh = 1;
     o.iow_leaf_batch = 32;  // 32 measured 2.5% faster on the bench frame than 65 (round 2)
     o.iow_coop_max = 4; o.iow_chunks_lpt = 0;
@@ -76,6 +77,12 @@ struct DevBuf {  // RAII device allocation
         hipError_t e = alloc(b);
         if (e != hipSuccess || !b) return e;
         return hipMemcpy(p, src, b, hipMemcpyHostToDevice);
+    }
+    // at least b bytes of capacity (contents undefined; `bytes` stays the capacity)
+    hipError_t reserve(size_t b) {
+        if (p && bytes >= b) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; }
+        return alloc(b);
     }
     // copy b bytes in, reusing the allocation when it is large enough (a scene update); `bytes`
     // stays the capacity
@@ -171,6 +178,7 @@ struct rt_dev_scene {
     uint32_t n_wnodes = 0;        // its nodes
     bool ri_ok = false;           // the RI grid applies (ri_cells / ri_ids hold it)
     DevBuf lbvh_ws;               // rt_dev_scene_inw_update: device LBVH workspace
+    DevBuf build_ws, ri_fill, ri_tmp;  // ... and the device build of the wide walk and RI grid (rt_build.hip)
     bool last_ln = false;         // the last INW fold launch used the LDS-staged kernels
     bool last_fu = false;         // ... their fused-fma cull instances
     uint32_t last_force = 0;      // ... its forced order (0: the probe's pick, read back from inw_mode)
@@ -446,6 +454,62 @@ int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const f
     return build_tables(s, spp);
 }
 
+// The same structures built on the device from the scene's device LBVH (rt_build.hip, DESIGN.md
+// "Device build"; rt_options.inw_device_build): no host build, no upload.  ms: host wall time of
+// the build (its level loop and the RI grid read counts back) in ms[0], 0 in ms[1].
+int make_inw_wide_device(rt_dev_scene *s, uint32_t n, double *ms) {
+    s->dfs_high = 0;
+    s->sl_ok = false;
+    s->n_wnodes = 0;
+    s->ri_ok = false;
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_OK(s->wnodes.reserve(size_t(n) * 40 * sizeof(float)));
+    HIP_OK(s->wrank.reserve(size_t(n) * 2 * sizeof(uint32_t)));
+    HIP_OK(s->wleaf.reserve(size_t(n) * 8 * sizeof(float)));
+    const size_t wsb = rtk::inw_build_workspace_bytes(n);
+    HIP_OK(s->build_ws.reserve(wsb));
+    rtk::InwWideDev out{s->wnodes.as<float4>(), s->wrank.as<uint32_t>(), s->wleaf.as<float4>(), 0, 0, 0, 0.0f};
+    HIP_OK(rtk::inw_wide_build_device(s->nodes.as<float4>(), n, s->build_ws.p, s->build_ws.bytes, out, nullptr));
+    if (s->opt.inw_wide_walk) {
+        float lo[3], hi[3];
+        HIP_OK(rtk::ri_bounds_device(s->wleaf.as<float4>(), n, s->build_ws.p, lo, hi, nullptr));
+        double dlo[3], dhi[3], inv[3];
+        int dim[3];
+        for (int a = 0; a < 3; a++) { dlo[a] = lo[a]; dhi[a] = hi[a]; }
+        if (rtamd::ri_grid_dims(dlo, dhi, n, dim, inv)) {
+            const size_t nc = size_t(dim[0]) * dim[1] * dim[2];
+            HIP_OK(s->ri_cells.reserve((nc + 1) * sizeof(uint32_t)));
+            const size_t tb = rtk::ri_scan_temp_bytes(nc + 1);
+            HIP_OK(s->ri_tmp.reserve(tb));
+            uint32_t total = 0, over = 0;
+            HIP_OK(rtk::ri_count_device(s->wleaf.as<float4>(), n, s->build_ws.p, dlo, inv, dim, s->ri_cells.as<uint32_t>(),
+                                        s->ri_tmp.p, tb, &total, &over, nullptr));
+            if (!over) {
+                HIP_OK(s->ri_ids.reserve(std::max<size_t>(1, total) * sizeof(uint32_t)));
+                HIP_OK(s->ri_fill.reserve(std::max<size_t>(1, nc) * sizeof(uint32_t)));
+                HIP_OK(rtk::ri_fill_device(s->wleaf.as<float4>(), n, dlo, inv, dim, s->ri_cells.as<uint32_t>(),
+                                           s->ri_fill.as<uint32_t>(), s->ri_ids.as<uint32_t>(), nullptr));
+                for (int a = 0; a < 3; a++) {
+                    s->ri_lo[a] = float(dlo[a]); s->ri_hi[a] = float(dhi[a]); s->ri_inv[a] = float(inv[a]);
+                    s->ri_dim[a] = dim[a];
+                }
+                s->ri_ok = true;
+            }
+        }
+        s->n_wnodes = out.n_wnodes;
+        s->wdepth = out.depth;
+        s->wbound = out.wbound;
+    }
+    HIP_OK(hipDeviceSynchronize());
+    s->dfs_high = out.dfs_high;
+    s->sl_ok = true;  // the device LBVH has the stackless layout by construction (rt_lbvh.hip)
+    if (ms) {
+        ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        ms[1] = 0.0;
+    }
+    return RT_OK;
+}
+
 // RT_Base<>::OnUpdateBase's per-redraw work on an existing device scene (In-Next-Week/base.h:
 // 96-175): new records, the LBVH (the caller's, or built on the device from the boxes), the wide
 // walk and RI grid rebuilt on the host, every upload into the scene's buffers.  ms[4]: host time
@@ -460,6 +524,9 @@ int update_inw(rt_dev_scene *s, const float *geom, uint32_t n, const float *node
         t = now;
     };
     if (n > (1u << 24)) return RT_E_UNSUPPORTED;  // node / object ids are stored as floats (exact to 2^24)
+    // the wide walk's structures and the RI grid built on the device from the device LBVH
+    // (rt_options.inw_device_build; a caller's host LBVH keeps the host builders)
+    const bool device_build = s->opt.inw_device_build && !nodes && n >= 2;
     // Until every step below has succeeded the buffers may hold a mix of the old and the new
     // scene (sizes included): the scene refuses renders (launch_scene) and keeps its old n and
     // counts, so nothing indexes past a buffer.  The new sizes are committed at the end.
@@ -484,15 +551,19 @@ int update_inw(rt_dev_scene *s, const float *geom, uint32_t n, const float *node
         const size_t ws = rtk::lbvh_workspace_bytes(n);
         if (s->lbvh_ws.bytes < ws) { s->lbvh_ws.~DevBuf(); new (&s->lbvh_ws) DevBuf(); HIP_OK(s->lbvh_ws.alloc(ws)); }
         HIP_OK(rtk::lbvh_build_device(d_aabb.as<float>(), n, s->nodes.as<float>(), s->lbvh_ws.p, ws, nullptr));
-        host_nodes.resize(nbytes / sizeof(float));
-        HIP_OK(hipMemcpy(host_nodes.data(), s->nodes.p, nbytes, hipMemcpyDeviceToHost));
-        nodes = host_nodes.data();
+        if (!device_build) {  // the host builders read it
+            host_nodes.resize(nbytes / sizeof(float));
+            HIP_OK(hipMemcpy(host_nodes.data(), s->nodes.p, nbytes, hipMemcpyDeviceToHost));
+            nodes = host_nodes.data();
+        }
     } else {
         HIP_OK(s->nodes.store(nodes, nbytes));
     }
     lap(1);
     double w[2] = {0.0, 0.0};
-    if (int rc = make_inw_wide(s, nodes, n, w); rc != RT_OK) return rc;
+    if (device_build) {
+        if (int rc = make_inw_wide_device(s, n, w); rc != RT_OK) return rc;
+    } else if (int rc = make_inw_wide(s, nodes, n, w); rc != RT_OK) return rc;
     if (ms) { ms[2] = w[0]; ms[3] = w[1]; }
     s->n = n;
     s->n_lights = nl;
@@ -1411,6 +1482,19 @@ int rt_dev_scene_set_options(rt_dev_scene *s, const rt_options *o) {
     s->opt = *o;
     s->opt.inw_wide_walk = wide;
     s->opt.iow_linear = linear;
+    return RT_OK;
+}
+
+int rt_debug_wide_info(rt_dev_scene *s, uint32_t info[8], uint32_t *rank_out) {
+    if (!s || s->kind == 3 || !info) return RT_E_ARG;
+    HIP_OK(hipSetDevice(s->device));
+    HIP_OK(hipDeviceSynchronize());
+    const uint32_t cells = s->ri_ok ? uint32_t(s->ri_dim[0]) * uint32_t(s->ri_dim[1]) * uint32_t(s->ri_dim[2]) : 0u;
+    const uint32_t v[8] = {s->n_wnodes, s->dfs_high, uint32_t(s->wdepth), s->ri_ok ? 1u : 0u, cells,
+                           s->sl_ok ? 1u : 0u, s->n, 0u};
+    std::memcpy(info, v, sizeof(v));
+    if (rank_out && s->n_wnodes)
+        HIP_OK(hipMemcpy(rank_out, s->wrank.p, size_t(s->n) * 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

@@ -845,6 +845,21 @@ bool lbvh_walk_info(const float *nodes, uint32_t n, uint32_t &high, bool &stackl
     return true;
 }
 
+bool ri_grid_dims(const double lo[3], const double hi[3], uint32_t n, int dim[3], double inv[3]) {
+    double ext[3], vol = 1.0;
+    for (int a = 0; a < 3; a++) {
+        if (!(hi[a] >= lo[a]) || !std::isfinite(lo[a]) || !std::isfinite(hi[a])) return false;
+        ext[a] = std::fmax(hi[a] - lo[a], 1e-6 * (1.0 + std::fabs(lo[a])));
+        vol *= ext[a];
+    }
+    const double cell = std::cbrt(vol / (2.0 * n));
+    for (int a = 0; a < 3; a++) {
+        dim[a] = int(std::fmin(512.0, std::fmax(1.0, std::ceil(ext[a] / cell))));
+        inv[a] = double(dim[a]) / ext[a];
+    }
+    return true;
+}
+
 RiGrid ri_grid_build(const float *lbox, uint32_t n) {
     RiGrid G;
     double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
@@ -853,19 +868,9 @@ RiGrid ri_grid_build(const float *lbox, uint32_t n) {
             lo[a] = std::fmin(lo[a], double(lbox[size_t(g) * 8 + a]));
             hi[a] = std::fmax(hi[a], double(lbox[size_t(g) * 8 + 3 + a]));
         }
-    double ext[3], vol = 1.0;
-    for (int a = 0; a < 3; a++) {
-        if (!(hi[a] >= lo[a]) || !std::isfinite(lo[a]) || !std::isfinite(hi[a])) return G;
-        ext[a] = std::fmax(hi[a] - lo[a], 1e-6 * (1.0 + std::fabs(lo[a])));
-        vol *= ext[a];
-    }
-    const double cell = std::cbrt(vol / (2.0 * n));
     int dim[3];
     double inv[3];
-    for (int a = 0; a < 3; a++) {
-        dim[a] = int(std::fmin(512.0, std::fmax(1.0, std::ceil(ext[a] / cell))));
-        inv[a] = double(dim[a]) / ext[a];
-    }
+    if (!ri_grid_dims(lo, hi, n, dim, inv)) return G;
     const size_t nc = size_t(dim[0]) * dim[1] * dim[2];
     std::vector<uint32_t> cnt(nc + 1, 0);
     auto range = [&](uint32_t g, int a, int &c0, int &c1) {

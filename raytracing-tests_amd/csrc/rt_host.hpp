@@ -148,6 +148,9 @@ struct RiGrid {
     std::vector<uint32_t> cells, ids;  // cell offsets (cells + 1), object ids
 };
 RiGrid ri_grid_build(const float *leafbox, uint32_t n);
+// its cell counts per axis over the leaf boxes' bounds [lo, hi] (false: not finite), shared with
+// the device build (rt_build.hip)
+bool ri_grid_dims(const double lo[3], const double hi[3], uint32_t n, int dim[3], double inv[3]);
 
 // ---- camera (materials.cpp:321-328, base.h:274-281) ------------------------------------
 Vec3 front_from_pitch_yaw(float pitch_deg, float yaw_deg, bool normalize);

@@ -337,6 +337,12 @@ __device__ __forceinline__ RayRet iow_eval(const IowScene &S, f3 go, f3 gd, f3 t
     return iow_eval_c(S, go, gd, td_id, nd_id, min_t, best, max_t, contrib, c0, c1);
 }
 
+// IOW BVH-stack slot p of a lane (16-bit links): slots 2q and 2q + 1 share the lane's dword in row
+// q, [q][lane][2], so the 32 lanes of an LDS access group always touch 32 different banks, whatever
+// their stack depths ([slot][lane] put two lanes in each dword: a 2-way conflict whenever their
+// depths differ).  b = the lane's pair base, lds + 2 * lane.
+__device__ __forceinline__ short &bslot(short *b, int p) { return b[(p >> 1) * (2 * kBlock) + (p & 1)]; }
+
 // LaunchRay 03...glsl:196-256.  The reference loops over every object and keeps the first
 // strictly nearer hit, i.e. the minimum t with the lowest index among exact ties.  The BVH
 // walk visits a superset of the objects that can attain that minimum and applies the same
@@ -394,9 +400,9 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
                     // branch-free pushes, farthest first: a miss is written above the top and
                     // overwritten before it could be popped (the array has 3 spare entries)
                     int p = sp;
-                    bstk[p * kBlock] = (short)k3; p += t3 != kMiss;
-                    bstk[p * kBlock] = (short)k2; p += t2 != kMiss;
-                    bstk[p * kBlock] = (short)k1; p += t1 != kMiss;
+                    bslot(bstk, p) = (short)k3; p += t3 != kMiss;
+                    bslot(bstk, p) = (short)k2; p += t2 != kMiss;
+                    bslot(bstk, p) = (short)k1; p += t1 != kMiss;
                     if (p > BCAP) { ovf = true; p = BCAP; }
                     sp = p;
                     cur = k0;
@@ -407,7 +413,7 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
                 }
                 if (pop) {
                     if (sp == 0) walking = false;
-                    else cur = bstk[(--sp) * kBlock];
+                    else cur = bslot(bstk, --sp);
                 }
             }
             if (__all(!walking || pend >= 0) || __popcll(__ballot(pend >= 0)) >= F_.leaf_batch) {
@@ -457,7 +463,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
 }
 
 // Closest hit of one (wave-uniform) ray with the whole wave.  wl: the wave's LDS list, entry k
-// at wl[(k >> 6) * kBlock + (k & 63)], cap entries (a multiple of 64 * kCoopR).  Returns the
+// at wl[(k >> 7) * (2 * kBlock) + (k & 127)] (bslot's layout), cap entries (a multiple of 64 * kCoopR).  Returns the
 // (uniform) winner and its cold record; nbox / nprim are the boxes and objects tested.  The
 // loads of a batch of kCoopR boxes per lane, and a candidate's hot and cold records, are
 // issued together: a lone ray's query costs about two memory latencies, not one per step.
@@ -505,7 +511,7 @@ __device__ void iow_coop_search(const IowScene &S, f3 go, f3 gd, float max_t, sh
                     const unsigned long long cm = __ballot(cand);
                     if (cand) {
                         const uint32_t k = cnt + lanes_below(cm);
-                        wl[(k >> 6) * kBlock + (k & 63)] = (short)j;
+                        wl[(k >> 7) * (2 * kBlock) + (k & 127)] = (short)j;
                     }
                     cnt += (uint32_t)__popcll(cm);
                 }
@@ -520,7 +526,7 @@ __device__ void iow_coop_search(const IowScene &S, f3 go, f3 gd, float max_t, sh
         for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
             const uint32_t k = k0 + lane;
             if (k < cnt) {
-                const int j = cull ? (int)wl[(k >> 6) * kBlock + (k & 63)] : (int)(jb + k);
+                const int j = cull ? (int)wl[(k >> 7) * (2 * kBlock) + (k & 127)] : (int)(jb + k);
                 const float4 *cold = reinterpret_cast<const float4 *>(S.cold + (size_t)j * kIowCold);
                 const float4 q0 = cold[0], q1 = cold[1];
                 const int was = bj;
@@ -690,7 +696,7 @@ __device__ __forceinline__ void iow_seg_step(const IowScene &S, const Frame &F, 
         return;
     }
     constexpr int kCap = BS * 64;  // the wave's BVH-stack slots, as a list
-    short *wl = bstk - (threadIdx.x & 63);
+    short *wl = bstk - 2 * (threadIdx.x & 63);
     DBG_T0(F, t_pop);
     SegIn in{};
     if (seg) in = iow_seg_pop(S, K, sidx);
@@ -844,7 +850,7 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
     __shared__ unsigned long long s_dbg[SUB * kBlock / 64][kDbgSlots];
     __shared__ float4 s_nodes[LN ? kIowLdsNodes * 7 : 1];
     const int sb = (int)(threadIdx.x / kBlock), tl = (int)(threadIdx.x % kBlock);
-    short *bstk = lds_bvh + sb * Cfg::BS * kBlock + tl;
+    short *bstk = lds_bvh + sb * Cfg::BS * kBlock + 2 * tl;  // bslot's layout
     const float4 *nodes = iow_stage_nodes<LN>(S, s_nodes);
     Ctr c;
     if (f.dbg) {
@@ -1069,7 +1075,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     __shared__ unsigned long long s_dbg[SUB * kBlock / 64][kDbgSlots];
     __shared__ float4 s_nodes[LN ? kIowLdsNodes * 7 : 1];
     const int sb = (int)(threadIdx.x / kBlock), tl = (int)(threadIdx.x % kBlock);
-    short *bstk = lds_bvh + sb * Cfg::BS * kBlock + tl;
+    short *bstk = lds_bvh + sb * Cfg::BS * kBlock + 2 * tl;  // bslot's layout
     const float4 *nodes = iow_stage_nodes<LN>(S, s_nodes);
     Ctr c;  // per unit here: written to the unit's record, never flushed
     if (f.dbg) {

@@ -243,6 +243,30 @@ hipError_t launch_iow03_spec(const Frame &f, const IowScene &sc, const SpecRecs 
 // LBVH build on the device (rt_lbvh.hip); ws = lbvh_workspace_bytes(n) of scratch
 size_t lbvh_workspace_bytes(uint32_t n);
 hipError_t lbvh_build_device(const float *aabb, uint32_t n, float *out, void *ws, size_t ws_bytes, hipStream_t s);
+// INW wide walk structures built on the device from a device LBVH (rt_build.hip, DESIGN.md
+// "Device build"): 4-wide culling BVH (10 float4 per node, <= n nodes), depth-first ranks (2n),
+// leaf boxes (2n float4); out's scalars are filled in.  Synchronises the stream (level counts).
+struct InwWideDev {
+    float4 *wnodes;
+    uint32_t *rank;
+    float4 *leafbox;
+    uint32_t n_wnodes, dfs_high;
+    int depth;
+    float wbound;
+};
+size_t inw_build_workspace_bytes(uint32_t n);
+hipError_t inw_wide_build_device(const float4 *nodes, uint32_t n, void *ws, size_t ws_bytes, InwWideDev &out,
+                                 hipStream_t s);
+// the surrounding-RI grid on the device (rtamd::ri_grid_build's cells and ids): the leaf boxes'
+// bounds (synchronises), then per-cell counts scanned into cells[0..nc] with the total and an
+// over-64 flag read back (synchronises), then the ids
+hipError_t ri_bounds_device(const float4 *leafbox, uint32_t n, void *ws, float lo[3], float hi[3], hipStream_t s);
+size_t ri_scan_temp_bytes(size_t cells);
+hipError_t ri_count_device(const float4 *leafbox, uint32_t n, void *ws, const double lo[3], const double inv[3],
+                           const int dim[3], uint32_t *cells, void *tmp, size_t tmp_bytes, uint32_t *total,
+                           uint32_t *over, hipStream_t s);
+hipError_t ri_fill_device(const float4 *leafbox, uint32_t n, const double lo[3], const double inv[3], const int dim[3],
+                          const uint32_t *cells, uint32_t *fill, uint32_t *ids, hipStream_t s);
 // Texture producers (rt_texture.hip): noise textures (MakeTexture, utility.h:69-192) and the
 // Mercator <-> cubic re-projection (utility.cpp:266-463).  noise_batches_exact(W): the
 // reference's 4 column batches tile [0, W) (other widths index out of bounds there).

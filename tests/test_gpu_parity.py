@@ -216,6 +216,18 @@ def test_scene_update_matches_fresh_scene(gpu, device_lbvh, n_new):
         print("update ms", list(tm))
         g, gd, gs = frame(s)
         h, hd, hs = frame(f)
+        # the walk structures: with the device LBVH they are built on the device (rt_build.hip,
+        # binned SAH), else on the host as for the fresh scene; the depth-first ranks and the stack
+        # high-water mark are functions of the LBVH alone, so they must equal the fresh scene's
+        info_s, info_f = (C.c_uint32 * 8)(), (C.c_uint32 * 8)()
+        rank_s, rank_f = (C.c_uint32 * (2 * b.n))(), (C.c_uint32 * (2 * b.n))()
+        assert lib.rt_debug_wide_info(s, info_s, rank_s) == 0 and lib.rt_debug_wide_info(f, info_f, rank_f) == 0
+        print("wide info update", list(info_s), "fresh", list(info_f))
+        assert info_s[0] > 0 and info_s[3] == 1 and info_s[5] == 1 and info_s[6] == b.n
+        assert info_s[1] == info_f[1]
+        assert list(rank_s) == list(rank_f)
+        if not device_lbvh:
+            assert list(info_s) == list(info_f)
     finally:
         lib.rt_dev_scene_free(s)
         lib.rt_dev_scene_free(f)
