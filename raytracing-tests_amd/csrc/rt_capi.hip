@@ -10,6 +10,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <memory>
 #include <new>
@@ -239,7 +240,7 @@ struct rt_dev_scene {
     // rt_debug_time_kernels: HIP events around every launch of the main sample-parallel kernel
     std::vector<std::pair<hipEvent_t, hipEvent_t>> kt_ev;
     size_t kt_used = 0;
-    unsigned epoch = 0;  // frame tag of the asynchronous-window records
+    unsigned epoch = 0;  // frame tag of the sample records (16 bits in their flags; next_spec_epoch)
     ~rt_dev_scene() {
         if (ev_start) (void)hipEventDestroy(ev_start);
     }
@@ -652,6 +653,21 @@ int ensure_lanes(rt_dev_scene *s, int groups, size_t temp_bytes) {
     return RT_OK;
 }
 
+// Frame tag of the sample-parallel records: a record is "done" for a frame when its flags carry
+// the frame's tag (16 bits).  The tags are process-wide, so a new scene whose record buffers
+// reuse a freed scene's memory never takes that scene's records for its own (the same render of
+// the full frame, then of one tile alone, found the full frame's records at its own indices and
+// returned their colours), and a scene clears its flags when its tag comes round again.
+unsigned next_spec_epoch(rt_dev_scene *s) {
+    static std::atomic<unsigned> g{0};
+    unsigned v;
+    do v = (g.fetch_add(1u) + 1u) & 0xffffu; while (v == 0u);
+    if (v <= s->epoch && s->sp_col.p)  // wrapped since this scene's last frame: forget its tags
+        (void)hipMemset(s->sp_col.p, 0, s->sp_col.bytes);
+    s->epoch = v;
+    return v;
+}
+
 // Sample-parallel records for P pixel units x S samples; false if they do not fit.
 bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
     const size_t n = size_t(P) * S;
@@ -676,6 +692,10 @@ bool ensure_spec(rt_dev_scene *s, uint32_t P, uint32_t S) {
         s->sp_sorder.alloc(size_t(S) * sizeof(uint32_t)) != hipSuccess ||
         s->sp_fcost.alloc(size_t(S) * sizeof(unsigned long long)) != hipSuccess ||
         s->sp_temp.alloc(s->sp_temp_bytes = rtk::sort_pairs_temp_bytes(n, 24)) != hipSuccess) {
+        s->spec_cap = s->spec_units = 0;
+        return false;
+    }
+    if (hipMemset(s->sp_col.p, 0, s->sp_col.bytes) != hipSuccess) {  // no flags: no record is done
         s->spec_cap = s->spec_units = 0;
         return false;
     }
@@ -840,7 +860,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     unsigned *sc = s->sp_counts.as<unsigned>();  // group g: [32g] list count, [32g+16] fallback count
     rtk::SpecRecs R{s->sp_col.as<float4>(), s->sp_fin.as<float4>(), s->sp_ctr.as<uint4>(),
                           s->sp_assume.as<float4>(), P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(),
-                          sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), ++s->epoch,
+                          sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), next_spec_epoch(s),
                           s->sp_front.as<uint4>(), s->sp_sorder.as<uint32_t>(),
                           uint32_t(o.spec_probe),
                           S > 2 && groups == 1 ? uint32_t(std::min(int(S) - 2, o.spec_heavy >= 0 ? o.spec_heavy
@@ -1296,7 +1316,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         P.wide_walk = sc.wnodes != nullptr;
         P.beams = sc.beam != nullptr;
         P.ri_grid = sc.ri_cells != nullptr;
-        P.fused_cull = s->last_fu ? 1 : 0;
+        P.fused_cull = s->last_fu && sc.wnodes ? 1 : 0;  // the fused cull is the wide walk's
         P.lds_nodes = s->last_ln ? int(std::min<uint32_t>(s->n_wnodes, uint32_t(rtk::kInwLdsNodes))) : 0;
         P.stackless = sc.sl ? 1 : 0;
         // the LBVH nodes the stackless walks read from LDS (LN kernels without the wide walk)

@@ -2777,6 +2777,16 @@ __global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S, Chunk ch, C
 // carries another epoch, and the host clears the rings with 0xff bytes (an epoch of 63, never
 // valid) whenever the epoch wraps to 0, so a stale entry never passes for a finished one and no
 // per-frame clear is needed.  Within a frame, slot g mod R last held g - R (R <= 2^16 < 2^26).
+// The fold kernels' framebuffer stores: written once, never read back by the frame, so they go
+// out as streaming (nontemporal) stores and do not push the waves' fold-ring lines out of L2
+typedef float fb_v4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void fb_store(const Frame &f, size_t o, float4 v) {
+    const fb_v4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<fb_v4 *>(f.out_rgba) + o);
+}
+__device__ __forceinline__ void depth_store(const Frame &f, size_t o, float d) {
+    __builtin_nontemporal_store(d, f.out_depth + o);
+}
 __device__ __forceinline__ uint32_t ring_tag(const InwScene &S, uint32_t g) {
     return (g & 0x03ffffffu) | S.ring_epoch;
 }
@@ -3090,10 +3100,10 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                     if (lane == 0) {
                         const UnitPix p = unit_pixel(f, unit);
                         if (p.out != (size_t)-1) {
-                            reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
-                                make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
-                                            p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
-                            if (f.out_depth) f.out_depth[p.out] = pdep[jf & 63u];
+                            fb_store(f, p.out,
+                                     make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
+                                                 p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f));
+                            if (f.out_depth) depth_store(f, p.out, pdep[jf & 63u]);
                         }
                     }
                     sf = 0;
@@ -3299,9 +3309,9 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                     if (++sf == spp) {  // pixel complete: End()'s imageStore (01_BVH...glsl:652)
                         const UnitPix p = unit_pixel(f, my_blk * 64u + lane);
                         if (p.out != (size_t)-1)
-                            reinterpret_cast<float4 *>(f.out_rgba)[p.out] =
-                                make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
-                                            p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f);
+                            fb_store(f, p.out,
+                                     make_float4(p.in_image ? acc.x * inv : 0.0f, p.in_image ? acc.y * inv : 0.0f,
+                                                 p.in_image ? acc.z * inv : 0.0f, p.in_image ? 1.0f : 0.0f));
                     }
                 }
                 if (sf == spp) { sf = 0; bf++; }
@@ -3359,7 +3369,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                         busy = true;
                         inw_start_sample(S, f, K, px.x, px.y, s, c);
                     } else {  // a padding slot: an empty sample, folded as zero
-                        if ((uint32_t)s == mid && f.out_depth && px.out != (size_t)-1) f.out_depth[px.out] = 0.0f;
+                        if ((uint32_t)s == mid && f.out_depth && px.out != (size_t)-1) depth_store(f, px.out, 0.0f);
                         wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(ring_tag(S, g)));
                     }
                 }
@@ -3377,7 +3387,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
             wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
                                         __uint_as_float(ring_tag(S, g)));
-            if ((uint32_t)s == mid && f.out_depth) f.out_depth[px.out] = dep;  // 01_BVH...glsl:667-668
+            if ((uint32_t)s == mid && f.out_depth) depth_store(f, px.out, dep);  // 01_BVH...glsl:667-668
             busy = false;
         }
     }

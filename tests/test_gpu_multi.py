@@ -28,7 +28,9 @@ def test_blocking_multi_matches_single_device(gpu, preset, n, w, h, spp, tile):
     m, md, mst = R.render_inw_multi(sc, [0], tile=tile)
     assert compare(m, g)["exact_frac"] == 1.0
     assert compare(md, gd)["exact_frac"] == 1.0
-    for k in ("segments", "node_visits", "prim_tests", "shadow_queries", "stack_drops", "nan_drops"):
+    # the wide walk's node and object counts depend on which rays share a wave (postponed leaves
+    # are tested together; tiles regroup the pixels), so the ray-level counters must agree
+    for k in ("segments", "shadow_queries", "stack_drops", "nan_drops"):
         assert mst[k] == gst[k], (k, mst[k], gst[k])
 
 
@@ -72,7 +74,7 @@ def test_group_async_frames_match_image_render(gpu):
             (a, ad, ac), (b, bd, bc) = out
             assert compare(a, b)["exact_frac"] == 1.0, i
             assert compare(ad, bd)["exact_frac"] == 1.0, i
-            assert np.array_equal(ac, bc), (i, ac, bc)
+            assert ac[0] == bc[0] and np.array_equal(ac[3:], bc[3:]), (i, ac, bc)  # ray-level counters
     finally:
         lib.rt_group_free(grp)
         lib.rt_dev_scene_free(s)

@@ -167,7 +167,7 @@ def test_repeated_frames_on_one_device_scene(gpu):
     finally:
         lib.rt_dev_scene_free(s)
     refs = [O.render(x) for x in (sc, sc2)]
-    assert compare(refs[0][0], refs[1][0])["exact_frac"] < 0.5  # the two views differ
+    assert int((refs[0][0] != refs[1][0]).any(axis=-1).sum()) > 200  # the two views differ (the sky is shared)
     for i, (a, d, n) in enumerate(frames):
         o, od, ost = refs[i % 2]
         assert compare(a, o)["exact_frac"] == 1.0, i
