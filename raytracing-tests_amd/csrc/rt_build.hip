@@ -28,6 +28,7 @@ namespace {
 constexpr int kB = 256;
 constexpr int kBins = 32;
 constexpr int kLevelBatch = 8;   // levels launched between two reads of the pending-task count
+constexpr int kSahFirst = 20;    // the binary SAH levels launched before the first read (C3's tree: ~20)
 constexpr int kMaxLevels = 256;  // binary SAH levels (a chain over n objects is at most n deep; the
                                  // binned split halves a degenerate range, so depth <= ~2 log2 n)
 
@@ -455,6 +456,10 @@ hipError_t inw_wide_build_device(const float4 *nodes, uint32_t n, void *ws, size
     hipLaunchKernelGGL(k_leaf_counts, dim3(nblk(n)), dim3(kB), 0, s, nodes, n, w.leafnode, w.lcnt);
     hipLaunchKernelGGL(k_ranks, dim3(nblk(n)), dim3(kB), 0, s, nodes, n, w.leafnode, w.lcnt, out.rank);
     hipLaunchKernelGGL(k_high, dim3(nblk(nn)), dim3(kB), 0, s, nodes, nn, w.meta);
+    // the RI grid's bounds (the leaf boxes'), read back with the counts below
+    const uint32_t binit[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+    BUILD_HIP(hipMemcpyAsync(w.ri_bnd, binit, sizeof(binit), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_ri_bounds, dim3(nblk(n)), dim3(kB), 0, s, out.leafbox, n, w.ri_bnd);
     BUILD_HIP(hipGetLastError());
     // binary SAH tree: root task (node 0, all objects); meta[0] = node counter (1: the root)
     const uint32_t one = 1u;
@@ -463,8 +468,8 @@ hipError_t inw_wide_build_device(const float4 *nodes, uint32_t n, void *ws, size
     BUILD_HIP(hipMemcpyAsync(w.lvl_cnt, &one, 4, hipMemcpyHostToDevice, s));
     BUILD_HIP(hipMemcpyAsync(w.meta, &one, 4, hipMemcpyHostToDevice, s));
     int lvl = 0;
-    for (;;) {
-        for (int k = 0; k < kLevelBatch && lvl < kMaxLevels; k++, lvl++)
+    for (int batch = kSahFirst;; batch = kLevelBatch) {
+        for (int k = 0; k < batch && lvl < kMaxLevels; k++, lvl++)
             hipLaunchKernelGGL(k_sah_level, dim3(1024), dim3(kB), 0, s, w.task[lvl & 1], w.lvl_cnt + lvl,
                                w.task[(lvl + 1) & 1], w.lvl_cnt + lvl + 1, w.ids, w.ids2, w.box, w.cen, w.bin,
                                w.meta);
@@ -486,38 +491,26 @@ hipError_t inw_wide_build_device(const float4 *nodes, uint32_t n, void *ws, size
             hipLaunchKernelGGL(k_collapse_level, dim3(nblk(n)), dim3(kB), 0, s, w.wtask[wl & 1], w.wlvl_cnt + wl,
                                w.wtask[(wl + 1) & 1], w.wlvl_cnt + wl + 1, w.bin, out.wnodes, w.meta + 1);
         BUILD_HIP(hipGetLastError());
-        uint32_t cnts[kLevelBatch + 1];
-        BUILD_HIP(hipMemcpyAsync(cnts, w.wlvl_cnt + wl - kLevelBatch, sizeof(cnts), hipMemcpyDeviceToHost, s));
+        // this batch's level counts, the counters (meta) and the RI bounds in one read
+        uint32_t rb[kLevelBatch + 1 + 4 + 6];
+        BUILD_HIP(hipMemcpyAsync(rb, w.wlvl_cnt + wl - kLevelBatch, (kLevelBatch + 1) * 4, hipMemcpyDeviceToHost, s));
+        BUILD_HIP(hipMemcpyAsync(rb + kLevelBatch + 1, w.meta, 4 * 4, hipMemcpyDeviceToHost, s));
+        BUILD_HIP(hipMemcpyAsync(rb + kLevelBatch + 5, w.ri_bnd, 6 * 4, hipMemcpyDeviceToHost, s));
         BUILD_HIP(hipStreamSynchronize(s));
-        if (cnts[kLevelBatch] == 0) {
+        if (rb[kLevelBatch] == 0) {
             int d = wl - kLevelBatch;
-            while (d < wl && cnts[d - (wl - kLevelBatch)] != 0) d++;
+            while (d < wl && rb[d - (wl - kLevelBatch)] != 0) d++;
             out.depth = d;
+            const uint32_t *meta = rb + kLevelBatch + 1, *b = rb + kLevelBatch + 5;
+            out.n_wnodes = meta[1];
+            out.dfs_high = meta[2] ? meta[2] : 1u;
+            out.wbound = __builtin_bit_cast(float, meta[3]);
+            auto dec = [](uint32_t u) { return __builtin_bit_cast(float, (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); };
+            for (int a = 0; a < 3; a++) { out.ri_lo[a] = dec(b[a]); out.ri_hi[a] = dec(b[3 + a]); }
             break;
         }
         if (wl >= kMaxLevels) return hipErrorNotSupported;
     }
-    uint32_t meta[4];
-    BUILD_HIP(hipMemcpyAsync(meta, w.meta, sizeof(meta), hipMemcpyDeviceToHost, s));
-    BUILD_HIP(hipStreamSynchronize(s));
-    out.n_wnodes = meta[1];
-    out.dfs_high = meta[2] ? meta[2] : 1u;
-    out.wbound = __builtin_bit_cast(float, meta[3]);
-    return hipSuccess;
-}
-
-hipError_t ri_bounds_device(const float4 *leafbox, uint32_t n, void *ws, float lo[3], float hi[3], hipStream_t s) {
-    BuildWs w;
-    carve(ws, n, &w);
-    const uint32_t init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
-    BUILD_HIP(hipMemcpyAsync(w.ri_bnd, init, sizeof(init), hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_ri_bounds, dim3(nblk(n)), dim3(kB), 0, s, leafbox, n, w.ri_bnd);
-    BUILD_HIP(hipGetLastError());
-    uint32_t b[6];
-    BUILD_HIP(hipMemcpyAsync(b, w.ri_bnd, sizeof(b), hipMemcpyDeviceToHost, s));
-    BUILD_HIP(hipStreamSynchronize(s));
-    auto dec = [](uint32_t u) { return __builtin_bit_cast(float, (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); };
-    for (int a = 0; a < 3; a++) { lo[a] = dec(b[a]); hi[a] = dec(b[3 + a]); }
     return hipSuccess;
 }
 

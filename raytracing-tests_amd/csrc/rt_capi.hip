@@ -469,14 +469,12 @@ int make_inw_wide_device(rt_dev_scene *s, uint32_t n, double *ms) {
     HIP_OK(s->wleaf.reserve(size_t(n) * 8 * sizeof(float)));
     const size_t wsb = rtk::inw_build_workspace_bytes(n);
     HIP_OK(s->build_ws.reserve(wsb));
-    rtk::InwWideDev out{s->wnodes.as<float4>(), s->wrank.as<uint32_t>(), s->wleaf.as<float4>(), 0, 0, 0, 0.0f};
+    rtk::InwWideDev out{s->wnodes.as<float4>(), s->wrank.as<uint32_t>(), s->wleaf.as<float4>(), 0, 0, 0, 0.0f, {}, {}};
     HIP_OK(rtk::inw_wide_build_device(s->nodes.as<float4>(), n, s->build_ws.p, s->build_ws.bytes, out, nullptr));
     if (s->opt.inw_wide_walk) {
-        float lo[3], hi[3];
-        HIP_OK(rtk::ri_bounds_device(s->wleaf.as<float4>(), n, s->build_ws.p, lo, hi, nullptr));
         double dlo[3], dhi[3], inv[3];
         int dim[3];
-        for (int a = 0; a < 3; a++) { dlo[a] = lo[a]; dhi[a] = hi[a]; }
+        for (int a = 0; a < 3; a++) { dlo[a] = out.ri_lo[a]; dhi[a] = out.ri_hi[a]; }
         if (rtamd::ri_grid_dims(dlo, dhi, n, dim, inv)) {
             const size_t nc = size_t(dim[0]) * dim[1] * dim[2];
             HIP_OK(s->ri_cells.reserve((nc + 1) * sizeof(uint32_t)));
@@ -1226,8 +1224,9 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     const int blocks = s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 16 : 15);
     // the top of the wide BVH staged in LDS (768-lane blocks, 3 waves per SIMD);
     // inw_lds_nodes = 0: 256-lane blocks reading every node from L1 / L2 (A/B)
-    // (without the wide walk the stackless LBVH walks read the top of the LBVH from that LDS)
-    const int blocks_ln = o.inw_lds_nodes && (s->n_wnodes || (s->dfs_high && s->sl_ok && o.inw_stackless))
+    // (without the wide walk the stackless LBVH walks read the top of the LBVH from that LDS; the
+    // stack walks run in the same 768-lane instances, with nothing staged)
+    const int blocks_ln = o.inw_lds_nodes && (s->n_wnodes || s->dfs_high)
                               ? s->cus * rtk::resident_blocks_per_cu(s->layout == 4 ? 18 : 17) : 0;
     // inw_ring_pm = 0: k_inw_pm's fold ring in LDS (768-lane blocks), else a global
     // ring of that many entries per wave (1024 for the 256-lane blocks)

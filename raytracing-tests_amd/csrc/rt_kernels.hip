@@ -337,11 +337,20 @@ __device__ __forceinline__ RayRet iow_eval(const IowScene &S, f3 go, f3 gd, f3 t
     return iow_eval_c(S, go, gd, td_id, nd_id, min_t, best, max_t, contrib, c0, c1);
 }
 
-// IOW BVH-stack slot p of a lane (16-bit links): slots 2q and 2q + 1 share the lane's dword in row
-// q, [q][lane][2], so the 32 lanes of an LDS access group always touch 32 different banks, whatever
-// their stack depths ([slot][lane] put two lanes in each dword: a 2-way conflict whenever their
-// depths differ).  b = the lane's pair base, lds + 2 * lane.
+// IOW BVH-stack slot p of a lane (16-bit links), [slot][lane]: two lanes share a dword, so two
+// lanes of an LDS access group whose stack depths differ hit one bank (a 2-way conflict).
+// RT_IOW_BSTK_PAIR (A/B variant, round 5): [slot pair][lane][2], the lane's two slots in its own
+// dword, conflict-free at any depths: C2's LDS bank-conflict cycles fell from 17.5% to 13.0% of the
+// LDS-active cycles, and the frame took 3.8% longer (3,835 / 3,857 against 3,702 / 3,699 ms, same
+// box, profiles/r05_ab_stackless_iow_bstk.json): the address arithmetic of every push and pop costs more
+// than the conflicts did.  b = the lane's base, lds + kBstkLane * lane.
+#ifdef RT_IOW_BSTK_PAIR
 __device__ __forceinline__ short &bslot(short *b, int p) { return b[(p >> 1) * (2 * kBlock) + (p & 1)]; }
+constexpr int kBstkLane = 2;
+#else
+__device__ __forceinline__ short &bslot(short *b, int p) { return b[p * kBlock]; }
+constexpr int kBstkLane = 1;
+#endif
 
 // LaunchRay 03...glsl:196-256.  The reference loops over every object and keeps the first
 // strictly nearer hit, i.e. the minimum t with the lowest index among exact ties.  The BVH
@@ -463,7 +472,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
 }
 
 // Closest hit of one (wave-uniform) ray with the whole wave.  wl: the wave's LDS list, entry k
-// at wl[(k >> 7) * (2 * kBlock) + (k & 127)] (bslot's layout), cap entries (a multiple of 64 * kCoopR).  Returns the
+// at lane k & 63's BVH-stack slot k >> 6 (bslot), cap entries (a multiple of 64 * kCoopR).  Returns the
 // (uniform) winner and its cold record; nbox / nprim are the boxes and objects tested.  The
 // loads of a batch of kCoopR boxes per lane, and a candidate's hot and cold records, are
 // issued together: a lone ray's query costs about two memory latencies, not one per step.
@@ -511,7 +520,7 @@ __device__ void iow_coop_search(const IowScene &S, f3 go, f3 gd, float max_t, sh
                     const unsigned long long cm = __ballot(cand);
                     if (cand) {
                         const uint32_t k = cnt + lanes_below(cm);
-                        wl[(k >> 7) * (2 * kBlock) + (k & 127)] = (short)j;
+                        bslot(wl + kBstkLane * (k & 63), (int)(k >> 6)) = (short)j;
                     }
                     cnt += (uint32_t)__popcll(cm);
                 }
@@ -526,7 +535,7 @@ __device__ void iow_coop_search(const IowScene &S, f3 go, f3 gd, float max_t, sh
         for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
             const uint32_t k = k0 + lane;
             if (k < cnt) {
-                const int j = cull ? (int)wl[(k >> 7) * (2 * kBlock) + (k & 127)] : (int)(jb + k);
+                const int j = cull ? (int)bslot(wl + kBstkLane * (k & 63), (int)(k >> 6)) : (int)(jb + k);
                 const float4 *cold = reinterpret_cast<const float4 *>(S.cold + (size_t)j * kIowCold);
                 const float4 q0 = cold[0], q1 = cold[1];
                 const int was = bj;
@@ -696,7 +705,7 @@ __device__ __forceinline__ void iow_seg_step(const IowScene &S, const Frame &F, 
         return;
     }
     constexpr int kCap = BS * 64;  // the wave's BVH-stack slots, as a list
-    short *wl = bstk - 2 * (threadIdx.x & 63);
+    short *wl = bstk - kBstkLane * (threadIdx.x & 63);
     DBG_T0(F, t_pop);
     SegIn in{};
     if (seg) in = iow_seg_pop(S, K, sidx);
@@ -850,7 +859,7 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
     __shared__ unsigned long long s_dbg[SUB * kBlock / 64][kDbgSlots];
     __shared__ float4 s_nodes[LN ? kIowLdsNodes * 7 : 1];
     const int sb = (int)(threadIdx.x / kBlock), tl = (int)(threadIdx.x % kBlock);
-    short *bstk = lds_bvh + sb * Cfg::BS * kBlock + 2 * tl;  // bslot's layout
+    short *bstk = lds_bvh + sb * Cfg::BS * kBlock + kBstkLane * tl;  // bslot's layout
     const float4 *nodes = iow_stage_nodes<LN>(S, s_nodes);
     Ctr c;
     if (f.dbg) {
@@ -1075,7 +1084,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
     __shared__ unsigned long long s_dbg[SUB * kBlock / 64][kDbgSlots];
     __shared__ float4 s_nodes[LN ? kIowLdsNodes * 7 : 1];
     const int sb = (int)(threadIdx.x / kBlock), tl = (int)(threadIdx.x % kBlock);
-    short *bstk = lds_bvh + sb * Cfg::BS * kBlock + 2 * tl;  // bslot's layout
+    short *bstk = lds_bvh + sb * Cfg::BS * kBlock + kBstkLane * tl;  // bslot's layout
     const float4 *nodes = iow_stage_nodes<LN>(S, s_nodes);
     Ctr c;  // per unit here: written to the unit's record, never flushed
     if (f.dbg) {
@@ -2777,16 +2786,13 @@ __global__ __launch_bounds__(kBlock) void k_inw(Frame f, InwScene S, Chunk ch, C
 // carries another epoch, and the host clears the rings with 0xff bytes (an epoch of 63, never
 // valid) whenever the epoch wraps to 0, so a stale entry never passes for a finished one and no
 // per-frame clear is needed.  Within a frame, slot g mod R last held g - R (R <= 2^16 < 2^26).
-// The fold kernels' framebuffer stores: written once, never read back by the frame, so they go
-// out as streaming (nontemporal) stores and do not push the waves' fold-ring lines out of L2
-typedef float fb_v4 __attribute__((ext_vector_type(4)));
+// The fold kernels' framebuffer stores.  Measured and not kept (round 5): nontemporal stores here
+// raised C5's L2-to-fabric writes from 4.7 to 37 GB per frame (each streaming 16-B store leaves L2
+// as its own partial-line write) at the same frame time.
 __device__ __forceinline__ void fb_store(const Frame &f, size_t o, float4 v) {
-    const fb_v4 x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<fb_v4 *>(f.out_rgba) + o);
+    reinterpret_cast<float4 *>(f.out_rgba)[o] = v;
 }
-__device__ __forceinline__ void depth_store(const Frame &f, size_t o, float d) {
-    __builtin_nontemporal_store(d, f.out_depth + o);
-}
+__device__ __forceinline__ void depth_store(const Frame &f, size_t o, float d) { f.out_depth[o] = d; }
 __device__ __forceinline__ uint32_t ring_tag(const InwScene &S, uint32_t g) {
     return (g & 0x03ffffffu) | S.ring_epoch;
 }

@@ -253,14 +253,14 @@ struct InwWideDev {
     uint32_t n_wnodes, dfs_high;
     int depth;
     float wbound;
+    float ri_lo[3], ri_hi[3];  // bounds of the leaf boxes (the RI grid's extent)
 };
 size_t inw_build_workspace_bytes(uint32_t n);
 hipError_t inw_wide_build_device(const float4 *nodes, uint32_t n, void *ws, size_t ws_bytes, InwWideDev &out,
                                  hipStream_t s);
-// the surrounding-RI grid on the device (rtamd::ri_grid_build's cells and ids): the leaf boxes'
-// bounds (synchronises), then per-cell counts scanned into cells[0..nc] with the total and an
+// the surrounding-RI grid on the device (rtamd::ri_grid_build's cells and ids) over the extent
+// inw_wide_build_device returned: per-cell counts scanned into cells[0..nc] with the total and an
 // over-64 flag read back (synchronises), then the ids
-hipError_t ri_bounds_device(const float4 *leafbox, uint32_t n, void *ws, float lo[3], float hi[3], hipStream_t s);
 size_t ri_scan_temp_bytes(size_t cells);
 hipError_t ri_count_device(const float4 *leafbox, uint32_t n, void *ws, const double lo[3], const double inv[3],
                            const int dim[3], uint32_t *cells, void *tmp, size_t tmp_bytes, uint32_t *total,

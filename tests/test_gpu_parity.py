@@ -276,3 +276,21 @@ def test_debug_path_reports_the_fold_ring(gpu):
     assert p["lds_nodes"] > 5
     p = paths["sm"]
     assert p["kernel"].startswith("k_inw_sm") and p["ring_lds"] == 0 and p["lds_nodes"] > 5
+
+
+def test_iow03_tile_after_full_frame_uses_its_own_records(gpu):
+    """Sample-parallel IOW-03 records are tagged per frame: a fresh scene (rt_render_iow03 builds
+    one per call) whose record buffers reuse a freed scene's memory must not take that scene's
+    finished records for its own.  Render the full frame, then one tile alone, twice: the tile's
+    pixels and ray counts equal the oracle's each time (before the process-wide tags, the tile
+    returned the full frame's colours at its own record indices)."""
+    sc = R.make_scene(R.PRESET_IOW03_FINAL, 20250131, 0, width=120, height=80, spp=9)
+    R.render(sc)
+    p = R.RtParams.from_buffer_copy(sc.params)
+    p.tile_x0, p.tile_y0, p.tile_w, p.tile_h = 40, 16, 16, 16
+    o, _, ost = O.render(sc, p)
+    sl = (slice(16, 32), slice(40, 56))
+    for _ in range(2):
+        g, _, gst = R.render(sc, p)
+        assert compare(g[sl], o[sl])["exact_frac"] == 1.0
+        assert gst["segments"] == ost["segments"], (gst["segments"], ost["segments"])
