@@ -72,18 +72,6 @@ __global__ __launch_bounds__(kB) void k_leaves(const float4 *nodes, uint32_t nn,
     atomicMax(meta + 3, __float_as_uint(wb));  // non-negative: uint order = value order
 }
 
-// leaf counts of the LBVH's internal nodes (each object adds one to every ancestor)
-__global__ __launch_bounds__(kB) void k_leaf_counts(const float4 *nodes, uint32_t n, const uint32_t *leafnode,
-                                                    uint32_t *lcnt) {
-    const uint32_t g = blockIdx.x * kB + threadIdx.x;
-    if (g >= n) return;  // no cross-lane work in this kernel
-    uint32_t i = leafnode[g];
-    while (i != 0u) {
-        i = parent_of(nodes, i);
-        atomicAdd(lcnt + i, 1u);
-    }
-}
-
 // depth-first ranks (01_BVH...glsl:456-460: invert = 0 pops the right child, at the even index,
 // first; invert = 1 the left one): the leaves of every earlier-visited sibling on the path
 __global__ __launch_bounds__(kB) void k_ranks(const float4 *nodes, uint32_t n, const uint32_t *leafnode,
@@ -129,60 +117,193 @@ __device__ __forceinline__ int bin_of(float c, float cmn, float scale) {
     return min(kBins - 1, max(0, (int)((c - cmn) * scale)));
 }
 
-// One level of the binned SAH build.  Task = (node, lo, hi, parent) over ids[lo, hi); a block per
-// task.  A range of one object is a leaf (first child = -object, as the LBVH layout); else the
-// node takes the split of least SAH cost over 3 x (kBins - 1) bin boundaries (a range whose
-// centroids share one bin on every axis splits in the middle), stably partitions its ids, and
-// appends its children (allocated as a contiguous pair) to the next level's tasks.
+// One level of the binned SAH build.  Task = (node, lo, hi, cb) over ids[lo, hi), hi - lo >= 2: the
+// node takes the split of least SAH cost over 3 x (kBins - 1) bin boundaries (ties to the lower
+// (axis, boundary); a range whose centroids share one bin on every axis splits in the middle),
+// stably partitions its ids from ids_in into ids_out (the levels ping-pong between the two
+// arrays: every range of a level is written by its parent's task) and makes its children.
+// Numbering without counters: a range of m objects has 2m - 1 nodes, so a node's descendants own
+// the 2m - 2 ids from cb: its children are the pair cb, cb + 1 (the layout the collapse reads),
+// the left child's descendants follow from cb + 2, the right child's after those.  A child of one
+// object is written as a leaf (first child = -object, as the LBVH layout) by the lane that places
+// the object; the others are appended to the next level's tasks.  Ranges of more than kWaveMax
+// objects take a block, the others one wave (no barriers; the top levels hold the few big
+// ranges, the deep levels thousands of small ones).  Both paths pick the same split: costs are
+// min / max folds and exact counts.
+constexpr uint32_t kWaveMax = 256;
+constexpr int kU = 8;  // loads in flight per lane in the block path's loops
+struct SahBins {
+    uint32_t cnt[3][kBins];
+    uint32_t bb[3][kBins][6];  // orderable bits: lo min, hi max
+};
+__device__ __forceinline__ void bins_clear(SahBins &sb, uint32_t t, uint32_t nt) {
+    for (uint32_t k = t; k < 3u * kBins; k += nt) {
+        sb.cnt[k / kBins][k % kBins] = 0u;
+        for (int j = 0; j < 6; j++) sb.bb[k / kBins][k % kBins][j] = j < 3 ? 0xffffffffu : 0u;
+    }
+}
+__device__ __forceinline__ void bins_add(SahBins &sb, const float *bx, const float *c, const float *cmn,
+                                         const float *scale, const bool *ax_ok) {
+    for (int a = 0; a < 3; a++) {
+        if (!ax_ok[a]) continue;
+        const int b = bin_of(c[a], cmn[a], scale[a]);
+        atomicAdd(&sb.cnt[a][b], 1u);
+        for (int k = 0; k < 3; k++) {
+            atomicMin(&sb.bb[a][b][k], ford(bx[k]));
+            atomicMax(&sb.bb[a][b][3 + k], ford(bx[3 + k]));
+        }
+    }
+}
+__device__ __forceinline__ void load_item(const float *box, const float *cen, uint32_t g, float *bx, float *c) {
+    for (int k = 0; k < 6; k++) bx[k] = box[6 * g + k];
+    for (int k = 0; k < 3; k++) c[k] = cen[3 * g + k];
+}
+__device__ __forceinline__ void write_leaf(float *bin, uint32_t node, const float *box, uint32_t g) {
+    float *o = bin + (size_t)node * 8;
+    for (int k = 0; k < 6; k++) o[k] = box[6 * g + k];
+    o[6] = -(float)g;
+    o[7] = 0.0f;
+}
+// the object placed at position `dst` of a task split at nl: a child of one object is a leaf
+__device__ __forceinline__ void place(uint32_t g, uint32_t dst, const uint4 tk, uint32_t nl, uint32_t *ids_out,
+                                      float *bin, const float *box) {
+    ids_out[dst] = g;
+    const uint32_t lo = tk.y, hi = tk.z;
+    if (nl == 1u && dst == lo) write_leaf(bin, tk.w, box, g);
+    if (hi - lo - nl == 1u && dst == lo + nl) write_leaf(bin, tk.w + 1u, box, g);
+}
+// the task's node record and its internal children's tasks (one lane)
+__device__ __forceinline__ void sah_emit(const uint4 tk, uint32_t nl, const float *nbox, float *bin, uint4 *tout,
+                                         uint32_t *cnt_out) {
+    const uint32_t node = tk.x, lo = tk.y, hi = tk.z, cb = tk.w, nr = hi - lo - nl;
+    float *o = bin + (size_t)node * 8;
+    for (int k = 0; k < 6; k++) o[k] = nbox[k];
+    o[6] = (float)cb;
+    o[7] = 0.0f;
+    const uint32_t k = (nl > 1u ? 1u : 0u) + (nr > 1u ? 1u : 0u);
+    if (!k) return;
+    uint32_t slot = atomicAdd(cnt_out, k);
+    if (nl > 1u) tout[slot++] = make_uint4(cb, lo, lo + nl, cb + 2u);
+    if (nr > 1u) tout[slot] = make_uint4(cb + 1u, lo + nl, hi, cb + 2u + 2u * (nl - 1u));
+}
+__device__ __forceinline__ void bounds_init(float *v) {
+    for (int k = 0; k < 3; k++) { v[k] = v[6 + k] = __builtin_huge_valf(); v[3 + k] = v[9 + k] = -__builtin_huge_valf(); }
+}
+__device__ __forceinline__ void bounds_add(float *v, const float *bx, const float *c) {
+    for (int k = 0; k < 3; k++) {
+        v[k] = fminf(v[k], bx[k]);
+        v[3 + k] = fmaxf(v[3 + k], bx[3 + k]);
+        v[6 + k] = fminf(v[6 + k], c[k]);
+        v[9 + k] = fmaxf(v[9 + k], c[k]);
+    }
+}
+__device__ __forceinline__ void bounds_wave(float *v) {  // butterfly: every lane holds the result
+    for (int k = 0; k < 12; k++) {
+        const bool mx = (k % 6) >= 3;
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float w = __shfl_xor(v[k], off, 64);
+            v[k] = mx ? fmaxf(v[k], w) : fminf(v[k], w);
+        }
+    }
+}
+__device__ __forceinline__ void bin_frame(const float *v, float *cmn, float *scale, bool *ax_ok) {
+    for (int a = 0; a < 3; a++) {
+        cmn[a] = v[6 + a];
+        const float ext = v[9 + a] - cmn[a];
+        ax_ok[a] = ext > 0.0f;
+        scale[a] = ax_ok[a] ? (float)kBins / ext : 0.0f;
+    }
+}
+// least-cost boundary over the bins, one wave: lane k < 31 evaluates boundary k of each axis from
+// prefix / suffix folds over lanes 0..31 (empty bins fold as the identity); returns (axis *
+// (kBins - 1) + boundary, or -1) and the left count in nl
+__device__ __forceinline__ int sah_pick(const SahBins &sb, const bool *ax_ok, uint32_t lane, uint32_t m, uint32_t &nl) {
+    float bc = __builtin_huge_valf();
+    int bi = 0x7fffffff;
+    uint32_t pcnt[3] = {0u, 0u, 0u};
+    const uint32_t l = lane & 31u;
+    for (int a = 0; a < 3; a++) {
+        if (!ax_ok[a]) continue;  // uniform
+        uint32_t c = sb.cnt[a][l];
+        float b[6];
+        for (int j = 0; j < 6; j++)
+            b[j] = c ? fdeo(sb.bb[a][l][j]) : (j < 3 ? __builtin_huge_valf() : -__builtin_huge_valf());
+        uint32_t pc = c, sc = c;
+        float p[6], q[6];
+        for (int j = 0; j < 6; j++) p[j] = q[j] = b[j];
+        for (uint32_t off = 1; off < 32u; off <<= 1) {
+            const uint32_t up = __shfl_up(pc, off, 32), dn = __shfl_down(sc, off, 32);
+            float pu[6], qd[6];
+            for (int j = 0; j < 6; j++) { pu[j] = __shfl_up(p[j], off, 32); qd[j] = __shfl_down(q[j], off, 32); }
+            if (l >= off) {
+                pc += up;
+                for (int j = 0; j < 3; j++) { p[j] = fminf(p[j], pu[j]); p[3 + j] = fmaxf(p[3 + j], pu[3 + j]); }
+            }
+            if (l + off < 32u) {
+                sc += dn;
+                for (int j = 0; j < 3; j++) { q[j] = fminf(q[j], qd[j]); q[3 + j] = fmaxf(q[3 + j], qd[3 + j]); }
+            }
+        }
+        // boundary l: left = bins 0..l (prefix at l), right = bins l+1.. (suffix at l+1)
+        const uint32_t nr = __shfl_down(sc, 1, 32);
+        float r[6];
+        for (int j = 0; j < 6; j++) r[j] = __shfl_down(q[j], 1, 32);
+        pcnt[a] = pc;
+        if (l < (uint32_t)(kBins - 1) && pc && nr) {
+            const float cost = box_area(p[0], p[1], p[2], p[3], p[4], p[5]) * (float)pc +
+                               box_area(r[0], r[1], r[2], r[3], r[4], r[5]) * (float)nr;
+            if (cost < bc) { bc = cost; bi = a * (kBins - 1) + (int)l; }
+        }
+    }
+    for (int off = 32; off >= 1; off >>= 1) {  // least (cost, index)
+        const float c2 = __shfl_xor(bc, off, 64);
+        const int i2 = __shfl_xor(bi, off, 64);
+        if (c2 < bc || (c2 == bc && i2 < bi)) { bc = c2; bi = i2; }
+    }
+    if (!(bc < __builtin_huge_valf())) { nl = m / 2u; return -1; }
+    const int a = bi / (kBins - 1), k = bi % (kBins - 1);
+    nl = __shfl(a == 0 ? pcnt[0] : a == 1 ? pcnt[1] : pcnt[2], k, 64);
+    return bi;
+}
+__device__ __forceinline__ bool goes_left(int best, float c, uint32_t pos, uint32_t nl, float cmn, float scale, int k) {
+    return best >= 0 ? bin_of(c, cmn, scale) <= k : pos < nl;
+}
+
 __global__ __launch_bounds__(kB) void k_sah_level(const uint4 *tin, const uint32_t *cnt_in, uint4 *tout,
-                                                  uint32_t *cnt_out, uint32_t *ids, uint32_t *ids2, const float *box,
-                                                  const float *cen, float *bin, uint32_t *node_ctr) {
+                                                  uint32_t *cnt_out, const uint32_t *ids_in, uint32_t *ids_out,
+                                                  const float *box, const float *cen, float *bin) {
     __shared__ float s_red[12][kB / 64];
-    __shared__ uint32_t s_cnt[3][kBins];
-    __shared__ uint32_t s_bb[3][kBins][6];
-    __shared__ float s_cost[3 * (kBins - 1)];
-    __shared__ uint32_t s_scan[kB];
+    __shared__ SahBins s_bins;
+    __shared__ SahBins s_wbins[kB / 64];
+    __shared__ uint32_t s_wl[kB / 64];
     __shared__ float s_box[12];
     __shared__ int s_split[2];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t ntask = *cnt_in;
+    // big ranges: a block each
     for (uint32_t t = blockIdx.x; t < ntask; t += gridDim.x) {  // uniform per block
         const uint4 tk = tin[t];
-        const uint32_t node = tk.x, lo = tk.y, hi = tk.z, par = tk.w, m = hi - lo;
-        float *o = bin + (size_t)node * 8;
-        if (m == 1u) {
-            if (tid == 0) {
-                const uint32_t g = ids[lo];
-                for (int k = 0; k < 6; k++) o[k] = box[6 * g + k];
-                o[6] = -(float)g;
-                o[7] = (float)par;
-            }
-            continue;
-        }
-        // the node's box and its centroids' bounds
+        const uint32_t lo = tk.y, hi = tk.z, m = hi - lo;
+        if (m <= kWaveMax) continue;
         float v[12];
-        for (int k = 0; k < 3; k++) { v[k] = v[6 + k] = __builtin_huge_valf(); v[3 + k] = v[9 + k] = -__builtin_huge_valf(); }
-        for (uint32_t q = lo + tid; q < hi; q += kB) {
-            const uint32_t g = ids[q];
-            for (int k = 0; k < 3; k++) {
-                v[k] = fminf(v[k], box[6 * g + k]);
-                v[3 + k] = fmaxf(v[3 + k], box[6 * g + 3 + k]);
-                v[6 + k] = fminf(v[6 + k], cen[3 * g + k]);
-                v[9 + k] = fmaxf(v[9 + k], cen[3 * g + k]);
-            }
+        bounds_init(v);
+        for (uint32_t base = lo + tid; base < hi; base += kB * kU) {
+            uint32_t g[kU];
+            for (int u = 0; u < kU; u++) g[u] = base + u * kB < hi ? ids_in[base + u * kB] : 0xffffffffu;
+            for (int u = 0; u < kU; u++)
+                if (g[u] != 0xffffffffu) {
+                    float bx[6], c[3];
+                    load_item(box, cen, g[u], bx, c);
+                    bounds_add(v, bx, c);
+                }
         }
-        for (int k = 0; k < 12; k++) {  // wave reduction, then across the 4 waves
-            const bool mx = (k % 6) >= 3;
-            for (int off = 32; off >= 1; off >>= 1) {
-                const float w = __shfl_xor(v[k], off, 64);
-                v[k] = mx ? fmaxf(v[k], w) : fminf(v[k], w);
-            }
-            if (lane == 0) s_red[k][wv] = v[k];
+        bounds_wave(v);
+        if (lane < 12u) {
+            float x = v[0];
+            for (int k = 1; k < 12; k++) x = lane == (uint32_t)k ? v[k] : x;
+            s_red[lane][wv] = x;
         }
-        if (tid < 3u * kBins) {
-            s_cnt[tid / kBins][tid % kBins] = 0u;
-            for (int k = 0; k < 6; k++) s_bb[tid / kBins][tid % kBins][k] = k < 3 ? 0xffffffffu : 0u;
-        }
+        bins_clear(s_bins, tid, kB);
         __syncthreads();
         if (tid < 12u) {
             const bool mx = (tid % 6u) >= 3u;
@@ -193,143 +314,201 @@ __global__ __launch_bounds__(kB) void k_sah_level(const uint4 *tin, const uint32
         __syncthreads();
         float cmn[3], scale[3];
         bool ax_ok[3];
-        for (int a = 0; a < 3; a++) {
-            cmn[a] = s_box[6 + a];
-            const float ext = s_box[9 + a] - cmn[a];
-            ax_ok[a] = ext > 0.0f;
-            scale[a] = ax_ok[a] ? (float)kBins / ext : 0.0f;
-        }
-        // bins: counts and boxes (orderable bits) per axis
-        for (uint32_t q = lo + tid; q < hi; q += kB) {
-            const uint32_t g = ids[q];
-            for (int a = 0; a < 3; a++) {
-                if (!ax_ok[a]) continue;
-                const int b = bin_of(cen[3 * g + a], cmn[a], scale[a]);
-                atomicAdd(&s_cnt[a][b], 1u);
-                for (int k = 0; k < 3; k++) {
-                    atomicMin(&s_bb[a][b][k], ford(box[6 * g + k]));
-                    atomicMax(&s_bb[a][b][3 + k], ford(box[6 * g + 3 + k]));
-                }
-            }
-        }
-        __syncthreads();
-        // SAH cost of each boundary: area(L) * |L| + area(R) * |R|
-        if (tid < 3u * (kBins - 1)) {
-            const int a = (int)tid / (kBins - 1), k = (int)tid % (kBins - 1);
-            float cost = __builtin_huge_valf();
-            if (ax_ok[a]) {
-                uint32_t nl = 0, nr = 0;
-                float l[6] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf(),
-                              -__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
-                float r[6] = {l[0], l[1], l[2], l[3], l[4], l[5]};
-                for (int b = 0; b < kBins; b++) {
-                    const uint32_t c = s_cnt[a][b];
-                    if (!c) continue;
-                    float *d = b <= k ? l : r;
-                    (b <= k ? nl : nr) += c;
-                    for (int j = 0; j < 3; j++) {
-                        d[j] = fminf(d[j], fdeo(s_bb[a][b][j]));
-                        d[3 + j] = fmaxf(d[3 + j], fdeo(s_bb[a][b][3 + j]));
+        bin_frame(s_box, cmn, scale, ax_ok);
+        // bins: each thread takes a contiguous run of the range (neighbouring ids are often
+        // neighbouring objects, which share bins: spread them over the wave's lanes)
+        {
+            const uint32_t per = (m + kB - 1) / kB, q0 = lo + tid * per, q1 = min(hi, q0 + per);
+            for (uint32_t base = q0; base < q1; base += kU) {
+                uint32_t g[kU];
+                for (int u = 0; u < kU; u++) g[u] = base + u < q1 ? ids_in[base + u] : 0xffffffffu;
+                for (int u = 0; u < kU; u++)
+                    if (g[u] != 0xffffffffu) {
+                        float bx[6], c[3];
+                        load_item(box, cen, g[u], bx, c);
+                        bins_add(s_bins, bx, c, cmn, scale, ax_ok);
                     }
-                }
-                if (nl && nr)
-                    cost = box_area(l[0], l[1], l[2], l[3], l[4], l[5]) * (float)nl +
-                           box_area(r[0], r[1], r[2], r[3], r[4], r[5]) * (float)nr;
             }
-            s_cost[tid] = cost;
         }
         __syncthreads();
-        if (tid == 0) {  // least cost, ties to the lower (axis, boundary)
-            int best = -1;
-            float bc = __builtin_huge_valf();
-            for (int c = 0; c < 3 * (kBins - 1); c++)
-                if (s_cost[c] < bc) { bc = s_cost[c]; best = c; }
-            s_split[0] = best;
-            uint32_t nl = m / 2u;
-            if (best >= 0) {
-                nl = 0;
-                for (int b = 0; b <= best % (kBins - 1); b++) nl += s_cnt[best / (kBins - 1)][b];
-            }
-            s_split[1] = (int)nl;
+        if (wv == 0) {
+            uint32_t nl = 0;
+            const int best = sah_pick(s_bins, ax_ok, lane, m, nl);
+            if (lane == 0) { s_split[0] = best; s_split[1] = (int)nl; }
         }
         __syncthreads();
         const int best = s_split[0];
         const uint32_t nl = (uint32_t)s_split[1];
-        if (best >= 0) {  // stable partition of ids[lo, hi) by side, through ids2
-            const int a = best / (kBins - 1), k = best % (kBins - 1);
-            uint32_t left = 0, right = 0;  // placed so far (uniform)
-            for (uint32_t base = lo; base < hi; base += kB) {
-                const uint32_t q = base + tid;
-                uint32_t g = 0;
-                bool isl = false;
-                if (q < hi) {
-                    g = ids[q];
-                    isl = bin_of(cen[3 * g + a], cmn[a], scale[a]) <= k;
-                }
-                s_scan[tid] = isl ? 1u : 0u;
-                __syncthreads();
-                for (uint32_t off = 1; off < kB; off <<= 1) {  // inclusive scan
-                    const uint32_t x = tid >= off ? s_scan[tid - off] : 0u;
-                    __syncthreads();
-                    s_scan[tid] += x;
-                    __syncthreads();
-                }
-                const uint32_t incl = s_scan[tid], total = s_scan[kB - 1];
-                if (q < hi) {
-                    const uint32_t before = incl - (isl ? 1u : 0u);
-                    ids2[isl ? lo + left + before : lo + nl + right + (tid - before)] = g;
-                }
-                const uint32_t chunk = hi - base < (uint32_t)kB ? hi - base : (uint32_t)kB;
-                left += total;
-                right += chunk - total;
-                __syncthreads();
+        // stable partition by side: a wave per quarter of the range (64-aligned), a count pass,
+        // then each wave places its quarter from the counts of the quarters before it
+        const int a = best >= 0 ? best / (kBins - 1) : 0, k = best >= 0 ? best % (kBins - 1) : 0;
+        const uint32_t seg = ((m + 4u * 64u - 1u) / (4u * 64u)) * 64u;
+        const uint32_t s0 = min(hi, lo + wv * seg), s1 = min(hi, s0 + seg);
+        const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+        uint32_t nleft = 0;
+        for (uint32_t base = s0; base < s1; base += 64u * kU) {
+            float c[kU];
+            for (int u = 0; u < kU; u++) {
+                const uint32_t q = base + 64u * u + lane;
+                c[u] = q < s1 && best >= 0 ? cen[3 * ids_in[q] + a] : 0.0f;
             }
-            for (uint32_t q = lo + tid; q < hi; q += kB) ids[q] = ids2[q];
+            for (int u = 0; u < kU; u++) {
+                const uint32_t q = base + 64u * u + lane;
+                nleft += (uint32_t)__popcll(__ballot(q < s1 && goes_left(best, c[u], q - lo, nl, cmn[a], scale[a], k)));
+            }
         }
-        if (tid == 0) {
-            const uint32_t c0 = atomicAdd(node_ctr, 2u);
-            for (int k = 0; k < 6; k++) o[k] = s_box[k];
-            o[6] = (float)c0;
-            o[7] = (float)par;
-            const uint32_t slot = atomicAdd(cnt_out, 2u);
-            tout[slot] = make_uint4(c0, lo, lo + nl, node);
-            tout[slot + 1] = make_uint4(c0 + 1u, lo + nl, hi, node);
-        }
+        if (lane == 0) s_wl[wv] = nleft;
         __syncthreads();
+        uint32_t left = 0;
+        for (uint32_t w = 0; w < wv; w++) left += s_wl[w];
+        uint32_t right = (s0 - lo) - left;
+        for (uint32_t base = s0; base < s1; base += 64u * kU) {
+            uint32_t g[kU];
+            float c[kU];
+            for (int u = 0; u < kU; u++) {
+                const uint32_t q = base + 64u * u + lane;
+                g[u] = q < s1 ? ids_in[q] : 0u;
+                c[u] = q < s1 && best >= 0 ? cen[3 * g[u] + a] : 0.0f;
+            }
+            for (int u = 0; u < kU; u++) {
+                const uint32_t q = base + 64u * u + lane;
+                const bool has = q < s1, isl = has && goes_left(best, c[u], q - lo, nl, cmn[a], scale[a], k);
+                const uint64_t ml = __ballot(isl), mh = __ballot(has);
+                const uint32_t bl = (uint32_t)__popcll(ml & lt), bh = (uint32_t)__popcll(mh & lt);
+                if (has) place(g[u], isl ? lo + left + bl : lo + nl + right + (bh - bl), tk, nl, ids_out, bin, box);
+                left += (uint32_t)__popcll(ml);
+                right += (uint32_t)(__popcll(mh) - __popcll(ml));
+            }
+        }
+        if (tid == 0) sah_emit(tk, nl, s_box, bin, tout, cnt_out);
+        __syncthreads();  // s_wl, s_box and s_split are the next task's
+    }
+    // small ranges: a wave each
+    SahBins &wb = s_wbins[wv];
+    const uint32_t nw = gridDim.x * (kB / 64);
+    for (uint32_t t = blockIdx.x * (kB / 64) + wv; t < ntask; t += nw) {  // uniform per wave
+        const uint4 tk = tin[t];
+        const uint32_t lo = tk.y, hi = tk.z, m = hi - lo;
+        if (m > kWaveMax) continue;
+        uint32_t g[kWaveMax / 64];
+        for (uint32_t j = 0; j < kWaveMax / 64; j++) {
+            const uint32_t q = lo + lane + 64u * j;
+            g[j] = q < hi ? ids_in[q] : 0u;
+        }
+        float v[12];
+        bounds_init(v);
+        for (uint32_t j = 0; j < kWaveMax / 64; j++)
+            if (lo + lane + 64u * j < hi) {
+                float bx[6], c[3];
+                load_item(box, cen, g[j], bx, c);
+                bounds_add(v, bx, c);
+            }
+        bounds_wave(v);
+        float cmn[3], scale[3];
+        bool ax_ok[3];
+        bin_frame(v, cmn, scale, ax_ok);
+        bins_clear(wb, lane, 64u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t j = 0; j < kWaveMax / 64; j++)
+            if (lo + lane + 64u * j < hi) {
+                float bx[6], c[3];
+                load_item(box, cen, g[j], bx, c);
+                bins_add(wb, bx, c, cmn, scale, ax_ok);
+            }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t nl = 0;
+        const int best = sah_pick(wb, ax_ok, lane, m, nl);
+        const int a = best >= 0 ? best / (kBins - 1) : 0, k = best >= 0 ? best % (kBins - 1) : 0;
+        uint32_t left = 0, right = 0;
+        const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+        for (uint32_t j = 0; j < kWaveMax / 64 && lo + 64u * j < hi; j++) {  // uniform
+            const uint32_t q = lo + lane + 64u * j;
+            const bool has = q < hi;
+            const bool isl = has && goes_left(best, best >= 0 ? cen[3 * g[j] + a] : 0.0f, q - lo, nl, cmn[a], scale[a], k);
+            const uint64_t ml = __ballot(isl), mh = __ballot(has);
+            const uint32_t bl = (uint32_t)__popcll(ml & lt), bh = (uint32_t)__popcll(mh & lt);
+            if (has) place(g[j], isl ? lo + left + bl : lo + nl + right + (bh - bl), tk, nl, ids_out, bin, box);
+            left += (uint32_t)__popcll(ml);
+            right += (uint32_t)(__popcll(mh) - __popcll(ml));
+        }
+        if (lane == 0) {
+            float nb[6];
+            for (int j = 0; j < 6; j++) nb[j] = v[j];
+            sah_emit(tk, nl, nb, bin, tout, cnt_out);
+        }
+        // the bins are reused by the wave's next task: its reads above are done (wave in order)
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
 // One level of the 4-wide collapse (rtamd::bvh4_collapse): a wide node gathers its binary node's
 // children and opens the largest-area internal one until it holds four; internal children become
-// the next level's wide nodes (indices in level order).  Wide node = 10 float4: lx ly lz hx hy hz
-// (SoA over the 4 children), lx ly lz again, the links (int bits: wide index + 1, or -object;
-// an empty slot is a box at 1e30 with link 1e9, culled by every ray).
+// the next level's wide nodes.  Wide node = 10 float4: lx ly lz hx hy hz (SoA over the 4
+// children), lx ly lz again, the links (int bits: wide index + 1, or -object; an empty slot is a
+// box at 1e30 with link 1e9, culled by every ray).  Numbering breadth first without a node
+// counter: level wl + 1's wide nodes follow all earlier levels' (the prefix of the level counts),
+// in the order of their task slots; a wave takes its slots with one atomic.  meta[1] sums the
+// wide nodes (the root counted by the caller).
 __device__ __forceinline__ float bin_area(const float *bin, int i) {
     const float *b = bin + (size_t)i * 8;
     const float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
     return dx * dy + dy * dz + dz * dx;
 }
-__global__ __launch_bounds__(kB) void k_collapse_level(const uint2 *tin, const uint32_t *cnt_in, uint2 *tout,
-                                                       uint32_t *cnt_out, const float *bin, float4 *wnodes,
-                                                       uint32_t *wide_ctr) {
-    const uint32_t t = blockIdx.x * kB + threadIdx.x;
-    if (t >= *cnt_in) return;  // no cross-lane work in this kernel
-    const uint2 tk = tin[t];
+__global__ __launch_bounds__(kB) void k_collapse_level(const uint2 *tin, uint32_t *wlvl_cnt, int wl, uint2 *tout,
+                                                       const float *bin, float4 *wnodes, uint32_t *meta) {
+    const uint32_t t = blockIdx.x * kB + threadIdx.x, lane = threadIdx.x & 63u;
+    const uint32_t ntask = wlvl_cnt[wl];
+    if (blockIdx.x * kB + (threadIdx.x & ~63u) >= ntask) return;  // whole waves only (the scan below)
+    // wide nodes before level wl + 1: the level counts 0..wl
+    uint32_t before = 0;
+    for (int i = (int)lane; i <= wl; i += 64) before += wlvl_cnt[i];
+    for (int off = 32; off >= 1; off >>= 1) before += (uint32_t)__shfl_xor((int)before, off, 64);
+    const bool act = t < ntask;
     auto is_leaf = [&](int i) { return !(bin[(size_t)i * 8 + 6] > 0.1f); };
     auto first = [&](int i) { return (int)bin[(size_t)i * 8 + 6]; };
-    int ch[4] = {first((int)tk.x), first((int)tk.x) + 1, -1, -1};
-    int nch = 2;
-    while (nch < 4) {
-        int pick = -1;
-        for (int k = 0; k < nch; k++)
-            if (!is_leaf(ch[k]) && (pick < 0 || bin_area(bin, ch[k]) > bin_area(bin, ch[pick]))) pick = k;
-        if (pick < 0) break;
-        const int b = ch[pick];
-        for (int k = pick; k < nch - 1; k++) ch[k] = ch[k + 1];
-        ch[nch - 1] = first(b);
-        ch[nch] = first(b) + 1;
-        nch++;
+    int ch[4] = {-1, -1, -1, -1};
+    int nch = 0;
+    uint2 tk = make_uint2(0u, 0u);
+    if (act) {
+        tk = tin[t];
+        ch[0] = first((int)tk.x);
+        ch[1] = ch[0] + 1;
+        nch = 2;
+        while (nch < 4) {
+            int pick = -1;
+            for (int k = 0; k < nch; k++)
+                if (!is_leaf(ch[k]) && (pick < 0 || bin_area(bin, ch[k]) > bin_area(bin, ch[pick]))) pick = k;
+            if (pick < 0) break;
+            const int b = ch[pick];
+            for (int k = pick; k < nch - 1; k++) ch[k] = ch[k + 1];
+            ch[nch - 1] = first(b);
+            ch[nch] = first(b) + 1;
+            nch++;
+        }
     }
+    bool internal[4];
+    uint32_t nk = 0;
+    for (int k = 0; k < 4; k++) {
+        internal[k] = k < nch && !is_leaf(ch[k]);
+        nk += internal[k] ? 1u : 0u;
+    }
+    uint32_t incl = nk;  // inclusive scan of the wave's internal-child counts
+    for (uint32_t off = 1; off < 64u; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    uint32_t base = 0;
+    if (lane == 63u && total) {
+        base = atomicAdd(wlvl_cnt + wl + 1, total);
+        atomicAdd(meta + 1, total);
+    }
+    base = __shfl(base, 63, 64);
+    if (!act) return;
+    uint32_t slot = base + incl - nk;
     float pl[6][4];
     int lk[4];
     for (int k = 0; k < 4; k++) {
@@ -340,10 +519,10 @@ __global__ __launch_bounds__(kB) void k_collapse_level(const uint2 *tin, const u
         }
         const float *bb = bin + (size_t)ch[k] * 8;
         for (int a = 0; a < 6; a++) pl[a][k] = bb[a];
-        if (is_leaf(ch[k])) lk[k] = (int)bb[6];
+        if (!internal[k]) lk[k] = (int)bb[6];
         else {
-            const uint32_t w = atomicAdd(wide_ctr, 1u);
-            tout[atomicAdd(cnt_out, 1u)] = make_uint2((uint32_t)ch[k], w);
+            const uint32_t w = before + slot;
+            tout[slot++] = make_uint2((uint32_t)ch[k], w);
             lk[k] = (int)w + 1;
         }
     }
@@ -356,13 +535,22 @@ __global__ __launch_bounds__(kB) void k_collapse_level(const uint2 *tin, const u
 // ---- surrounding-RI grid (rtamd::ri_grid_build): bounds, per-cell counts, offsets, ids
 __global__ __launch_bounds__(kB) void k_ri_bounds(const float4 *leafbox, uint32_t n, uint32_t *bnd) {
     const uint32_t g = blockIdx.x * kB + threadIdx.x;
-    if (g >= n) return;  // no cross-lane work in this kernel
-    const float4 n0 = leafbox[2 * g], n1 = leafbox[2 * g + 1];
-    const float lo[3] = {n0.x, n0.y, n0.z}, hi[3] = {n0.w, n1.x, n1.y};
-    for (int a = 0; a < 3; a++) {
-        atomicMin(bnd + a, ford(lo[a]));
-        atomicMax(bnd + 3 + a, ford(hi[a]));
+    uint32_t v[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+    if (g < n) {
+        const float4 n0 = leafbox[2 * g], n1 = leafbox[2 * g + 1];
+        v[0] = ford(n0.x); v[1] = ford(n0.y); v[2] = ford(n0.z);
+        v[3] = ford(n0.w); v[4] = ford(n1.x); v[5] = ford(n1.y);
     }
+    for (int off = 32; off >= 1; off >>= 1)  // a wave's bounds, then one atomic per wave and bound
+        for (int a = 0; a < 6; a++) {
+            const uint32_t w = (uint32_t)__shfl_xor((int)v[a], off, 64);
+            v[a] = a < 3 ? min(v[a], w) : max(v[a], w);
+        }
+    if ((threadIdx.x & 63u) == 0u)
+        for (int a = 0; a < 3; a++) {
+            atomicMin(bnd + a, v[a]);
+            atomicMax(bnd + 3 + a, v[3 + a]);
+        }
 }
 struct RiDims { double lo[3], inv[3]; int dim[3]; };
 __device__ __forceinline__ void ri_range(const RiDims &d, float lo_v, float hi_v, int a, int &c0, int &c1) {
@@ -398,7 +586,7 @@ inline uint32_t nblk(size_t n) { return (uint32_t)((n + kB - 1) / kB); }
 // workspace carve-up (256-B aligned pieces)
 struct BuildWs {
     float *box, *cen, *bin;
-    uint32_t *leafnode, *lcnt, *ids, *ids2, *meta, *lvl_cnt, *wlvl_cnt;
+    uint32_t *leafnode, *ids, *ids2, *meta, *lvl_cnt, *wlvl_cnt;
     uint4 *task[2];
     uint2 *wtask[2];
     uint32_t *ri_bnd, *ri_flag;
@@ -416,7 +604,6 @@ static size_t carve(void *ws, uint32_t n, BuildWs *w) {
     t.cen = static_cast<float *>(take((size_t)n * 3 * 4));
     t.bin = static_cast<float *>(take(nn * 8 * 4));
     t.leafnode = static_cast<uint32_t *>(take((size_t)n * 4));
-    t.lcnt = static_cast<uint32_t *>(take(nn * 4));
     t.ids = static_cast<uint32_t *>(take((size_t)n * 4));
     t.ids2 = static_cast<uint32_t *>(take((size_t)n * 4));
     t.meta = static_cast<uint32_t *>(take(16 * 4));
@@ -440,39 +627,36 @@ size_t inw_build_workspace_bytes(uint32_t n) { return n ? carve(reinterpret_cast
         if (e_ != hipSuccess) return e_;                                                  \
     } while (0)
 
-hipError_t inw_wide_build_device(const float4 *nodes, uint32_t n, void *ws, size_t ws_bytes, InwWideDev &out,
-                                 hipStream_t s) {
-    if (n < 2 || !nodes || !ws || ws_bytes < inw_build_workspace_bytes(n) || !out.wnodes || !out.rank || !out.leafbox)
+hipError_t inw_wide_build_device(const float4 *nodes, const uint32_t *lcnt, uint32_t n, void *ws, size_t ws_bytes,
+                                 InwWideDev &out, hipStream_t s) {
+    if (n < 2 || !nodes || !lcnt || !ws || ws_bytes < inw_build_workspace_bytes(n) || !out.wnodes || !out.rank || !out.leafbox)
         return hipErrorInvalidValue;
     BuildWs w;
     carve(ws, n, &w);
     const uint32_t nn = 2 * n - 1;
     BUILD_HIP(hipMemsetAsync(w.meta, 0, 16 * 4, s));
-    BUILD_HIP(hipMemsetAsync(w.lcnt, 0, (size_t)nn * 4, s));
     BUILD_HIP(hipMemsetAsync(w.lvl_cnt, 0, (kMaxLevels + 1) * 4, s));
     BUILD_HIP(hipMemsetAsync(w.wlvl_cnt, 0, (kMaxLevels + 1) * 4, s));
     hipLaunchKernelGGL(k_leaves, dim3(nblk(nn)), dim3(kB), 0, s, nodes, nn, n, out.leafbox, w.box, w.cen, w.leafnode,
                        w.ids, w.meta);
-    hipLaunchKernelGGL(k_leaf_counts, dim3(nblk(n)), dim3(kB), 0, s, nodes, n, w.leafnode, w.lcnt);
-    hipLaunchKernelGGL(k_ranks, dim3(nblk(n)), dim3(kB), 0, s, nodes, n, w.leafnode, w.lcnt, out.rank);
+    hipLaunchKernelGGL(k_ranks, dim3(nblk(n)), dim3(kB), 0, s, nodes, n, w.leafnode, lcnt, out.rank);
     hipLaunchKernelGGL(k_high, dim3(nblk(nn)), dim3(kB), 0, s, nodes, nn, w.meta);
     // the RI grid's bounds (the leaf boxes'), read back with the counts below
     const uint32_t binit[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
     BUILD_HIP(hipMemcpyAsync(w.ri_bnd, binit, sizeof(binit), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_ri_bounds, dim3(nblk(n)), dim3(kB), 0, s, out.leafbox, n, w.ri_bnd);
     BUILD_HIP(hipGetLastError());
-    // binary SAH tree: root task (node 0, all objects); meta[0] = node counter (1: the root)
+    // binary SAH tree: root task (node 0, all objects, its descendants from node 1)
     const uint32_t one = 1u;
-    const uint4 root = make_uint4(0u, 0u, n, 0u);
+    const uint4 root = make_uint4(0u, 0u, n, 1u);
     BUILD_HIP(hipMemcpyAsync(w.task[0], &root, sizeof(root), hipMemcpyHostToDevice, s));
     BUILD_HIP(hipMemcpyAsync(w.lvl_cnt, &one, 4, hipMemcpyHostToDevice, s));
-    BUILD_HIP(hipMemcpyAsync(w.meta, &one, 4, hipMemcpyHostToDevice, s));
     int lvl = 0;
     for (int batch = kSahFirst;; batch = kLevelBatch) {
         for (int k = 0; k < batch && lvl < kMaxLevels; k++, lvl++)
             hipLaunchKernelGGL(k_sah_level, dim3(1024), dim3(kB), 0, s, w.task[lvl & 1], w.lvl_cnt + lvl,
-                               w.task[(lvl + 1) & 1], w.lvl_cnt + lvl + 1, w.ids, w.ids2, w.box, w.cen, w.bin,
-                               w.meta);
+                               w.task[(lvl + 1) & 1], w.lvl_cnt + lvl + 1, (lvl & 1) ? w.ids2 : w.ids,
+                               (lvl & 1) ? w.ids : w.ids2, w.box, w.cen, w.bin);
         BUILD_HIP(hipGetLastError());
         uint32_t pending = 0;
         BUILD_HIP(hipMemcpyAsync(&pending, w.lvl_cnt + lvl, 4, hipMemcpyDeviceToHost, s));
@@ -488,8 +672,8 @@ hipError_t inw_wide_build_device(const float4 *nodes, uint32_t n, void *ws, size
     int wl = 0;
     for (;;) {
         for (int k = 0; k < kLevelBatch && wl < kMaxLevels; k++, wl++)
-            hipLaunchKernelGGL(k_collapse_level, dim3(nblk(n)), dim3(kB), 0, s, w.wtask[wl & 1], w.wlvl_cnt + wl,
-                               w.wtask[(wl + 1) & 1], w.wlvl_cnt + wl + 1, w.bin, out.wnodes, w.meta + 1);
+            hipLaunchKernelGGL(k_collapse_level, dim3(nblk(n)), dim3(kB), 0, s, w.wtask[wl & 1], w.wlvl_cnt, wl,
+                               w.wtask[(wl + 1) & 1], w.bin, out.wnodes, w.meta);
         BUILD_HIP(hipGetLastError());
         // this batch's level counts, the counters (meta) and the RI bounds in one read
         uint32_t rb[kLevelBatch + 1 + 4 + 6];

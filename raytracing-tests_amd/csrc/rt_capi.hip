@@ -178,7 +178,7 @@ struct rt_dev_scene {
     int wdepth = 0;               // levels of the 4-wide culling BVH
     uint32_t n_wnodes = 0;        // its nodes
     bool ri_ok = false;           // the RI grid applies (ri_cells / ri_ids hold it)
-    DevBuf lbvh_ws;               // rt_dev_scene_inw_update: device LBVH workspace
+    DevBuf lbvh_ws, aabb, lcnt;   // rt_dev_scene_inw_update: device LBVH workspace, object boxes, leaf counts
     DevBuf build_ws, ri_fill, ri_tmp;  // ... and the device build of the wide walk and RI grid (rt_build.hip)
     bool last_ln = false;         // the last INW fold launch used the LDS-staged kernels
     bool last_fu = false;         // ... their fused-fma cull instances
@@ -470,7 +470,8 @@ int make_inw_wide_device(rt_dev_scene *s, uint32_t n, double *ms) {
     const size_t wsb = rtk::inw_build_workspace_bytes(n);
     HIP_OK(s->build_ws.reserve(wsb));
     rtk::InwWideDev out{s->wnodes.as<float4>(), s->wrank.as<uint32_t>(), s->wleaf.as<float4>(), 0, 0, 0, 0.0f, {}, {}};
-    HIP_OK(rtk::inw_wide_build_device(s->nodes.as<float4>(), n, s->build_ws.p, s->build_ws.bytes, out, nullptr));
+    HIP_OK(rtk::inw_wide_build_device(s->nodes.as<float4>(), s->lcnt.as<uint32_t>(), n, s->build_ws.p,
+                                      s->build_ws.bytes, out, nullptr));
     if (s->opt.inw_wide_walk) {
         double dlo[3], dhi[3], inv[3];
         int dim[3];
@@ -545,11 +546,12 @@ int update_inw(rt_dev_scene *s, const float *geom, uint32_t n, const float *node
             new (&s->nodes) DevBuf();
             HIP_OK(s->nodes.alloc(nbytes));
         }
-        DevBuf d_aabb;
-        HIP_OK(d_aabb.upload(aabbs, size_t(n) * 6 * sizeof(float)));
+        HIP_OK(s->aabb.store(aabbs, size_t(n) * 6 * sizeof(float)));
         const size_t ws = rtk::lbvh_workspace_bytes(n);
-        if (s->lbvh_ws.bytes < ws) { s->lbvh_ws.~DevBuf(); new (&s->lbvh_ws) DevBuf(); HIP_OK(s->lbvh_ws.alloc(ws)); }
-        HIP_OK(rtk::lbvh_build_device(d_aabb.as<float>(), n, s->nodes.as<float>(), s->lbvh_ws.p, ws, nullptr));
+        HIP_OK(s->lbvh_ws.reserve(ws));
+        if (device_build) HIP_OK(s->lcnt.reserve(size_t(2 * n - 1) * sizeof(uint32_t)));
+        HIP_OK(rtk::lbvh_build_device(s->aabb.as<float>(), n, s->nodes.as<float>(), s->lbvh_ws.p, ws, nullptr,
+                                      device_build ? s->lcnt.as<uint32_t>() : nullptr));
         if (!device_build) {  // the host builders read it
             host_nodes.resize(nbytes / sizeof(float));
             HIP_OK(hipMemcpy(host_nodes.data(), s->nodes.p, nbytes, hipMemcpyDeviceToHost));

@@ -240,9 +240,11 @@ uint32_t units_of(const Frame &f);
 // sample-parallel IOW-03 pass over the units of `mode` (kSpec*)
 hipError_t launch_iow03_spec(const Frame &f, const IowScene &sc, const SpecRecs &R, int mode, const Cont &ct,
                              uint32_t n_units, unsigned *counter, int blocks_cap, hipStream_t s);
-// LBVH build on the device (rt_lbvh.hip); ws = lbvh_workspace_bytes(n) of scratch
+// LBVH build on the device (rt_lbvh.hip); ws = lbvh_workspace_bytes(n) of scratch; lcnt (optional,
+// 2n - 1 entries): every node's leaf count, in the output's (breadth-first) numbering
 size_t lbvh_workspace_bytes(uint32_t n);
-hipError_t lbvh_build_device(const float *aabb, uint32_t n, float *out, void *ws, size_t ws_bytes, hipStream_t s);
+hipError_t lbvh_build_device(const float *aabb, uint32_t n, float *out, void *ws, size_t ws_bytes, hipStream_t s,
+                             uint32_t *lcnt = nullptr);
 // INW wide walk structures built on the device from a device LBVH (rt_build.hip, DESIGN.md
 // "Device build"): 4-wide culling BVH (10 float4 per node, <= n nodes), depth-first ranks (2n),
 // leaf boxes (2n float4); out's scalars are filled in.  Synchronises the stream (level counts).
@@ -256,8 +258,9 @@ struct InwWideDev {
     float ri_lo[3], ri_hi[3];  // bounds of the leaf boxes (the RI grid's extent)
 };
 size_t inw_build_workspace_bytes(uint32_t n);
-hipError_t inw_wide_build_device(const float4 *nodes, uint32_t n, void *ws, size_t ws_bytes, InwWideDev &out,
-                                 hipStream_t s);
+// nodes: the device LBVH (lbvh_build_device), lcnt: its leaf counts (lbvh_build_device's lcnt)
+hipError_t inw_wide_build_device(const float4 *nodes, const uint32_t *lcnt, uint32_t n, void *ws, size_t ws_bytes,
+                                 InwWideDev &out, hipStream_t s);
 // the surrounding-RI grid on the device (rtamd::ri_grid_build's cells and ids) over the extent
 // inw_wide_build_device returned: per-cell counts scanned into cells[0..nc] with the total and an
 // over-64 flag read back (synchronises), then the ids

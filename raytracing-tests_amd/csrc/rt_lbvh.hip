@@ -77,20 +77,25 @@ __global__ void k_scene_box(const float *aabb, uint32_t n, float *part /* blocks
         }
 }
 
-// fold of the block partials in index order (one thread): first-occurrence ties
+// fold of the block partials (one wave): the (value, index) order of `better` is a total order,
+// so the lane-parallel fold picks the element the host's index-order fold picks
 __global__ void k_scene_box_final(const float *part, int blocks, float *box) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (blockIdx.x != 0) return;
+    const int lane = (int)threadIdx.x;  // blocks <= 64 (lbvh_build_device)
     for (int a = 0; a < 6; a++) {
         float v = 0.0f;
         uint32_t id = 0xffffffffu;
-        for (int b = 0; b < blocks; b++) {
-            const float x = part[(size_t)b * 12 + a];
-            const uint32_t j = __float_as_uint(part[(size_t)b * 12 + 6 + a]);
-            if (j == 0xffffffffu) continue;
-            const bool take = id == 0xffffffffu || better(a, x, j, v, id);
+        if (lane < blocks) {
+            v = part[(size_t)lane * 12 + a];
+            id = __float_as_uint(part[(size_t)lane * 12 + 6 + a]);
+        }
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float x = __shfl_xor(v, off, 64);
+            const uint32_t j = (uint32_t)__shfl_xor((int)id, off, 64);
+            const bool take = j != 0xffffffffu && (id == 0xffffffffu || better(a, x, j, v, id));
             if (take) { v = x; id = j; }
         }
-        box[a] = v;
+        if (lane == 0) box[a] = v;
     }
 }
 
@@ -200,16 +205,20 @@ __global__ void k_boxes(const float *aabb, const uint32_t *ids, uint32_t n, cons
     }
 }
 
-// depth and first leaf of every node -> breadth-first key (depth, first leaf)
-__global__ void k_bfs_keys(uint32_t n, const int *parent, const int *left, unsigned long long *key, uint32_t *vals) {
+// depth and first leaf of every node -> breadth-first key (depth, first leaf); the node's leaf
+// count (its leaves are the sorted range first..last)
+__global__ void k_bfs_keys(uint32_t n, const int *parent, const int *left, const int *right, unsigned long long *key,
+                           uint32_t *vals, uint32_t *cnt) {
     const uint32_t v = blockIdx.x * kB + threadIdx.x;
     if (v >= 2 * n - 1) return;
     uint32_t depth = 0;
     for (int p = parent[v]; p >= 0; p = parent[p]) depth++;
-    int first = (int)v;
+    int first = (int)v, last = (int)v;
     while (first >= (int)n) first = left[first];
+    while (last >= (int)n) last = right[last];
     key[v] = ((unsigned long long)depth << 32) | (uint32_t)first;
     vals[v] = v;
+    cnt[v] = (uint32_t)(last - first + 1);
 }
 
 __global__ void k_rank(const uint32_t *order, uint32_t total, uint32_t *rank) {
@@ -219,7 +228,8 @@ __global__ void k_rank(const uint32_t *order, uint32_t total, uint32_t *rank) {
 
 // ConstructLBVH_Buff layout: {bb_min[3], bb_max[3], leftData, rightData} in BFS order
 __global__ void k_write(uint32_t n, const uint32_t *order, const uint32_t *rank, const int *parent, const int *left,
-                        const uint32_t *ids, const float *bmin, const float *bmax, float *out) {
+                        const uint32_t *ids, const float *bmin, const float *bmax, const uint32_t *cnt, float *out,
+                        uint32_t *lcnt) {
     const uint32_t r = blockIdx.x * kB + threadIdx.x;
     if (r >= 2 * n - 1) return;
     const uint32_t v = order[r];
@@ -227,6 +237,7 @@ __global__ void k_write(uint32_t n, const uint32_t *order, const uint32_t *rank,
     for (int a = 0; a < 3; a++) { o[a] = bmin[(size_t)v * 3 + a]; o[3 + a] = bmax[(size_t)v * 3 + a]; }
     o[6] = v >= n ? (float)rank[left[v]] : -(float)ids[v];
     o[7] = parent[v] >= 0 ? (float)rank[parent[v]] : 0.0f;
+    if (lcnt) lcnt[r] = cnt[v];
 }
 
 }  // namespace
@@ -235,7 +246,7 @@ namespace {
 struct LbvhWs {
     float *part, *box;
     unsigned long long *k0, *k1;
-    uint32_t *v0, *v1, *rank;
+    uint32_t *v0, *v1, *rank, *cnt;
     int *parent, *left, *right;
     unsigned *arrive;
     float *bmin, *bmax;
@@ -260,12 +271,14 @@ LbvhWs lbvh_layout(uint32_t n, void *ws) {
     w.bmin = (float *)take(total * 12 + 12);
     w.bmax = (float *)take(total * 12 + 12);
     w.rank = (uint32_t *)take(total * 4 + 4);
+    w.cnt = (uint32_t *)take(total * 4 + 4);
     w.sort_bytes = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, w.sort_bytes, w.k0, w.k1, w.v0, w.v1, (int)total);
     w.sort_tmp = take(w.sort_bytes);
     w.bytes = size_t(p - base);
     return w;
 }
+const uint32_t kOne = 1u;
 __global__ void k_single(const float *aabb, float *out) {  // n == 1: the root is the leaf
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     for (int a = 0; a < 6; a++) out[a] = aabb[a];
@@ -276,10 +289,12 @@ __global__ void k_single(const float *aabb, float *out) {  // n == 1: the root i
 
 size_t lbvh_workspace_bytes(uint32_t n) { return n ? lbvh_layout(n, nullptr).bytes : 0; }
 
-hipError_t lbvh_build_device(const float *aabb, uint32_t n, float *out, void *ws, size_t ws_bytes, hipStream_t s) {
+hipError_t lbvh_build_device(const float *aabb, uint32_t n, float *out, void *ws, size_t ws_bytes, hipStream_t s,
+                             uint32_t *lcnt) {
     if (n == 0) return hipErrorInvalidValue;
     if (n == 1) {
         hipLaunchKernelGGL(k_single, dim3(1), dim3(64), 0, s, aabb, out);
+        if (lcnt) return hipMemcpyAsync(lcnt, &kOne, 4, hipMemcpyHostToDevice, s);
         return hipGetLastError();
     }
     const LbvhWs w = lbvh_layout(n, ws);
@@ -307,13 +322,13 @@ hipError_t lbvh_build_device(const float *aabb, uint32_t n, float *out, void *ws
     if ((e = hipMemsetAsync(arrive, 0, total * 4, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_links, dim3((n - 1 + kB - 1) / kB), dim3(kB), 0, s, k1, n, parent, left, right);
     hipLaunchKernelGGL(k_boxes, dim3(gn), dim3(kB), 0, s, aabb, v1, n, parent, left, right, bmin, bmax, arrive);
-    hipLaunchKernelGGL(k_bfs_keys, dim3(gt), dim3(kB), 0, s, n, parent, left, k0, v0);
+    hipLaunchKernelGGL(k_bfs_keys, dim3(gt), dim3(kB), 0, s, n, parent, left, right, k0, v0, w.cnt);
     if ((e = hipcub::DeviceRadixSort::SortPairs(sort_tmp, sort_bytes, k0, k1, v0, rank, (int)total, 0, 64, s)) !=
         hipSuccess)
         return e;
     // rank[] now holds the BFS order (node ids); invert into v0 = rank of each node
     hipLaunchKernelGGL(k_rank, dim3(gt), dim3(kB), 0, s, rank, (uint32_t)total, v0);
-    hipLaunchKernelGGL(k_write, dim3(gt), dim3(kB), 0, s, n, rank, v0, parent, left, v1, bmin, bmax, out);
+    hipLaunchKernelGGL(k_write, dim3(gt), dim3(kB), 0, s, n, rank, v0, parent, left, v1, bmin, bmax, w.cnt, out, lcnt);
     return hipGetLastError();
 }
 
