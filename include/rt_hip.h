@@ -113,7 +113,9 @@ typedef struct rt_options {
     int inw_ring_pm;        /* pixel-major fold ring: 0 (default) in LDS, 256 entries per wave, beside
                                5 staged nodes; else a global ring of that many entries per wave
                                (power of two >= 64) beside 236 staged nodes */
-    int inw_ring_sm;        /* ... of the sample-major kernel */
+    int inw_ring_sm;        /* sample-major fold ring: 0 (default) in LDS, 256 entries per wave, when the
+                               scene's BVH top fits the 5 nodes staged beside it (nothing lost), else a
+                               global ring of 256; else a global ring of that many entries per wave */
     int inw_stackless;      /* the reference's LBVH walks (closest hit, surrounding RI) without their stack, by
                                the node buffer's parent links, wherever no push could drop; their top
                                nodes staged in LDS when there is no wide walk (DESIGN.md "Stackless") */
@@ -315,7 +317,7 @@ typedef struct rt_path_info {
     int claim_order;
     int ring_entries;     /* fold window of the kernel that ran */
     int iow_bvh;          /* IOW-03: 0 linear loop, 1 culling BVH, 2 culling BVH in LDS */
-    int ring_lds;         /* 1: the fold ring was in LDS (k_inw_pm, inw_ring_pm = 0) */
+    int ring_lds;         /* 1: the fold ring was in LDS (k_inw_pm: inw_ring_pm = 0; k_inw_sm: inw_ring_sm = 0 and a BVH top of <= 5 nodes) */
     int stackless;        /* 1: the reference LBVH walks ran stackless where no push could drop */
     int lbvh_lds_nodes;   /* LBVH nodes the stackless walks read from LDS (no wide walk) */
 } rt_path_info;

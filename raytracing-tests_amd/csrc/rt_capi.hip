@@ -32,7 +32,7 @@ rt_options default_options() {
     std::memset(&o, 0, sizeof(o));
     o.size = sizeof(rt_options);
     o.inw_wide_walk = 1; o.inw_order = 0; o.inw_beams = 1; o.inw_ri_grid = 1; o.inw_lds_nodes = 1;
-    o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 0; o.inw_ring_sm = 256; o.inw_stackless = 1;
+    o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 0; o.inw_ring_sm = 0; o.inw_stackless = 1;
     o.inw_device_build = 1;
     o.iow_spec = 1; o.iow_linear = 0; o.iow_narrow = 0; o.iow_lds_bvh = 1;
     o.iow_leaf_batch = 32;  // 32 measured 2.5% faster on the bench frame than 65 (round 2)
@@ -47,7 +47,7 @@ rt_options default_options() {
 bool options_ok(const rt_options *o) {
     auto pow2 = [](int r) { return r >= 64 && r <= (1 << 16) && (r & (r - 1)) == 0; };
     return o && o->size == sizeof(rt_options) && o->inw_order >= -1 && o->inw_order <= 2 && (o->inw_ring_pm == 0 || pow2(o->inw_ring_pm)) &&
-           pow2(o->inw_ring_sm) && o->iow_leaf_batch >= 1 && o->iow_leaf_batch <= 65 && o->iow_coop_max >= 0 &&
+           (o->inw_ring_sm == 0 || pow2(o->inw_ring_sm)) && o->iow_leaf_batch >= 1 && o->iow_leaf_batch <= 65 && o->iow_coop_max >= 0 &&
            o->rounds_seq >= 0 && o->rounds_seq <= 14 && o->rounds_spec >= 0 && o->rounds_spec <= 14 &&
            o->park_min >= -1 && o->spec_iters >= 0 && o->spec_probe >= 1 && o->spec_heavy >= -1 &&
            o->spec_rounds >= 0 && o->spec_tail_rounds >= 0 && o->spec_tail_budget >= 1 && o->spec_scan >= 0 &&
@@ -184,6 +184,7 @@ struct rt_dev_scene {
     bool last_fu = false;         // ... their fused-fma cull instances
     uint32_t last_force = 0;      // ... its forced order (0: the probe's pick, read back from inw_mode)
     bool last_lring = false;      // ... k_inw_pm's fold ring was in LDS
+    bool last_lring_sm = false;   // ... k_inw_sm's
     char kname[64] = {0};         // the fold kernel's instance name (rt_debug_launches)
     uint32_t last_ring[2] = {0, 0};  // ... its fold windows (pixel-major, sample-major)
     uint32_t ring_frame = 0;         // frames rendered with the current fold rings (their tag epoch)
@@ -1234,9 +1235,15 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // ring of that many entries per wave (1024 for the 256-lane blocks)
     const bool lring = o.inw_ring_pm == 0 && blocks_ln > 0;
     const uint32_t ring_pm = lring ? rtk::kPmLdsRing : uint32_t(o.inw_ring_pm ? o.inw_ring_pm : 1024);
-    const uint32_t ring_sm = uint32_t(o.inw_ring_sm);
+    // inw_ring_sm = 0: k_inw_sm's ring in LDS too when the staging keeps every node it would stage
+    // anyway (a BVH top of at most kPmLdsNodes wide nodes: INW-04's rooms), else a global ring of
+    // 256 entries; a power of two: the global ring of that size
+    const bool fits5 = s->n_wnodes ? s->n_wnodes <= rtk::kPmLdsNodes
+                                   : (s->sl_ok && 2 * size_t(s->n) - 1 <= size_t(rtk::kPmLdsNodes) * 10 / 2);
+    const bool lring_sm = o.inw_ring_sm == 0 && blocks_ln > 0 && fits5;
+    const uint32_t ring_sm = lring_sm ? rtk::kPmLdsRing : uint32_t(o.inw_ring_sm ? o.inw_ring_sm : 256);
     const size_t waves = std::max(size_t(blocks) * (rtk::kBlock / 64), size_t(blocks_ln) * (3 * rtk::kBlock / 64));
-    const size_t ring_bytes = waves * std::max(lring ? 0u : ring_pm, ring_sm) * sizeof(float4);
+    const size_t ring_bytes = waves * std::max(lring ? 0u : ring_pm, lring_sm ? 0u : ring_sm) * sizeof(float4);
     if (s->inw_ring.bytes < ring_bytes) {
         s->inw_ring.~DevBuf();
         new (&s->inw_ring) DevBuf();
@@ -1254,6 +1261,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     set_wide(s, sc);
     sc.ring_epoch = epoch << 26;
     sc.lring = lring ? 1u : 0u;
+    sc.lring_sm = lring_sm ? 1u : 0u;
 #ifdef RT_INW_PARK  // walk parking (experiment): 2 float4 per lane of the fold grid
     {
         const size_t need = waves * 64 * 2 * sizeof(float4);
@@ -1277,6 +1285,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     s->last_force = force;
     s->last_ring[0] = ring_pm;
     s->last_lring = lring;
+    s->last_lring_sm = lring_sm;
     s->last_ring[1] = ring_sm;
     s->last_kernel = s->layout == 4 ? "k_inw_fold<true>" : "k_inw_fold<false>";
     s->last_ln = blocks_ln > 0;
@@ -1534,7 +1543,13 @@ int rt_debug_path(rt_dev_scene *s, rt_path_info *out) {
         if (s->last_lring) P.lds_nodes = std::min(P.lds_nodes, int(rtk::kPmLdsNodes));
         if (s->last_lring) P.lbvh_lds_nodes = std::min(P.lbvh_lds_nodes, int(rtk::kPmLdsNodes * 10 / 2));
     }
-    else if (std::strncmp(name, "k_inw_sm", 8) == 0) { P.order = 2; P.ring_entries = int(s->last_ring[1]); }
+    else if (std::strncmp(name, "k_inw_sm", 8) == 0) {
+        P.order = 2;
+        P.ring_entries = int(s->last_ring[1]);
+        P.ring_lds = s->last_lring_sm ? 1 : 0;
+        if (s->last_lring_sm) P.lds_nodes = std::min(P.lds_nodes, int(rtk::kPmLdsNodes));
+        if (s->last_lring_sm) P.lbvh_lds_nodes = std::min(P.lbvh_lds_nodes, int(rtk::kPmLdsNodes * 10 / 2));
+    }
     if (P.order != 1) { P.beams = 0; P.claim_order = 0; }  // both serve the pixel-major kernel only
     *out = P;
     return RT_OK;
@@ -1648,7 +1663,8 @@ int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {
         auto tf = [](bool b) { return b ? "true" : "false"; };
         const bool fu = s->last_fu, ln = s->last_ln, lights = s->layout == 4;
         if (sm)
-            std::snprintf(s->kname, sizeof(s->kname), "k_inw_sm<%s, %s, %s>", tf(lights), tf(ln), tf(fu));
+            std::snprintf(s->kname, sizeof(s->kname), "k_inw_sm<%s, %s, %s, %s>", tf(lights), tf(ln), tf(fu),
+                          tf(s->last_lring_sm));
         else
             std::snprintf(s->kname, sizeof(s->kname), "k_inw_pm<%s, %s, %s, %s>", tf(lights), tf(ln), tf(fu),
                           tf(s->last_lring));

@@ -3254,16 +3254,20 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
 }
 
 // sample-major stream (see above): entry g = block ordinal b, sample s, pixel p (b * 64 * spp + s * 64 + p)
-template <bool LIGHTS, bool LN = false, bool FU = false>
+// LRING: the fold ring in LDS after the first kPmLdsNodes staged nodes, as k_inw_pm's (InwScene::
+// lring_sm: chosen when the scene's BVH top fits those nodes, so the staging loses nothing)
+template <bool LIGHTS, bool LN = false, bool FU = false, bool LRING = false>
 __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_waves_per_eu(LN ? 3 : (LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES)))) void k_inw_sm(Frame f, InwScene S0, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force, const uint32_t *) {
     if (!inw_sample_major(mode, force)) return;  // the probe picked k_inw_pm for this frame
     constexpr int SUB = LN ? 3 : 1;
+    constexpr bool LR = LN && LRING;
     __shared__ float lds[SUB * kFStack * kBlock];
     InwScene S = S0;
     if constexpr (LN) {
-        const uint32_t n = S.wnodes ? (S.n_wnodes < (uint32_t)kInwLdsNodes ? S.n_wnodes : (uint32_t)kInwLdsNodes) : 0u;
+        const uint32_t cap = LR ? (uint32_t)kPmLdsNodes : (uint32_t)kInwLdsNodes;
+        const uint32_t n = S.wnodes ? (S.n_wnodes < cap ? S.n_wnodes : cap) : 0u;
         for (uint32_t i = threadIdx.x; i < n * (uint32_t)kInwNodeF4; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
-        const uint32_t nb = (!S.wnodes && S.sl) ? min(2u * S.n - 1u, (uint32_t)(kInwLdsNodes * kInwNodeF4 / 2)) : 0u;
+        const uint32_t nb = (!S.wnodes && S.sl) ? min(2u * S.n - 1u, cap * (uint32_t)kInwNodeF4 / 2u) : 0u;
         for (uint32_t i = threadIdx.x; i < 2u * nb; i += SUB * kBlock) g_inw_lnodes[i] = S.nodes[i];
         __syncthreads();
         S.n_lnodes = n;
@@ -3272,8 +3276,11 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     Ctr c;
     FStack K{lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock), 0};
     const uint32_t lane = threadIdx.x & 63u;
+    if constexpr (LR) rmask = kPmLdsRing - 1u;
     const uint32_t rsize = rmask + 1u;
     float4 *wr = ring + (size_t)uni((blockIdx.x * (SUB * kBlock) + threadIdx.x) >> 6) * rsize;
+    // LR: this wave's ring, three planes (r, g, b) of kPmLdsRing floats
+    float *lr = reinterpret_cast<float *>(g_inw_lnodes + kPmLdsNodes * kInwNodeF4) + uni((threadIdx.x >> 6) * (3u * kPmLdsRing));
     const uint32_t spp = (uint32_t)f.spp, mid = spp / 2u, nblk = units_total(f) / 64u;
     const uint32_t E = 64u * spp;  // entries per block
     const float inv = rcp((float)f.spp);
@@ -3295,21 +3302,36 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     for (;;) {
         // ---- fold: lane p adds the finished samples of its pixel, in order (up to 2 per iteration)
         {
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's ring stores have landed (same CU: L1 write-through)
+            if constexpr (!LR) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's ring stores have landed (same CU: L1 write-through)
+            // LR: every issued entry is either held by a busy lane or stored (LDS ops of one wave
+            // complete in order), so the issued entries below the oldest one a busy lane holds are
+            // finished: no tags (the window keeps every unfolded entry from being overwritten)
+            uint32_t hold = 0u;
+            if constexpr (LR) hold = uni(__ockl_wfred_min_u32(busy ? g - (gi - rsize) : 0xffffffffu));
             const uint32_t my_blk = (uint32_t)__shfl((int)blk_slot, (int)(bf & 63u), 64);
             if (bf != nclaimed) {
                 uint32_t gg[2];
                 float4 v[2];
+                bool fin[2];
 #pragma unroll
                 for (int k = 0; k < 2; k++) {
                     const uint32_t sk = sf + (uint32_t)k;
                     gg[k] = bf * E + (sk < spp ? sk : spp - 1u) * 64u + lane;
-                    const bool ok = sk < spp && gg[k] - (gi - rsize) < rsize;  // issued (and inside the window)
-                    v[k] = ok ? wr[gg[k] & rmask] : make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(~ring_tag(S, gg[k])));
+                    const uint32_t rel = gg[k] - (gi - rsize);
+                    const bool ok = sk < spp && rel < rsize;  // issued (and inside the window)
+                    if constexpr (LR) {
+                        fin[k] = ok && rel < hold;
+                        const uint32_t e = gg[k] & rmask;
+                        v[k] = fin[k] ? make_float4(lr[e], lr[kPmLdsRing + e], lr[2u * kPmLdsRing + e], 0.0f)
+                                      : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    } else {
+                        v[k] = ok ? wr[gg[k] & rmask] : make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(~ring_tag(S, gg[k])));
+                        fin[k] = __float_as_uint(v[k].w) == ring_tag(S, gg[k]);
+                    }
                 }
 #pragma unroll
                 for (int k = 0; k < 2; k++) {
-                    if (__float_as_uint(v[k].w) != ring_tag(S, gg[k]) || sf == spp) break;
+                    if (!fin[k] || sf == spp) break;
                     const f3 gv = f3{v[k].x, v[k].y, v[k].z};
                     acc = sf == 0 ? gv : acc + gv;
                     if (++sf == spp) {  // pixel complete: End()'s imageStore (01_BVH...glsl:652)
@@ -3376,7 +3398,10 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                         inw_start_sample(S, f, K, px.x, px.y, s, c);
                     } else {  // a padding slot: an empty sample, folded as zero
                         if ((uint32_t)s == mid && f.out_depth && px.out != (size_t)-1) depth_store(f, px.out, 0.0f);
-                        wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(ring_tag(S, g)));
+                        if constexpr (LR) {
+                            const uint32_t e = g & rmask;
+                            lr[e] = 0.0f; lr[kPmLdsRing + e] = 0.0f; lr[2u * kPmLdsRing + e] = 0.0f;
+                        } else wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(ring_tag(S, g)));
                     }
                 }
                 gi += take;
@@ -3391,8 +3416,14 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             if (f.px_rays) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
         }
         if (busy && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
-            wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
-                                        __uint_as_float(ring_tag(S, g)));
+            if constexpr (LR) {
+                const uint32_t e = g & rmask;
+                lr[e] = __builtin_sqrtf(col.x);
+                lr[kPmLdsRing + e] = __builtin_sqrtf(col.y);
+                lr[2u * kPmLdsRing + e] = __builtin_sqrtf(col.z);
+            } else
+                wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
+                                            __uint_as_float(ring_tag(S, g)));
             if ((uint32_t)s == mid && f.out_depth) depth_store(f, px.out, dep);  // 01_BVH...glsl:667-668
             busy = false;
         }
@@ -3719,6 +3750,7 @@ hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uin
     do {                                                                                                    \
         if (k == 0 && sc.lring) hipLaunchKernelGGL((k_inw_pm<L, true, F, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border); \
         else if (k == 0) hipLaunchKernelGGL((k_inw_pm<L, true, F>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border); \
+        else if (sc.lring_sm) hipLaunchKernelGGL((k_inw_sm<L, true, F, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border); \
         else hipLaunchKernelGGL((k_inw_sm<L, true, F>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border);        \
     } while (0)
             if (sc.layout == 4) {

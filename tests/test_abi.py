@@ -41,7 +41,7 @@ def test_options_roundtrip_and_validation():
     lib = R.load()
     d = R.default_options()
     assert d.size == C.sizeof(R.RtOptions)
-    assert (d.inw_wide_walk, d.inw_order, d.inw_beams, d.inw_ring_pm, d.inw_ring_sm) == (1, 0, 1, 0, 256)
+    assert (d.inw_wide_walk, d.inw_order, d.inw_beams, d.inw_ring_pm, d.inw_ring_sm) == (1, 0, 1, 0, 0)
     assert (d.iow_spec, d.spec_rounds, d.spec_tail_rounds, d.spec_tail_budget) == (1, 24, 60, 3072)
     with R.options(inw_order=2, spec_iters=3) as o:
         g = R.get_options()

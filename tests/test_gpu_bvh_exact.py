@@ -146,6 +146,8 @@ def _same_frames(over, w, h, spp, scene):
     ({"inw_order": 1, "inw_ring_pm": 1024}, INW1, 128, 72, 300),  # the global ring (default: LDS)
     ({"inw_order": 1, "inw_ring_pm": 1024}, INW4, 128, 128, 16),
     ({"inw_order": 2, "inw_ring_sm": 64}, INW1, 128, 72, 20),   # a window of one sample row
+    ({"inw_order": 2, "inw_ring_sm": 256}, INW4, 128, 128, 16),  # global ring (default here: LDS)
+    ({"inw_order": 2, "inw_ring_sm": 64}, INW4, 97, 43, 300),    # a small global window, ragged units
     ({"inw_order": -1}, INW4, 128, 128, 16),
     ({"inw_order": 1}, INW4, 128, 128, 16),
     ({"inw_order": -1, "inw_wide_walk": 0}, INW4, 96, 96, 8),

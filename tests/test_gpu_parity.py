@@ -276,6 +276,33 @@ def test_debug_path_reports_the_fold_ring(gpu):
     assert p["lds_nodes"] > 5
     p = paths["sm"]
     assert p["kernel"].startswith("k_inw_sm") and p["ring_lds"] == 0 and p["lds_nodes"] > 5
+    # INW-04's room (4 wide nodes): the sample-major ring goes to LDS as well (inw_ring_sm = 0),
+    # beside every node the staging would take anyway; a power of two keeps the global ring
+    sc = R.make_scene(R.PRESET_INW04_CORNELL, 7, 0, width=64, height=64, spp=8)
+    s = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, sc.layout, R.fptr(sc.nodes),
+                             R.fptr(sc.lights if sc.n_lights else None), sc.n_lights, sc.params.spp, -1)
+    assert s
+    try:
+        for name, over in (("sm4", {"inw_order": 2}), ("sm4g", {"inw_order": 2, "inw_ring_sm": 256})):
+            o = R.default_options()
+            for k, v in over.items():
+                setattr(o, k, v)
+            assert lib.rt_dev_scene_set_options(s, C.byref(o)) == 0
+            img = torch.zeros((64, 64, 4), dtype=torch.float32, device=dev)
+            ctr = torch.zeros(6, dtype=torch.int64, device=dev)
+            rc = lib.rt_render_image_async(s, C.byref(sc.camera), C.byref(sc.params), img.data_ptr(), None,
+                                           ctr.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            assert rc == 0
+            torch.cuda.synchronize()
+            paths[name] = R.debug_path(s)
+    finally:
+        lib.rt_dev_scene_free(s)
+    print(paths["sm4"], paths["sm4g"])
+    p = paths["sm4"]
+    assert p["kernel"].startswith("k_inw_sm") and p["ring_lds"] == 1 and p["ring_entries"] == 256
+    assert p["lds_nodes"] == 4
+    p = paths["sm4g"]
+    assert p["kernel"].startswith("k_inw_sm") and p["ring_lds"] == 0 and p["lds_nodes"] == 4
 
 
 def test_iow03_tile_after_full_frame_uses_its_own_records(gpu):
