@@ -105,7 +105,8 @@ typedef struct rt_options {
     /* INW (In-Next-Week 01 / 04) */
     int inw_wide_walk;      /* [build] 1: 4-wide culling walk with the reference's leaf tests; 0: the LBVH walk as the shader does it */
     int inw_order;          /* fold kernel: 0 = the probe picks, 1 = pixel-major, 2 = sample-major, -1 = per-pixel k_inw */
-    int inw_beams;          /* per-pixel candidate lists for primary rays (pixel-major frames) */
+    int inw_beams;          /* per-pixel candidate lists for primary rays (pixel-major frames); 1: entries of
+                               32 bits (16-bit object id, entry t rounded down) when ids fit, 2: (id, t) pairs */
     int inw_ri_grid;        /* surrounding-RI queries through the uniform grid */
     int inw_lds_nodes;      /* top of the wide BVH staged in LDS (768-lane blocks) */
     int inw_fused_cull;     /* one fma per culling plane where the error bound holds */

@@ -1191,7 +1191,10 @@ int set_beam(rt_dev_scene *s, const rtk::Frame &f, rtk::InwScene &sc) {
     const double tmin = -Lh / (Ll - d0) - 0.01;
     const double r = d0 * std::fmax(1.0 - tmin / Ll, std::fabs(1.0 - tfar / Ll));
     const double R = r + 2e-3 + 1e-5 * (cam + tfar);
-    const size_t need = size_t(units) * cap * sizeof(uint2), need_n = size_t(units) * 2 * sizeof(uint32_t);
+    // object ids below 2^16: one uint32 per entry (the id, t's high half), else (id, t)
+    const bool b16 = s->n <= 65536u && s->opt.inw_beams != 2;  // inw_beams = 2: the pairs (A/B)
+    const size_t need = size_t(units) * cap * (b16 ? sizeof(uint32_t) : sizeof(uint2)),
+                 need_n = size_t(units) * 2 * sizeof(uint32_t);
     // the lists are an optional speed-up: on a device short of memory the frame runs without them
     size_t free_b = 0, total_b = 0;
     const size_t grow = (s->inw_beam.bytes < need ? need : 0) + (s->inw_beam_n.bytes < need_n ? need_n : 0);
@@ -1210,6 +1213,7 @@ int set_beam(rt_dev_scene *s, const rtk::Frame &f, rtk::InwScene &sc) {
     sc.beam_n = s->inw_beam_n.as<uint32_t>();
     sc.beam_cut = reinterpret_cast<const float *>(s->inw_beam_n.as<uint32_t>() + size_t(units));
     sc.beam_cap = cap;
+    sc.beam16 = b16 ? 1u : 0u;
     sc.beam_R = float(R);
     sc.beam_tmin = float(tmin);
     sc.beam_tfar = float(tfar);

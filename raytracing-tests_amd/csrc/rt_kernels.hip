@@ -2092,6 +2092,7 @@ __device__ float inw_closest_beam(const InwScene &S, const FStack &K, f3 o, f3 d
     uint32_t br = 0xffffffffu;
     const uint32_t *rank = S.rank + (invert ? S.n : 0u);
     const uint2 *list = S.beam + (size_t)unit * S.beam_cap;
+    const uint32_t *list16 = reinterpret_cast<const uint32_t *>(S.beam) + (size_t)unit * S.beam_cap;
     const float kap = S.beam_kappa;
     float lim = bt * kap + 0.01f;
     bool ovf = false;
@@ -2100,7 +2101,12 @@ __device__ float inw_closest_beam(const InwScene &S, const FStack &K, f3 o, f3 d
         bool act = ok && k < n;
         uint2 e = make_uint2(0u, 0u);
         if (act) {
-            e = list[k];
+            // packed entries hold t rounded down (and 0 for a negative entry): the list stays sorted,
+            // and a ray stops at a stored t above lim no earlier than at the exact one
+            if (S.beam16) {
+                const uint32_t p = list16[k];
+                e = make_uint2(p & 0xffffu, p & 0xffff0000u);
+            } else e = list[k];
             act = __uint_as_float(e.y) <= lim;
         }
         if (!__any(act)) break;
@@ -2880,8 +2886,17 @@ __global__ __launch_bounds__(kBeamBlock) void k_inw_beam(Frame f, InwScene S, co
         cur = stk[(--sp) * kBeamBlock];
     }
     if (bad) { nout[u] = kBeamOff; return; }
-    uint2 *dst = const_cast<uint2 *>(S.beam) + (size_t)u * cap;
-    for (uint32_t j = 0; j < nl; j++) dst[j] = L[j * kBeamBlock];
+    if (S.beam16) {  // object ids < 2^16: the id and the high half of max(t, 0) (t rounded down)
+        uint32_t *dst = reinterpret_cast<uint32_t *>(const_cast<uint2 *>(S.beam)) + (size_t)u * cap;
+        for (uint32_t j = 0; j < nl; j++) {
+            const uint2 e = L[j * kBeamBlock];
+            const uint32_t tb = __uint_as_float(e.y) > 0.0f ? e.y : 0u;
+            dst[j] = (e.x & 0xffffu) | (tb & 0xffff0000u);
+        }
+    } else {
+        uint2 *dst = const_cast<uint2 *>(S.beam) + (size_t)u * cap;
+        for (uint32_t j = 0; j < nl; j++) dst[j] = L[j * kBeamBlock];
+    }
     nout[u] = nl;
     cout[u] = cut;
 }

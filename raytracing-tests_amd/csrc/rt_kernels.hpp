@@ -97,7 +97,9 @@ struct InwScene {
     // whose culling box the beam of its primary rays can cross, sorted by the entry t of the
     // central ray into the box inflated by beam_R (k_inw_beam).  beam_n[u] = count (kBeamOff: use
     // the wide walk), beam_cut[u] = every object with an entry below it is listed.
-    const uint2 *beam = nullptr;  // beam_cap entries per unit: object id, entry t (float bits)
+    const uint2 *beam = nullptr;  // beam_cap entries per unit: object id, entry t (float bits); beam16:
+                                  // one uint32 each, id in the low half, t's high half (t rounded down)
+    uint32_t beam16 = 0;
     const uint32_t *beam_n = nullptr;
     const float *beam_cut = nullptr;
     uint32_t beam_cap = 0;

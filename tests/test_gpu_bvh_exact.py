@@ -159,6 +159,7 @@ def _same_frames(over, w, h, spp, scene):
     ({"inw_lds_nodes": 0, "inw_order": 2}, INW4, 128, 128, 16),
     # the per-frame shortcuts of the pixel-major kernel, each off (INW4 forced pixel-major)
     ({"inw_beams": 0}, INW1, 192, 108, 24),
+    ({"inw_beams": 2}, INW1, 192, 108, 24),              # (id, t) pairs (default: 32-bit entries)
     ({"inw_fused_cull": 0}, INW1, 192, 108, 24),
     ({"inw_ri_grid": 0}, INW1, 192, 108, 24),
     ({"inw_claim_order": 0}, INW1, 192, 108, 24),
