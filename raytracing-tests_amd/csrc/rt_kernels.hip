@@ -2083,16 +2083,17 @@ template <bool WANT_NORMAL>
 __device__ float inw_closest_beam(const InwScene &S, const FStack &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
                                   f3 &normal, float &extra, float init_geom, Ctr &c, uint32_t unit, bool &ok) {
     const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};  // the reference's reciprocals (test_aabb)
-    const uint32_t n = S.beam_n[unit];
-    ok = n != kBeamOff && K.size + S.dfs_high <= (uint32_t)kFStack && __builtin_isfinite(id.x) &&
+    const uint32_t nw = S.beam_n[unit], n = nw & 0xffu;  // k_inw_beam: offset in the block's region << 8 | count
+    ok = nw != kBeamOff && K.size + S.dfs_high <= (uint32_t)kFStack && __builtin_isfinite(id.x) &&
          __builtin_isfinite(id.y) && __builtin_isfinite(id.z) && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
     const float tlim0 = tlim;
     float bt = tlim0;
     int bg = -1;
     uint32_t br = 0xffffffffu;
     const uint32_t *rank = S.rank + (invert ? S.n : 0u);
-    const uint2 *list = S.beam + (size_t)unit * S.beam_cap;
-    const uint32_t *list16 = reinterpret_cast<const uint32_t *>(S.beam) + (size_t)unit * S.beam_cap;
+    const size_t lbase = (size_t)(unit & ~63u) * S.beam_cap + (nw >> 8);
+    const uint2 *list = S.beam + lbase;
+    const uint32_t *list16 = reinterpret_cast<const uint32_t *>(S.beam) + lbase;
     const float kap = S.beam_kappa;
     float lim = bt * kap + 0.01f;
     bool ovf = false;
@@ -2824,81 +2825,92 @@ __global__ __launch_bounds__(kBeamBlock) void k_inw_beam(Frame f, InwScene S, co
     if (inw_sample_major(mode, force)) return;
     __shared__ int st[kBeamStack * kBeamBlock];
     __shared__ uint2 lst[kBeamCapMax * kBeamBlock];
-    const uint32_t u = blockIdx.x * kBeamBlock + threadIdx.x;
-    if (u >= units_total(f)) return;
+    const uint32_t u = blockIdx.x * kBeamBlock + threadIdx.x, lane = threadIdx.x & 63u;
+    if (u >= units_total(f)) return;  // whole waves (units come in 8x8 blocks of 64)
     const UnitPix px = unit_pixel(f, u);
     uint32_t *nout = const_cast<uint32_t *>(S.beam_n);
     float *cout = const_cast<float *>(S.beam_cut);
-    if (!px.in_image) { nout[u] = 0u; cout[u] = kMiss; return; }
-    const f3 cd = inw_pixel_dir(f, px.x, px.y);
-    const f3 o = mk(f.pos[0], f.pos[1], f.pos[2]) + cd;
-    const f3 id = f3{rcp(cd.x), rcp(cd.y), rcp(cd.z)};
-    if (!(__builtin_isfinite(id.x) && __builtin_isfinite(id.y) && __builtin_isfinite(id.z))) { nout[u] = kBeamOff; return; }
-    const float R = S.beam_R, t0 = S.beam_tmin, t1 = S.beam_tfar;
     const uint32_t cap = S.beam_cap;
-    // near / far planes of each axis for this direction, inflated outward by R
-    const uint32_t ox = cd.x < 0.0f ? 3u : 0u, oy = cd.y < 0.0f ? 4u : 1u, oz = cd.z < 0.0f ? 5u : 2u;
-    const f3 rn = f3{cd.x < 0.0f ? R : -R, cd.y < 0.0f ? R : -R, cd.z < 0.0f ? R : -R};
-    int *stk = st + threadIdx.x;
     uint2 *L = lst + threadIdx.x;
-    int sp = 0, cur = S.wroot;
     uint32_t nl = 0;
     float cut = kMiss;
-    bool bad = false;
-    for (;;) {
-        const float4 *nd = S.wnodes + kInwNodeF4 * (cur - 1);
-        const float4 nx = nd[ox], fx = nd[ox + 3], ny = nd[oy], fy = nd[oy + 3], nz = nd[oz], fz = nd[oz + 3];
-        const float4 lk = nd[9];
-        const float nxa[4] = {nx.x, nx.y, nx.z, nx.w}, fxa[4] = {fx.x, fx.y, fx.z, fx.w};
-        const float nya[4] = {ny.x, ny.y, ny.z, ny.w}, fya[4] = {fy.x, fy.y, fy.z, fy.w};
-        const float nza[4] = {nz.x, nz.y, nz.z, nz.w}, fza[4] = {fz.x, fz.y, fz.z, fz.w};
-        const int lka[4] = {__float_as_int(lk.x), __float_as_int(lk.y), __float_as_int(lk.z), __float_as_int(lk.w)};
+    bool off = false;
+    if (px.in_image) {
+        const f3 cd = inw_pixel_dir(f, px.x, px.y);
+        const f3 o = mk(f.pos[0], f.pos[1], f.pos[2]) + cd;
+        const f3 id = f3{rcp(cd.x), rcp(cd.y), rcp(cd.z)};
+        off = !(__builtin_isfinite(id.x) && __builtin_isfinite(id.y) && __builtin_isfinite(id.z));
+        const float R = S.beam_R, t0 = S.beam_tmin, t1 = S.beam_tfar;
+        // near / far planes of each axis for this direction, inflated outward by R
+        const uint32_t ox = cd.x < 0.0f ? 3u : 0u, oy = cd.y < 0.0f ? 4u : 1u, oz = cd.z < 0.0f ? 5u : 2u;
+        const f3 rn = f3{cd.x < 0.0f ? R : -R, cd.y < 0.0f ? R : -R, cd.z < 0.0f ? R : -R};
+        int *stk = st + threadIdx.x;
+        int sp = 0, cur = S.wroot;
+        while (!off) {
+            const float4 *nd = S.wnodes + kInwNodeF4 * (cur - 1);
+            const float4 nx = nd[ox], fx = nd[ox + 3], ny = nd[oy], fy = nd[oy + 3], nz = nd[oz], fz = nd[oz + 3];
+            const float4 lk = nd[9];
+            const float nxa[4] = {nx.x, nx.y, nx.z, nx.w}, fxa[4] = {fx.x, fx.y, fx.z, fx.w};
+            const float nya[4] = {ny.x, ny.y, ny.z, ny.w}, fya[4] = {fy.x, fy.y, fy.z, fy.w};
+            const float nza[4] = {nz.x, nz.y, nz.z, nz.w}, fza[4] = {fz.x, fz.y, fz.z, fz.w};
+            const int lka[4] = {__float_as_int(lk.x), __float_as_int(lk.y), __float_as_int(lk.z), __float_as_int(lk.w)};
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const float te = fmaxf(fmaxf(((nxa[k] + rn.x) - o.x) * id.x, ((nya[k] + rn.y) - o.y) * id.y),
-                                   ((nza[k] + rn.z) - o.z) * id.z);
-            const float tx = fminf(fminf(((fxa[k] - rn.x) - o.x) * id.x, ((fya[k] - rn.y) - o.y) * id.y),
-                                   ((fza[k] - rn.z) - o.z) * id.z);
-            if (!(fmaxf(te, t0) <= fminf(tx, t1))) continue;
-            const int l = lka[k];
-            if (l > 0) {
-                if (sp == kBeamStack) bad = true;
-                else stk[(sp++) * kBeamBlock] = l;
-            } else {  // keep the cap smallest entries, sorted (insertion)
-                float tv = te;
-                uint32_t gv = (uint32_t)(-l);
-                if (nl == cap) {
-                    const float last = __uint_as_float(L[(cap - 1) * kBeamBlock].y);
-                    if (!(tv < last)) { cut = fminf(cut, tv); continue; }
-                    cut = fminf(cut, last);
-                    nl--;
+            for (int k = 0; k < 4; k++) {
+                const float te = fmaxf(fmaxf(((nxa[k] + rn.x) - o.x) * id.x, ((nya[k] + rn.y) - o.y) * id.y),
+                                       ((nza[k] + rn.z) - o.z) * id.z);
+                const float tx = fminf(fminf(((fxa[k] - rn.x) - o.x) * id.x, ((fya[k] - rn.y) - o.y) * id.y),
+                                       ((fza[k] - rn.z) - o.z) * id.z);
+                if (!(fmaxf(te, t0) <= fminf(tx, t1))) continue;
+                const int l = lka[k];
+                if (l > 0) {
+                    if (sp == kBeamStack) off = true;
+                    else stk[(sp++) * kBeamBlock] = l;
+                } else {  // keep the cap smallest entries, sorted (insertion)
+                    float tv = te;
+                    uint32_t gv = (uint32_t)(-l);
+                    if (nl == cap) {
+                        const float last = __uint_as_float(L[(cap - 1) * kBeamBlock].y);
+                        if (!(tv < last)) { cut = fminf(cut, tv); continue; }
+                        cut = fminf(cut, last);
+                        nl--;
+                    }
+                    uint32_t j = nl;
+                    while (j > 0 && __uint_as_float(L[(j - 1) * kBeamBlock].y) > tv) {
+                        L[j * kBeamBlock] = L[(j - 1) * kBeamBlock];
+                        j--;
+                    }
+                    L[j * kBeamBlock] = make_uint2(gv, __float_as_uint(tv));
+                    nl++;
                 }
-                uint32_t j = nl;
-                while (j > 0 && __uint_as_float(L[(j - 1) * kBeamBlock].y) > tv) {
-                    L[j * kBeamBlock] = L[(j - 1) * kBeamBlock];
-                    j--;
-                }
-                L[j * kBeamBlock] = make_uint2(gv, __float_as_uint(tv));
-                nl++;
             }
+            if (off || sp == 0) break;
+            cur = stk[(--sp) * kBeamBlock];
         }
-        if (bad || sp == 0) break;
-        cur = stk[(--sp) * kBeamBlock];
     }
-    if (bad) { nout[u] = kBeamOff; return; }
+    // The block's 64 lists packed densely in its region of 64 * cap entries, in unit order (the
+    // fold kernel claims a block's pixels one after another, so their lists share cache lines):
+    // beam_n[u] = offset in the region << 8 | count
+    const uint32_t cnt = off ? 0u : nl;
+    uint32_t incl = cnt;
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    const uint32_t at = incl - cnt;
+    const size_t base = (size_t)(u & ~63u) * cap + at;
     if (S.beam16) {  // object ids < 2^16: the id and the high half of max(t, 0) (t rounded down)
-        uint32_t *dst = reinterpret_cast<uint32_t *>(const_cast<uint2 *>(S.beam)) + (size_t)u * cap;
-        for (uint32_t j = 0; j < nl; j++) {
+        uint32_t *dst = reinterpret_cast<uint32_t *>(const_cast<uint2 *>(S.beam)) + base;
+        for (uint32_t j = 0; j < cnt; j++) {
             const uint2 e = L[j * kBeamBlock];
             const uint32_t tb = __uint_as_float(e.y) > 0.0f ? e.y : 0u;
             dst[j] = (e.x & 0xffffu) | (tb & 0xffff0000u);
         }
     } else {
-        uint2 *dst = const_cast<uint2 *>(S.beam) + (size_t)u * cap;
-        for (uint32_t j = 0; j < nl; j++) dst[j] = L[j * kBeamBlock];
+        uint2 *dst = const_cast<uint2 *>(S.beam) + base;
+        for (uint32_t j = 0; j < cnt; j++) dst[j] = L[j * kBeamBlock];
     }
-    nout[u] = nl;
-    cout[u] = cut;
+    nout[u] = off ? kBeamOff : (at << 8) | nl;
+    cout[u] = px.in_image ? cut : kMiss;
 }
 
 template <bool LIGHTS>

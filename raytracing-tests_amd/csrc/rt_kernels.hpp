@@ -95,8 +95,10 @@ struct InwScene {
     float4 *park = nullptr;   // RT_INW_PARK builds: 2 float4 of parked walk state per lane of the fold grid
     // Pixel beams (DESIGN.md §5 "Pixel beams"; null beam = off): for each pixel unit, the objects
     // whose culling box the beam of its primary rays can cross, sorted by the entry t of the
-    // central ray into the box inflated by beam_R (k_inw_beam).  beam_n[u] = count (kBeamOff: use
-    // the wide walk), beam_cut[u] = every object with an entry below it is listed.
+    // central ray into the box inflated by beam_R (k_inw_beam).  The 64 lists of an 8x8 block are
+    // packed in unit order in the block's region of 64 * beam_cap entries: beam_n[u] = offset in
+    // the region << 8 | count (kBeamOff: use the wide walk), beam_cut[u] = every object with an
+    // entry below it is listed.
     const uint2 *beam = nullptr;  // beam_cap entries per unit: object id, entry t (float bits); beam16:
                                   // one uint32 each, id in the low half, t's high half (t rounded down)
     uint32_t beam16 = 0;
