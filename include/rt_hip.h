@@ -123,6 +123,8 @@ typedef struct rt_options {
     int inw_device_build;   /* rt_dev_scene_inw_update with the LBVH built on the device: the wide walk's
                                4-wide BVH (binned SAH), ranks and RI grid built on the device too (0: on
                                the host from the read-back LBVH, as rt_dev_scene_inw does) */
+    int inw_claim_xcd;      /* pixel-major claims from 8 queues, one per XCD (an 8x8 block's pixels are
+                               written by one XCD's L2, whole lines), idle XCDs taking from the others */
     /* IOW-03 (In-One-Weekend 03) */
     int iow_spec;           /* sample-parallel speculation (0: the sequential per-pixel kernel) */
     int iow_linear;         /* [build] the shader's linear object loop instead of the culling BVH */

@@ -33,7 +33,7 @@ rt_options default_options() {
     o.size = sizeof(rt_options);
     o.inw_wide_walk = 1; o.inw_order = 0; o.inw_beams = 1; o.inw_ri_grid = 1; o.inw_lds_nodes = 1;
     o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 0; o.inw_ring_sm = 0; o.inw_stackless = 1;
-    o.inw_device_build = 1;
+    o.inw_device_build = 1; o.inw_claim_xcd = 1;
     o.iow_spec = 1; o.iow_linear = 0; o.iow_narrow = 0; o.iow_lds_bvh = 1;
     o.iow_leaf_batch = 32;  // 32 measured 2.5% faster on the bench frame than 65 (round 2)
     o.iow_coop_max = 4; o.iow_chunks_lpt = 0;
@@ -265,7 +265,7 @@ int build_tables(rt_dev_scene *s, int spp) {
     s->s_stop = spp;
     for (int i = 0; i < spp; i++)
         if (ring[size_t(i) * 2] < 0) { s->s_stop = i; break; }
-    HIP_OK(s->counter.alloc(256));  // queue counters 64 B apart (the INW fold launches use two)
+    HIP_OK(s->counter.alloc(1024));  // queue counters 64 B apart (the INW fold launches: two, + 8 XCD queues)
     HIP_OK(s->inw_mode.alloc(64));
     return RT_OK;
 }
@@ -1266,6 +1266,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     sc.ring_epoch = epoch << 26;
     sc.lring = lring ? 1u : 0u;
     sc.lring_sm = lring_sm ? 1u : 0u;
+    sc.xcdq = o.inw_claim_xcd ? 1u : 0u;
 #ifdef RT_INW_PARK  // walk parking (experiment): 2 float4 per lane of the fold grid
     {
         const size_t need = waves * 64 * 2 * sizeof(float4);

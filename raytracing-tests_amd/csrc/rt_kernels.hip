@@ -3066,6 +3066,8 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     uint32_t gf = 0, jf = 0, sf = 0;   // next entry to fold
     uint32_t nclaimed = 0;             // pixel ordinals claimed so far
     bool qdone = false;
+    uint32_t xq = 0;                   // S.xcdq: queues found empty (from this block's XCD on)
+    const uint32_t nblk8 = total / 64u;  // 8x8 blocks (units come in whole blocks)
     f3 acc = f3{0, 0, 0};              // running End() sum of pixel jf (the same in every lane)
     uint32_t pix_slot = 0xffffffffu;   // lane l: the unit of the claimed ordinal j with j % 64 == l
     // per lane: the sample it traces
@@ -3156,18 +3158,39 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             if (need > jf + 64u) need = jf + 64u;
             if (need > nclaimed) {
                 const uint32_t want = need - nclaimed;
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(counter, want);
-                base = uni((uint32_t)__shfl((int)base, 0, 64));
-                uint32_t got = want;
-                if (base >= total) { got = 0; qdone = true; }
-                else if (base + want >= total) { got = total - base; qdone = true; }
+                uint32_t base = 0, got = 0, qx = 0;
+                if (S.xcdq) {
+                    // per-XCD queues (rt_options.inw_claim_xcd): queue x holds the blocks of claim
+                    // ordinal b = x mod 8, in claim order, so a block's pixels -- whole 128-B lines of
+                    // the framebuffer per block row -- are written through one XCD's L2 (workgroups go
+                    // to the XCDs round robin); a wave whose queue is empty takes from the next ones
+                    while (xq < 8u) {  // wave-uniform
+                        qx = (blockIdx.x + xq) & 7u;
+                        const uint32_t nb = nblk8 > qx ? (nblk8 - qx + 7u) >> 3 : 0u, qt = nb * 64u;
+                        if (lane == 0) base = atomicAdd(counter + 64u + 16u * qx, want);
+                        base = uni((uint32_t)__shfl((int)base, 0, 64));
+                        if (base < qt) {
+                            got = min(want, qt - base);
+                            if (base + want >= qt) xq++;
+                            break;
+                        }
+                        xq++;
+                    }
+                    if (xq >= 8u) qdone = true;
+                } else {
+                    if (lane == 0) base = atomicAdd(counter, want);
+                    base = uni((uint32_t)__shfl((int)base, 0, 64));
+                    got = want;
+                    if (base >= total) { got = 0; qdone = true; }
+                    else if (base + want >= total) { got = total - base; qdone = true; }
+                }
 #ifdef RT_DIAG_SPLIT
                 if (qdone && t_qd == 0) t_qd = wall_clock64();
 #endif
                 const uint32_t rel = (lane - nclaimed) & 63u;
                 if (rel < got) {  // ordinal -> unit through the claim order (block-wise)
-                    const uint32_t u = base + rel;
+                    uint32_t u = base + rel;
+                    if (S.xcdq) u = (((u >> 6) << 3) + qx) * 64u + (u & 63u);  // queue ordinal -> claim ordinal
                     pix_slot = border ? border[u >> 6] * 64u + (u & 63u) : u;
                 }
                 nclaimed += got;
@@ -3769,6 +3792,8 @@ hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uin
     if (sc.beam && (e = launch_inw_beam(f, sc, mode, force, s)) != hipSuccess) return e;
     for (int k = 0; k < 2; k++) {  // (pm, then sm) each with its own queue counter
         if ((e = hipMemsetAsync(counter + 16 * k, 0, sizeof(unsigned), s)) != hipSuccess) return e;
+        if (k == 0 && sc.xcdq && (e = hipMemsetAsync(counter + 64, 0, 8 * 16 * sizeof(unsigned), s)) != hipSuccess)
+            return e;  // k_inw_pm's per-XCD queues
         const uint32_t rm = (k == 0 ? ring_pm : ring_sm) - 1u;
         unsigned *ctr = counter + 16 * k;
         if (blocks_ln > 0) {  // the LDS-staged BVH top (768-lane blocks); FU: the fused-fma cull

@@ -91,6 +91,7 @@ struct InwScene {
     int fused = 0;          // the wide walk culls with one fma per plane (cull4nf<true>; set per frame)
     uint32_t lring = 0;       // k_inw_pm (768-lane instances): the fold ring in LDS (kPmLdsRing entries per wave)
     uint32_t lring_sm = 0;    // k_inw_sm (768-lane instances): the same
+    uint32_t xcdq = 0;        // k_inw_pm claims from per-XCD queues (rt_options.inw_claim_xcd)
     uint32_t ring_epoch = 0;  // fold-ring tags: the frame's epoch (0..62) << 26 (ring_tag, rt_kernels.hip)
     float4 *park = nullptr;   // RT_INW_PARK builds: 2 float4 of parked walk state per lane of the fold grid
     // Pixel beams (DESIGN.md §5 "Pixel beams"; null beam = off): for each pixel unit, the objects

@@ -74,7 +74,7 @@ class RtOptions(C.Structure):
     """rt_options (include/rt_hip.h): the exact strategy switches of the render path."""
     _fields_ = [("size", C.c_uint32)] + [(n, C.c_int) for n in (
         "inw_wide_walk", "inw_order", "inw_beams", "inw_ri_grid", "inw_lds_nodes", "inw_fused_cull",
-        "inw_claim_order", "inw_ring_pm", "inw_ring_sm", "inw_stackless", "inw_device_build",
+        "inw_claim_order", "inw_ring_pm", "inw_ring_sm", "inw_stackless", "inw_device_build", "inw_claim_xcd",
         "iow_spec", "iow_linear", "iow_narrow", "iow_lds_bvh", "iow_leaf_batch", "iow_coop_max", "iow_chunks_lpt",
         "rounds_seq", "rounds_spec", "park_min",
         "spec_iters", "spec_probe", "spec_heavy", "spec_rounds", "spec_tail_rounds", "spec_tail_budget", "spec_scan",

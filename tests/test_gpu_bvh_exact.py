@@ -163,6 +163,8 @@ def _same_frames(over, w, h, spp, scene):
     ({"inw_fused_cull": 0}, INW1, 192, 108, 24),
     ({"inw_ri_grid": 0}, INW1, 192, 108, 24),
     ({"inw_claim_order": 0}, INW1, 192, 108, 24),
+    ({"inw_claim_xcd": 0}, INW1, 192, 108, 24),          # one claim queue (default: one per XCD)
+    ({"inw_claim_xcd": 0, "inw_claim_order": 0}, INW1, 97, 43, 7),
     ({"inw_beams": 0, "inw_order": 1}, INW4, 128, 128, 16),
     ({"inw_fused_cull": 0, "inw_order": 1}, INW4, 128, 128, 16),
     ({"inw_ri_grid": 0, "inw_order": 1}, INW4, 128, 128, 16),
