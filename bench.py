@@ -645,10 +645,12 @@ def main():
             "path": path,
             "options": {k: v for k, v in R.get_options().as_dict().items()
                         if v != R.default_options().as_dict()[k]} or "defaults",
-            "timed_region": ("per step: rt_pack_inw + rt_dev_scene_inw_update (records, device LBVH, host wide "
-                             "walk + RI grid, uploads) + rt_render_tiles_async of one full frame (the reference's "
-                             "whole redraw, RT_Base::OnUpdateBase); only the first frame's device allocations are "
-                             "outside it") if args.rebuild else
+            "timed_region": ("per step: rt_pack_inw + rt_dev_scene_inw_update (records, device LBVH, the wide "
+                             "walk's BVH + ranks + RI grid built on the "
+                             + ("device" if R.get_options().inw_device_build else "host, uploads")
+                             + ") + rt_render_tiles_async of one full frame (the reference's whole redraw, "
+                             "RT_Base::OnUpdateBase); only the first frame's device allocations are outside it")
+                            if args.rebuild else
                             ("rt_render_tiles_async of one full frame per step (+ the RCCL gather and rank 0's "
                              "frame assembly at N > 1) on a device scene built before timing: the host "
                              "acceleration structures, the scene upload and the device allocations of the first "
