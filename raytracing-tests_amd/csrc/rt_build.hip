@@ -128,10 +128,12 @@ __device__ __forceinline__ int bin_of(float c, float cmn, float scale) {
 // object is written as a leaf (first child = -object, as the LBVH layout) by the lane that places
 // the object; the others are appended to the next level's tasks.  Ranges of more than kWaveMax
 // objects take a block, the others one wave (no barriers; the top levels hold the few big
-// ranges, the deep levels thousands of small ones).  Both paths pick the same split: costs are
-// min / max folds and exact counts.
+// ranges, the deep levels thousands of small ones).  Both paths pick the same split from the same
+// bins (costs are min / max folds and exact counts); a block bins an evenly spaced sample of a
+// range of more than kSahSample objects.
 constexpr uint32_t kWaveMax = 256;
 constexpr int kU = 8;  // loads in flight per lane in the block path's loops
+constexpr uint32_t kSahSample = 2048;  // objects binned per range (evenly spaced) above this
 struct SahBins {
     uint32_t cnt[3][kBins];
     uint32_t bb[3][kBins][6];  // orderable bits: lo min, hi max
@@ -316,12 +318,21 @@ __global__ __launch_bounds__(kB) void k_sah_level(const uint4 *tin, const uint32
         bool ax_ok[3];
         bin_frame(s_box, cmn, scale, ax_ok);
         // bins: each thread takes a contiguous run of the range (neighbouring ids are often
-        // neighbouring objects, which share bins: spread them over the wave's lanes)
+        // neighbouring objects, which share bins: spread them over the wave's lanes).  A range of
+        // more than kSahSample objects bins kSahSample of them, evenly spaced: the split is chosen
+        // from the sample, the partition below counts the true sides (the top levels' LDS atomics
+        // otherwise serialise one block on 21 atomics per object)
         {
-            const uint32_t per = (m + kB - 1) / kB, q0 = lo + tid * per, q1 = min(hi, q0 + per);
-            for (uint32_t base = q0; base < q1; base += kU) {
+            const bool smp = m > kSahSample;
+            const uint32_t ms = smp ? kSahSample : m;
+            const uint32_t per = (ms + kB - 1) / kB, k0 = tid * per, k1 = min(ms, k0 + per);
+            for (uint32_t base = k0; base < k1; base += kU) {
                 uint32_t g[kU];
-                for (int u = 0; u < kU; u++) g[u] = base + u < q1 ? ids_in[base + u] : 0xffffffffu;
+                for (int u = 0; u < kU; u++) {
+                    const uint32_t k = base + u;
+                    const uint32_t q = smp ? lo + (uint32_t)(((uint64_t)k * m) / kSahSample) : lo + k;
+                    g[u] = k < k1 ? ids_in[q] : 0xffffffffu;
+                }
                 for (int u = 0; u < kU; u++)
                     if (g[u] != 0xffffffffu) {
                         float bx[6], c[3];
@@ -338,7 +349,7 @@ __global__ __launch_bounds__(kB) void k_sah_level(const uint4 *tin, const uint32
         }
         __syncthreads();
         const int best = s_split[0];
-        const uint32_t nl = (uint32_t)s_split[1];
+        const uint32_t nl_pick = (uint32_t)s_split[1];  // the sample's left count when sampled
         // stable partition by side: a wave per quarter of the range (64-aligned), a count pass,
         // then each wave places its quarter from the counts of the quarters before it
         const int a = best >= 0 ? best / (kBins - 1) : 0, k = best >= 0 ? best % (kBins - 1) : 0;
@@ -354,13 +365,16 @@ __global__ __launch_bounds__(kB) void k_sah_level(const uint4 *tin, const uint32
             }
             for (int u = 0; u < kU; u++) {
                 const uint32_t q = base + 64u * u + lane;
-                nleft += (uint32_t)__popcll(__ballot(q < s1 && goes_left(best, c[u], q - lo, nl, cmn[a], scale[a], k)));
+                nleft += (uint32_t)__popcll(__ballot(q < s1 && goes_left(best, c[u], q - lo, nl_pick, cmn[a], scale[a], k)));
             }
         }
         if (lane == 0) s_wl[wv] = nleft;
         __syncthreads();
-        uint32_t left = 0;
-        for (uint32_t w = 0; w < wv; w++) left += s_wl[w];
+        uint32_t left = 0, nl = 0;  // nl: the true left count
+        for (uint32_t w = 0; w < kB / 64; w++) {
+            if (w < wv) left += s_wl[w];
+            nl += s_wl[w];
+        }
         uint32_t right = (s0 - lo) - left;
         for (uint32_t base = s0; base < s1; base += 64u * kU) {
             uint32_t g[kU];
