@@ -111,9 +111,9 @@ typedef struct rt_options {
     int inw_lds_nodes;      /* top of the wide BVH staged in LDS (768-lane blocks) */
     int inw_fused_cull;     /* one fma per culling plane where the error bound holds */
     int inw_claim_order;    /* pixel-major claims costliest 8x8 blocks first */
-    int inw_ring_pm;        /* pixel-major fold ring: 0 (default) in LDS, 256 entries per wave, beside
-                               5 staged nodes; else a global ring of that many entries per wave
-                               (power of two >= 64) beside 236 staged nodes */
+    int inw_ring_pm;        /* pixel-major fold ring: 0 (default) in LDS, 256 entries per wave, the walks
+                               reading every node from L1 / L2; else a global ring of that many entries
+                               per wave (power of two >= 64) beside 236 staged nodes */
     int inw_ring_sm;        /* sample-major fold ring: 0 (default) in LDS, 256 entries per wave, when the
                                scene's BVH top fits the 5 nodes staged beside it (nothing lost), else a
                                global ring of 256; else a global ring of that many entries per wave */

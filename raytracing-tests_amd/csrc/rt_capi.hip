@@ -1545,8 +1545,7 @@ int rt_debug_path(rt_dev_scene *s, rt_path_info *out) {
         P.order = 1;
         P.ring_entries = int(s->last_ring[0]);
         P.ring_lds = s->last_lring ? 1 : 0;
-        if (s->last_lring) P.lds_nodes = std::min(P.lds_nodes, int(rtk::kPmLdsNodes));
-        if (s->last_lring) P.lbvh_lds_nodes = std::min(P.lbvh_lds_nodes, int(rtk::kPmLdsNodes * 10 / 2));
+        if (s->last_lring) { P.lds_nodes = 0; P.lbvh_lds_nodes = 0; }  // the ring instances stage no nodes
     }
     else if (std::strncmp(name, "k_inw_sm", 8) == 0) {
         P.order = 2;

@@ -1817,11 +1817,12 @@ constexpr int kInwNodeF4 = 10;
 // leave of 160 KB
 // (kInwLdsNodes = 236: rt_kernels.hpp)
 __shared__ float4 g_inw_lnodes[kInwLdsNodes * kInwNodeF4];
-// k_inw_pm with LN and InwScene::lring (rt_options.inw_ring_pm = 0, the default): the first
-// kPmLdsNodes nodes, then the 12 waves' fold rings of kPmLdsRing entries (r, g, b planes) in the
-// same LDS (a 256-entry window costs 0.5% against 1024, 128 entries 7%; the ring
-// takes the LDS of all but the top 5 nodes, which were worth 1.5%, and saves 1% of global ring
-// traffic -- 0.57 against 42 GB of L2-to-fabric traffic per C3 frame)
+// k_inw_pm / k_inw_sm with LN and InwScene::lring / lring_sm: room for kPmLdsNodes nodes, then the
+// 12 waves' fold rings of kPmLdsRing entries (r, g, b planes) in the same LDS (a
+// 256-entry window costs 0.5% against 1024, 128 entries 7%; the ring takes the LDS of all but 5
+// nodes, which were worth 1.5%, and saves 1% of global ring traffic -- 0.57 against 42 GB of
+// L2-to-fabric traffic per C3 frame).  k_inw_pm's ring instances leave those 5 slots unused (its
+// walks read no staged node), k_inw_sm's stage the BVH there when it fits
 static_assert(kPmLdsNodes * kInwNodeF4 * 16 + 12 * 3 * kPmLdsRing * 4 <= kInwLdsNodes * kInwNodeF4 * 16, "LDS ring");
 template <bool LN>
 __device__ __forceinline__ const float4 *inw_node_ptr(const InwScene &S, int cur) {
@@ -3035,8 +3036,12 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     // LRING: the fold ring in LDS, after the first kPmLdsNodes staged nodes (InwScene::lring; an
     // instance of its own: as a per-frame branch it cost 1% of C3 in either mode)
     constexpr bool LR = LN && LRING;
-    if constexpr (LN) {
-        const uint32_t cap = LR ? (uint32_t)kPmLdsNodes : (uint32_t)kInwLdsNodes;
+    // WLN: the walks read staged nodes.  The LDS-ring instances stage none: the top 5 nodes the
+    // ring leaves room for sit in L1 anyway, and the walk loop without the LDS branch (its exec
+    // masking and the base pointer kept in a VGPR lane) ran C3 2% faster
+    constexpr bool WLN = LN && !LR;
+    if constexpr (WLN) {
+        const uint32_t cap = (uint32_t)kInwLdsNodes;
         const uint32_t n = S.wnodes ? (S.n_wnodes < cap ? S.n_wnodes : cap) : 0u;
         for (uint32_t i = threadIdx.x; i < n * (uint32_t)kInwNodeF4; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
         // no wide walk: the stackless LBVH walks read the top of the LBVH (2 float4 per node) there
@@ -3260,7 +3265,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             if (go) {
                 WalkPark wp{pslot, parked, false};
                 if (f.px_rays && !parked) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
-                inw_segment<LIGHTS, LN, FU, PK>(S, f, K, s, col, dep, c, bu, &wp);
+                inw_segment<LIGHTS, WLN, FU, PK>(S, f, K, s, col, dep, c, bu, &wp);
                 parked = PK && wp.parked;
             }
             if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring

@@ -182,7 +182,7 @@ def test_inw_strategies_bit_identical(gpu, over, scene, w, h, spp):
 
 
 @pytest.mark.parametrize("over,scene,w,h,spp", [
-    ({}, INW1, 160, 90, 12),                       # pixel-major fold (k_inw_pm, LDS ring: 25 LBVH nodes in LDS)
+    ({}, INW1, 160, 90, 12),                       # pixel-major fold (k_inw_pm, LDS ring: no staged nodes)
     ({"inw_order": 2}, INW1, 160, 90, 12),          # sample-major fold (1,180 LBVH nodes in LDS)
     ({"inw_order": -1}, INW1, 160, 90, 12),         # the per-pixel kernel (no LDS staging)
     ({"inw_lds_nodes": 0}, INW1, 160, 90, 12),      # 256-lane instances, every node from global memory
