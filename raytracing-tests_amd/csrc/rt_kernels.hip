@@ -1703,21 +1703,23 @@ __device__ __forceinline__ bool test_aabb(float4 n0, float4 n1, f3 o, f3 id, flo
     return tlim > 0.0f ? tlim > tmin : true;
 }
 
-// The same test, also returning the entry t it compares (te) -- the wide walk's guard below.
+// The same test, also returning the entry t it compares (te) -- the wide walk's guard below.  Every
+// axis is evaluated (test_aabb returns at the first failing one): the same result and, when it
+// passes, the same te.  Without the early outs the compiler issues the box's loads together
+// instead of one round trip per axis: C3 201.7 -> 196.5 ms, C5 6.92 -> 6.79 s (same-box A/B,
+// profiles/r05_ab_leaf_test.json)
 __device__ __forceinline__ bool test_aabb_te(float4 n0, float4 n1, f3 o, f3 id, float tlim, float &te) {
     float a = (n0.x - o.x) * id.x, b = (n0.w - o.x) * id.x;
     float tmin = fminf(a, b), tmax = fmaxf(a, b);
-    te = tmin;
-    if (tmax <= tmin) return false;
+    bool ok = !(tmax <= tmin);
     a = (n0.y - o.y) * id.y; b = (n1.x - o.y) * id.y;
     tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
-    te = tmin;
-    if (tmax <= tmin) return false;
+    ok = ok && !(tmax <= tmin);
     a = (n0.z - o.z) * id.z; b = (n1.y - o.z) * id.z;
     tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
+    ok = ok && !(tmax <= tmin);
     te = tmin;
-    if (tmax <= tmin) return false;
-    return tlim > 0.0f ? tlim > tmin : true;
+    return ok && (tlim > 0.0f ? tlim > tmin : true);
 }
 
 // closest-hit LBVH DFS (01_BVH...glsl:431-473, 04...glsl:524-563, shadow 620-657)
@@ -2099,21 +2101,27 @@ __device__ float inw_closest_beam(const InwScene &S, const FStack &K, f3 o, f3 d
     float lim = bt * kap + 0.01f;
     bool ovf = false;
     uint32_t k = 0;
+    // packed entries hold t rounded down (and 0 for a negative entry): the list stays sorted, and a
+    // ray stops at a stored t above lim no earlier than at the exact one
+    auto entry = [&](uint32_t j) {
+        if (S.beam16) {
+            const uint32_t p = list16[j];
+            return make_uint2(p & 0xffffu, p & 0xffff0000u);
+        }
+        return list[j];
+    };
+    uint2 en = ok && n > 0u ? entry(0) : make_uint2(0u, 0u);  // the next entry, loaded a candidate ahead
     for (;;) {
         bool act = ok && k < n;
         uint2 e = make_uint2(0u, 0u);
         if (act) {
-            // packed entries hold t rounded down (and 0 for a negative entry): the list stays sorted,
-            // and a ray stops at a stored t above lim no earlier than at the exact one
-            if (S.beam16) {
-                const uint32_t p = list16[k];
-                e = make_uint2(p & 0xffffu, p & 0xffff0000u);
-            } else e = list[k];
+            e = en;
             act = __uint_as_float(e.y) <= lim;
         }
         if (!__any(act)) break;
         OCC_TALLY(c, kOccBeam, act);
         if (act) {
+            if (k + 1u < n) en = entry(k + 1u);
             const int g = (int)e.x;
             c.prims++;
             const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
@@ -2239,12 +2247,17 @@ __device__ float inw_ri_grid(const InwScene &S, f3 hp, float ratio, Ctr &c, bool
     uint32_t rk[kRiMax];
     float rv[kRiMax];
     int nin = 0;
+    // an object's leaf box, record and rank are loaded together (one round trip; the hit object
+    // itself is always listed and inside its box), the next id while this one is tested
+    uint32_t gn = b < e ? S.ri_ids[b] : 0u;
     for (uint32_t k = b; k < e; k++) {
-        const int g = (int)S.ri_ids[k];
+        const int g = (int)gn;
+        if (k + 1 < e) gn = S.ri_ids[k + 1];
         c.prims++;
         const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
-        if (!(hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z)) continue;
         const Xf x = load_xf(S, g);
+        const uint32_t rg = S.rank[g];
+        if (!(hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z)) continue;
         f3 v = (hp - x.pos) + x.delta * (1.0f - ratio);
         v = tmul(x.R, v);
         v.x *= x.is.x; v.y *= x.is.y; v.z *= x.is.z;
@@ -2254,7 +2267,7 @@ __device__ float inw_ri_grid(const InwScene &S, f3 hp, float ratio, Ctr &c, bool
         else inside = false;
         if (inside) {
             if (nin == kRiMax) { ok = false; return 1.0f; }
-            rk[nin] = S.rank[g];
+            rk[nin] = rg;
             rv[nin] = x.ri_acc;
             nin++;
         }

@@ -3,8 +3,8 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 V=$1; CFG=${2:-c3}
-O=gpurun_out/r05_ab_$V; rm -rf $O; mkdir -p $O
-B="timeout -k 10 300 python3 bench.py --no-cpu-baseline --config $CFG --steps 5"
+O=gpurun_out/r05_ab_${V}_$CFG; rm -rf $O; mkdir -p $O
+B="timeout -k 10 300 python3 bench.py --no-cpu-baseline --config $CFG --steps ${STEPS:-5}"
 for i in 1 2; do
   $B > $O/base_$i.json 2> $O/base_$i.err || exit 1
   RT_HIP_LIB=raytracing-tests_amd/librt_hip_$V.so $B > $O/var_$i.json 2> $O/var_$i.err || exit 1
