@@ -1690,17 +1690,32 @@ __device__ __forceinline__ Xf load_xf(const InwScene &S, int g) {
 }
 
 // TestIntersectAABB 01_BVH...glsl:187-208 (reciprocals of the ray direction hoisted)
+// EO (default): the shader's early outs.  !EO: every axis evaluated -- the same result, with the
+// node's two loads issued together (see test_aabb_te below); INW-04's reference walks (its
+// axis-aligned rays) run 1.1% faster that way at C5, INW-01's early-out code generation is 1% faster at C3
+template <bool EO = true>
 __device__ __forceinline__ bool test_aabb(float4 n0, float4 n1, f3 o, f3 id, float tlim) {
     float a = (n0.x - o.x) * id.x, b = (n0.w - o.x) * id.x;
     float tmin = fminf(a, b), tmax = fmaxf(a, b);
-    if (tmax <= tmin) return false;  // axis 0 re-applied by the loop is idempotent
-    a = (n0.y - o.y) * id.y; b = (n1.x - o.y) * id.y;
-    tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
-    if (tmax <= tmin) return false;
-    a = (n0.z - o.z) * id.z; b = (n1.y - o.z) * id.z;
-    tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
-    if (tmax <= tmin) return false;
-    return tlim > 0.0f ? tlim > tmin : true;
+    if constexpr (EO) {
+        if (tmax <= tmin) return false;  // axis 0 re-applied by the loop is idempotent
+        a = (n0.y - o.y) * id.y; b = (n1.x - o.y) * id.y;
+        tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
+        if (tmax <= tmin) return false;
+        a = (n0.z - o.z) * id.z; b = (n1.y - o.z) * id.z;
+        tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
+        if (tmax <= tmin) return false;
+        return tlim > 0.0f ? tlim > tmin : true;
+    } else {
+        bool ok = !(tmax <= tmin);
+        a = (n0.y - o.y) * id.y; b = (n1.x - o.y) * id.y;
+        tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
+        ok = ok && !(tmax <= tmin);
+        a = (n0.z - o.z) * id.z; b = (n1.y - o.z) * id.z;
+        tmin = fmaxf(fminf(a, b), tmin); tmax = fminf(fmaxf(a, b), tmax);
+        ok = ok && !(tmax <= tmin);
+        return ok && (tlim > 0.0f ? tlim > tmin : true);
+    }
 }
 
 // The same test, also returning the entry t it compares (te) -- the wide walk's guard below.  Every
@@ -1723,7 +1738,7 @@ __device__ __forceinline__ bool test_aabb_te(float4 n0, float4 n1, f3 o, f3 id, 
 }
 
 // closest-hit LBVH DFS (01_BVH...glsl:431-473, 04...glsl:524-563, shadow 620-657)
-template <bool WANT_NORMAL>
+template <bool WANT_NORMAL, bool EO = true>
 __device__ float inw_traverse(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
                               float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c) {
     float final_geom = init_geom;
@@ -1737,7 +1752,7 @@ __device__ float inw_traverse(const InwScene &S, FStack &K, f3 o, f3 d, float ra
             const int node = (int)K.at(K.size);
             const float4 n0 = S.nodes[2 * node], n1 = S.nodes[2 * node + 1];
             c.nodes++;
-            if (test_aabb(n0, n1, o, id, tlim)) {
+            if (test_aabb<EO>(n0, n1, o, id, tlim)) {
                 const float left = n1.z;
                 if (left > 0.1f) {
                     const float right = left + 1.0f;
@@ -2324,7 +2339,7 @@ __device__ __forceinline__ uint32_t lbvh_next(const InwScene &S, uint32_t cur, f
     }
 }
 
-template <bool WANT_NORMAL, bool LN = false>
+template <bool WANT_NORMAL, bool LN = false, bool EO = true>
 __device__ float inw_traverse_sl(const InwScene &S, f3 o, f3 d, float ratio, bool invert, float &tlim, f3 &normal,
                                  float &extra, float init_geom, Ctr &c) {
     float final_geom = init_geom;
@@ -2335,7 +2350,7 @@ __device__ float inw_traverse_sl(const InwScene &S, f3 o, f3 d, float ratio, boo
         float4 n0, n1;
         lbvh_node<LN>(S, cur, n0, n1);
         c.nodes++;
-        if (test_aabb(n0, n1, o, id, tlim)) {
+        if (test_aabb<EO>(n0, n1, o, id, tlim)) {
             const float left = n1.z;
             if (left > 0.1f) {  // descend: the child the reference pops first
                 const uint32_t L = (uint32_t)left;
@@ -2404,7 +2419,8 @@ __device__ float inw_surrounding_ri_sl(const InwScene &S, f3 hp, float ratio, Ct
     return acc;
 }
 
-template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false>
+// EO: the reference walks' box test with the shader's early outs (INW-01) or all axes (INW-04)
+template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false, bool EO = true>
 __device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
                                              float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c,
                                              WalkPark *wp = nullptr) {
@@ -2415,8 +2431,8 @@ __device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o,
     OCC_TALLY(c, kOccRef, !ok);
     if (ok) return g;
     if (S.sl && K.size + S.dfs_high <= (uint32_t)kFStack)  // no push of the reference walk could drop
-        return inw_traverse_sl<WANT_NORMAL, LN>(S, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
-    return inw_traverse<WANT_NORMAL>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
+        return inw_traverse_sl<WANT_NORMAL, LN, EO>(S, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
+    return inw_traverse<WANT_NORMAL, EO>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
 }
 template <bool LN = false>
 __device__ __forceinline__ float inw_ri(const InwScene &S, FStack &K, f3 hp, float ratio, Ctr &c) {
@@ -2559,7 +2575,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
             fg = inw_closest_beam<true>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c, bunit,
                                         beam_ok);
         if (!beam_ok) {
-            fg = inw_closest<true, LN, FU, PK>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c,
+            fg = inw_closest<true, LN, FU, PK, !LIGHTS>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c,
                                                wp);
             if (PK && wp->parked) return;  // the walk goes on in the next iteration
         }
@@ -2626,7 +2642,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
                     f3 sd = normalize((bmin + (bmax - bmin) * ratio) - so);
                     c.shadow++;
                     f3 dummy_n; float dummy_e;
-                    float sg = inw_closest<false, LN, FU>(S, K, so, sd, ratio, invert, sl, dummy_n, dummy_e, -1.0f, c);
+                    float sg = inw_closest<false, LN, FU, false, !LIGHTS>(S, K, so, sd, ratio, invert, sl, dummy_n, dummy_e, -1.0f, c);
                     is_lit += (uint32_t)is_lit_geom(S, f2u(sg + 0.1f));
                 }
                 const uint32_t nl = S.n_lights > 1 ? S.n_lights : 1u;
