@@ -1916,6 +1916,15 @@ __device__ __forceinline__ void cull4nf(const float4 nx, const float4 ny, const 
     t3 = one(a[1].y, a[3].y, a[5].y, a[7].y, a[9].y, a[11].y);
 }
 
+// An empty asm that reads the object-space ray: the compiler must have it (so the object record's
+// loads) before the caller's box-test branch, instead of sinking the loads behind the branch --
+// one round trip for box and record instead of two or three (leaf tests, beam candidates)
+__device__ __forceinline__ void keep_before_branch(f3 to, f3 td) {
+#ifndef RT_LEAF_SINK
+    asm volatile("" ::"v"(to.x), "v"(to.y), "v"(to.z), "v"(td.x), "v"(td.y), "v"(td.z));
+#endif
+}
+
 // ---------------------------------------------------------------- INW wide walk
 // The reference's closest hit (01_BVH...glsl:431-473) is the nearest hit among the objects whose
 // LBVH leaf box its depth-first walk reaches, ties to the one it reaches first.  With finite ray
@@ -1992,9 +2001,11 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
         const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
         const Xf x = load_xf(S, g);  // loaded with the box, before its test: one memory latency
         float te;
-        if (!test_aabb_te(n0, n1, o, id, tlim0, te)) return;
+        const bool inb = test_aabb_te(n0, n1, o, id, tlim0, te);
         f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
         f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+        keep_before_branch(to, td);
+        if (!inb) return;
         float t = -1.0f;
         if (x.type == 1) t = t_ellipsoid(to, td, x.is);
         else if (x.type == 2) t = t_cuboid(to, td, x.scale);
@@ -2142,9 +2153,11 @@ __device__ float inw_closest_beam(const InwScene &S, const FStack &K, f3 o, f3 d
             const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
             const Xf x = load_xf(S, g);
             float te;
-            if (test_aabb_te(n0, n1, o, id, tlim0, te)) {
-                f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
-                f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+            const bool inb = test_aabb_te(n0, n1, o, id, tlim0, te);
+            f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+            f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+            keep_before_branch(to, td);
+            if (inb) {
                 float t = -1.0f;
                 if (x.type == 1) t = t_ellipsoid(to, td, x.is);
                 else if (x.type == 2) t = t_cuboid(to, td, x.scale);
