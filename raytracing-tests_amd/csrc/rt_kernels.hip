@@ -3116,6 +3116,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     uint32_t xq = 0;                   // S.xcdq: queues found empty (from this block's XCD on)
     const uint32_t nblk8 = total / 64u;  // 8x8 blocks (units come in whole blocks)
     f3 acc = f3{0, 0, 0};              // running End() sum of pixel jf (the same in every lane)
+    float accc = 0.0f;                 // LR: lane c < 3 holds channel c of that sum
     uint32_t pix_slot = 0xffffffffu;   // lane l: the unit of the claimed ordinal j with j % 64 == l
     // per lane: the sample it traces
     bool busy = false;
@@ -3142,6 +3143,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
             const uint32_t k = gf + lane;
             float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             uint32_t n;
+            bool continue_fold = true;  // (the LDS-ring fold below finishes the run itself)
             if constexpr (LR) {
                 // Every issued entry is either held by a busy lane or stored, so the entries below
                 // the smallest one a busy lane holds are finished: no tags.  LDS ops of one wave
@@ -3163,8 +3165,48 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                 const unsigned long long m = __ballot(fin);
                 n = ~m == 0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
             }
+#ifndef RT_FOLD_READLANE
+            if constexpr (LR) {
+                // LDS ring: lanes 0, 1, 2 add the r, g, b planes' entries straight from LDS, each
+                // its channel in sample order (the same float additions, two instructions per entry
+                // instead of three readlanes and three adds); the run splits at pixel ends
+                const float *pl = lr + (lane < 3u ? lane : 0u) * kPmLdsRing;
+                for (uint32_t i = 0; i < n;) {
+                    const uint32_t e = i + (n - i < spp - sf ? n - i : spp - sf);
+                    if (lane < 3u) {
+                        uint32_t j = i;
+                        if (sf == 0) { accc = pl[(gf + j) & rmask]; j++; }
+                        for (; j + 4u <= e; j += 4u) {  // four loads, then four adds in order
+                            const float a0 = pl[(gf + j) & rmask], a1 = pl[(gf + j + 1u) & rmask];
+                            const float a2 = pl[(gf + j + 2u) & rmask], a3 = pl[(gf + j + 3u) & rmask];
+                            accc = accc + a0; accc = accc + a1; accc = accc + a2; accc = accc + a3;
+                        }
+                        for (; j < e; j++) accc = accc + pl[(gf + j) & rmask];
+                    }
+                    sf += e - i;
+                    i = e;
+                    if (sf == spp) {  // pixel jf complete: End()'s imageStores (01_BVH...glsl:652, 667-668)
+                        const uint32_t unit = uni((uint32_t)__builtin_amdgcn_readlane((int)pix_slot, (int)(jf & 63u)));
+                        const float ax = rdl(accc, 0u), ay = rdl(accc, 1u), az = rdl(accc, 2u);
+                        if (lane == 0) {
+                            const UnitPix p = unit_pixel(f, unit);
+                            if (p.out != (size_t)-1) {
+                                fb_store(f, p.out,
+                                         make_float4(p.in_image ? ax * inv : 0.0f, p.in_image ? ay * inv : 0.0f,
+                                                     p.in_image ? az * inv : 0.0f, p.in_image ? 1.0f : 0.0f));
+                                if (f.out_depth) depth_store(f, p.out, pdep[jf & 63u]);
+                            }
+                        }
+                        sf = 0;
+                        jf++;
+                    }
+                }
+                gf += n;
+                continue_fold = false;
+            }
+#endif
             // the run splits at pixel ends: per pixel, its entries are added with no test between them
-            for (uint32_t i = 0; i < n;) {
+            for (uint32_t i = 0; continue_fold && i < n;) {
                 const uint32_t e = i + (n - i < spp - sf ? n - i : spp - sf);
                 uint32_t j = i;
                 if (sf == 0) { acc = f3{rdl(v.x, j), rdl(v.y, j), rdl(v.z, j)}; j++; }
@@ -3192,7 +3234,7 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                     jf++;
                 }
             }
-            gf += n;
+            if (continue_fold) gf += n;
         }
         INW_CYC(c, 2, t_fold);
         INW_T0(t_issue);
