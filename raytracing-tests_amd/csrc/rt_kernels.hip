@@ -2569,6 +2569,10 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
     const f3 D = mk(F.dir[0], F.dir[1], F.dir[2]);
     const float ratio = (float)s * F.inv_spp;
     const bool invert = dot(D, f3{1, 1, 1}) > 0.0f;
+    INW_T0(t_fn);
+#ifdef RT_DIAG_SPLIT
+    unsigned long long t_tail = 0;  // the scatter and pushes after the RI (phase 7)
+#endif
     do {
         const bool resumed = PK && wp->resume;
         if (!resumed) K.size -= 8;
@@ -2581,6 +2585,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         const float tlim0 = mf0 ? K.at(4) : kMaxT;
         float tlim = tlim0, extra = 0.0f;
         f3 normal = f3{0, 0, 0};
+        INW_CYC(c, 5, t_fn);  // the pop and the segment's prologue
         INW_T0(t_ch);
         float fg;
         bool beam_ok = false;
@@ -2593,6 +2598,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
             if (PK && wp->parked) return;  // the walk goes on in the next iteration
         }
         INW_CYC(c, 0, t_ch);
+        INW_T0(t_mat);
         const f3 hitpoint = co + cd * tlim;
         if (!(tlim < tlim0)) {
             if (mf0 && (int)(K.at(5) + 0.1f) < F.n_focus) {  // next focal lens, 01_BVH...glsl:506-528
@@ -2633,6 +2639,7 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         // run or reads no RI, the walk is skipped -- when it cannot drop a push (the wide walk's
         // condition; its drops are counted) and the walk is the wide one (whose node counts are
         // this build's own).  INW-04 decides after its shadow rays, which scale the contribution.
+        INW_CYC(c, 6, t_mat);  // a hit's material (and texture)
         const bool ri_forced = S.wnodes == nullptr || K.size + S.dfs_high > (uint32_t)kFStack;
         const bool ri_read = (m_refl > 0.002f || m_refr > 0.002f) && (m_refr > 0.002f || dot(normal, cd) > 0.0f);
         float surr = 1.0f;
@@ -2643,6 +2650,9 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
             surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
             INW_CYC(c, 1, t_ri);
         }
+#ifdef RT_DIAG_SPLIT
+        t_tail = clock64();
+#endif
         if (mf0) K.size = 0;  // 01_BVH...glsl:544-549: the lens record goes after a primary hit
         if (LIGHTS) {  // 04...glsl:604-665
             uint32_t is_lit = S.n_lights > 0 ? 0u : (uint32_t)is_lit_geom(S, f2u(fg + 0.1f));
@@ -2705,6 +2715,9 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         }
         color = color + m_color * contribution;
     } while (false);
+#ifdef RT_DIAG_SPLIT
+    if (t_tail) c.cyc[7] += clock64() - t_tail;
+#endif
 }
 
 template <bool LIGHTS>
@@ -3176,10 +3189,13 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
                     if (lane < 3u) {
                         uint32_t j = i;
                         if (sf == 0) { accc = pl[(gf + j) & rmask]; j++; }
-                        for (; j + 4u <= e; j += 4u) {  // four loads, then four adds in order
-                            const float a0 = pl[(gf + j) & rmask], a1 = pl[(gf + j + 1u) & rmask];
-                            const float a2 = pl[(gf + j + 2u) & rmask], a3 = pl[(gf + j + 3u) & rmask];
-                            accc = accc + a0; accc = accc + a1; accc = accc + a2; accc = accc + a3;
+                        constexpr uint32_t kFU = 4;  // loads in flight, then the adds in order (8, 16: same time)
+                        for (; j + kFU <= e; j += kFU) {
+                            float a[kFU];
+#pragma unroll
+                            for (uint32_t u = 0; u < kFU; u++) a[u] = pl[(gf + j + u) & rmask];
+#pragma unroll
+                            for (uint32_t u = 0; u < kFU; u++) accc = accc + a[u];
                         }
                         for (; j < e; j++) accc = accc + pl[(gf + j) & rmask];
                     }
@@ -3369,14 +3385,16 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         INW_CYC(c, 4, t_seg);
     }
 #ifdef RT_DIAG_SPLIT
-    // phases 0-1 run inside `if (busy)`: the wave's time there is the largest of its lanes'
-    for (int k = 0; k < 2; k++)
+    // phases 0-1 and 5-7 run inside `if (busy)`: the wave's time there is the largest of its lanes'
+    for (int k = 0; k < 8; k++) {
+        if (k >= 2 && k < 5) continue;
         for (int o = 32; o >= 1; o >>= 1) {
             const unsigned long long t = __shfl_xor(c.cyc[k], o, 64);
             c.cyc[k] = t > c.cyc[k] ? t : c.cyc[k];
         }
+    }
     if (f.dbg && lane == 0) {
-        for (int k = 0; k < 5; k++) atomicAdd(f.dbg + 8 + k, c.cyc[k]);
+        for (int k = 0; k < 8; k++) atomicAdd(f.dbg + 8 + k, c.cyc[k]);
         // wall clock (100 MHz): first / last wave start, first queue drain, first / last wave exit
         const unsigned long long t_end = wall_clock64();
         unsigned long long *t = reinterpret_cast<unsigned long long *>(f.dbg) + 16;

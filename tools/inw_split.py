@@ -79,8 +79,9 @@ b.record(st)
 torch.cuda.synchronize()
 lib.rt_debug_counters(None)
 d = [int(v) for v in dbg.cpu().tolist()]
-names = ("closest_hit", "ri_walk", "fold", "claim_issue", "segment_step")
-cyc = dict(zip(names, d[8:13]))
+names = ("closest_hit", "ri_walk", "fold", "claim_issue", "segment_step", "seg_prologue", "seg_material",
+         "seg_tail")
+cyc = dict(zip(names, d[8:16]))
 tot = cyc["fold"] + cyc["claim_issue"] + cyc["segment_step"]
 kname = C.create_string_buffer(64)
 lib.rt_debug_launches(scene, kname, 64)
