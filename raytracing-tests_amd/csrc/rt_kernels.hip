@@ -3002,10 +3002,10 @@ __global__ __launch_bounds__(kBlock) void k_inw_probe(Frame f, InwScene S, uint3
 
 // Claim order (DESIGN.md §5 "Claim order"): a persistent fold kernel's tail is the last pixels
 // it claims -- a wave needs spp / 64 rounds of samples for one pixel, so expensive pixels claimed
-// last leave the rest of the chip idle.  k_inw_cost estimates each 8x8 block's cost from the
-// primary rays of 16 of its pixels (a miss or a diffuse hit ends the sample; a reflective /
-// refractive hit starts a chain of about log(0.01) / log(coefficient) segments, two-sided for
-// refraction) and buckets it (256 log-scale keys); k_inw_order_scan / k_inw_order_scatter lay
+// last leave the rest of the chip idle.  k_inw_cost estimates each pixel's cost from its primary
+// ray (a miss or a diffuse hit ends the sample; a reflective / refractive hit starts a chain of
+// about log(0.01) / log(coefficient) segments, two-sided for refraction), keys each 8x8 block by
+// its costliest pixel and buckets it (256 log-scale keys); k_inw_order_scan / k_inw_order_scatter lay
 // the blocks out costliest first, and k_inw_pm claims through that order.  The order only decides
 // which wave traces which pixel when: every pixel's samples and sums are the same.  Pixel-major
 // frames only: the three kernels exit at once when the probe picked k_inw_sm, whose 8x8 blocks
@@ -3017,11 +3017,13 @@ __global__ __launch_bounds__(kBlock) void k_inw_cost(Frame f, InwScene S, uint32
     __shared__ float lds[kFStack * kBlock];
     Ctr c;  // not flushed: these rays are not the frame's
     FStack K{lds + threadIdx.x, 0};
-    const uint32_t lane = threadIdx.x & 63u, nblk = units_total(f) / 64u, p = lane & 15u;
-    const uint32_t blk = ((blockIdx.x * kBlock + threadIdx.x) >> 4);  // 16 lanes per block
+    // every pixel of the block (a wave per block); the block's key is its costliest pixel's, so the
+    // blocks claimed last hold no expensive pixel
+    const uint32_t lane = threadIdx.x & 63u, nblk = units_total(f) / 64u, p = lane;
+    const uint32_t blk = ((blockIdx.x * kBlock + threadIdx.x) >> 6);
     float est = 0.0f;
     if (blk < nblk) {
-        const UnitPix px = unit_pixel(f, blk * 64u + (p >> 2) * 16u + (p & 3u) * 2u);
+        const UnitPix px = unit_pixel(f, blk * 64u + p);
         if (px.in_image) {
             const int s = f.spp / 2;
             inw_start_sample(S, f, K, px.x, px.y, s, c);
@@ -3045,7 +3047,8 @@ __global__ __launch_bounds__(kBlock) void k_inw_cost(Frame f, InwScene S, uint32
             }
         }
     }
-    for (int o = 8; o >= 1; o >>= 1) est += __shfl_xor(est, o, 64);
+    for (int o = 32; o >= 1; o >>= 1) est = fmaxf(est, __shfl_xor(est, o, 64));
+    est *= 16.0f;  // the scale of the 16-pixel sums this key replaced
     if (p == 0 && blk < nblk) {
         const uint32_t k = (uint32_t)fminf(255.0f, 16.0f * __log2f(1.0f + est));
         key[blk] = k;
@@ -3887,7 +3890,7 @@ hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uin
         const uint32_t nblk = units_of(f) / 64u;
         uint32_t *key = cost, *order = cost + nblk, *hist = cost + 2 * nblk;
         if ((e = hipMemsetAsync(hist, 0, 256 * sizeof(uint32_t), s)) != hipSuccess) return e;
-        const dim3 g((nblk + 15u) / 16u);  // 16 blocks of 8x8 pixels per 256-lane block
+        const dim3 g((nblk + 3u) / 4u);  // 4 blocks of 8x8 pixels per 256-lane block
         if (sc.layout == 4) hipLaunchKernelGGL(k_inw_cost<true>, g, dim3(kBlock), 0, s, f, sc, key, hist, mode, force);
         else hipLaunchKernelGGL(k_inw_cost<false>, g, dim3(kBlock), 0, s, f, sc, key, hist, mode, force);
         hipLaunchKernelGGL(k_inw_order_scan, dim3(1), dim3(256), 0, s, hist, mode, force);
