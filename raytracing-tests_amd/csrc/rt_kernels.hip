@@ -3002,10 +3002,11 @@ __global__ __launch_bounds__(kBlock) void k_inw_probe(Frame f, InwScene S, uint3
 
 // Claim order (DESIGN.md §5 "Claim order"): a persistent fold kernel's tail is the last pixels
 // it claims -- a wave needs spp / 64 rounds of samples for one pixel, so expensive pixels claimed
-// last leave the rest of the chip idle.  k_inw_cost estimates each pixel's cost from its primary
-// ray (a miss or a diffuse hit ends the sample; a reflective / refractive hit starts a chain of
-// about log(0.01) / log(coefficient) segments, two-sided for refraction), keys each 8x8 block by
-// its costliest pixel and buckets it (256 log-scale keys); k_inw_order_scan / k_inw_order_scatter lay
+// last leave the rest of the chip idle.  k_inw_cost estimates each pixel's cost from the primary
+// rays of two of its samples, the costlier (a miss or a diffuse hit ends the sample; a reflective /
+// refractive hit starts a chain of about log(0.01) / log(coefficient) segments, two-sided for
+// refraction), keys each 8x8 block by its costliest pixel and buckets it (256 log-scale keys);
+// k_inw_order_scan / k_inw_order_scatter lay
 // the blocks out costliest first, and k_inw_pm claims through that order.  The order only decides
 // which wave traces which pixel when: every pixel's samples and sums are the same.  Pixel-major
 // frames only: the three kernels exit at once when the probe picked k_inw_sm, whose 8x8 blocks
@@ -3017,15 +3018,16 @@ __global__ __launch_bounds__(kBlock) void k_inw_cost(Frame f, InwScene S, uint32
     __shared__ float lds[kFStack * kBlock];
     Ctr c;  // not flushed: these rays are not the frame's
     FStack K{lds + threadIdx.x, 0};
-    // every pixel of the block (a wave per block); the block's key is its costliest pixel's, so the
-    // blocks claimed last hold no expensive pixel
+    // every pixel of the block (a wave per block), two samples each; the block's key is its
+    // costliest pixel's, so the blocks claimed last hold no expensive pixel
     const uint32_t lane = threadIdx.x & 63u, nblk = units_total(f) / 64u, p = lane;
     const uint32_t blk = ((blockIdx.x * kBlock + threadIdx.x) >> 6);
     float est = 0.0f;
     if (blk < nblk) {
         const UnitPix px = unit_pixel(f, blk * 64u + p);
-        if (px.in_image) {
-            const int s = f.spp / 2;
+        for (int si = 0; si < 2 && px.in_image; si++) {
+            const int s = si == 0 ? f.spp / 2 : f.spp / 4;
+            K.size = 0;
             inw_start_sample(S, f, K, px.x, px.y, s, c);
             K.size -= 8;
             const uint32_t b = K.size;
@@ -3035,16 +3037,17 @@ __global__ __launch_bounds__(kBlock) void k_inw_cost(Frame f, InwScene S, uint32
             f3 nrm;
             const float g = inw_closest<false>(S, K, o, d, (float)s * f.inv_spp, dot(D, f3{1, 1, 1}) > 0.0f, tlim,
                                                nrm, extra, -1.0f, c);
-            est = 1.0f;
+            float e1 = 1.0f;
             if (tlim < kMaxT) {
                 const float4 m0 = S.cold[2 * (int)g];
                 const float m = fminf(fmaxf(m0.x, m0.y), 0.99f);
-                if (LIGHTS) est += (float)S.n_lights;
+                if (LIGHTS) e1 += (float)S.n_lights;
                 if (m > 0.002f) {
                     const float n = fminf((float)f.max_bounces, 1.0f + __logf(0.01f) / __logf(m));
-                    est += n * (m0.x > 0.002f ? 2.0f : 1.0f) * (LIGHTS ? 1.0f + (float)S.n_lights : 1.0f);
+                    e1 += n * (m0.x > 0.002f ? 2.0f : 1.0f) * (LIGHTS ? 1.0f + (float)S.n_lights : 1.0f);
                 }
             }
+            est = fmaxf(est, e1);
         }
     }
     for (int o = 32; o >= 1; o >>= 1) est = fmaxf(est, __shfl_xor(est, o, 64));
