@@ -163,16 +163,38 @@ def refine_deal(lists, costs, times, nx: int, tol: float = 0.003):
 
 
 def assemble_lists(src, lists, nx: int, ny: int):
-    """src: [world, per_rank, T, T, 4] packed tiles as gathered on rank 0, where tile t of rank r
-    is lists[r][t].  Returns the [ny*T, nx*T, 4] frame (crop to W x H)."""
-    T = src.shape[2]
+    """src: [world, per_rank, T, T, C] packed tiles as gathered on rank 0 (C = 4 colour channels,
+    1 for depth), where tile t of rank r is lists[r][t].  Returns the [ny*T, nx*T, C] frame (crop
+    to W x H)."""
+    T, Cn = src.shape[2], src.shape[4]
     sel = [(r, t) for r, lst in enumerate(lists) for t in range(len(lst))]
     rr = torch.tensor([a for a, _ in sel], dtype=torch.long, device=src.device)
     tt = torch.tensor([b for _, b in sel], dtype=torch.long, device=src.device)
     idx = torch.tensor([ty * nx + tx for lst in lists for tx, ty in lst], dtype=torch.long, device=src.device)
-    grid = torch.empty((nx * ny, T, T, 4), dtype=src.dtype, device=src.device)
+    grid = torch.empty((nx * ny, T, T, Cn), dtype=src.dtype, device=src.device)
     grid[idx] = src[rr, tt]
-    return grid.view(ny, nx, T, T, 4).permute(0, 2, 1, 3, 4).reshape(ny * T, nx * T, 4)
+    return grid.view(ny, nx, T, T, Cn).permute(0, 2, 1, 3, 4).reshape(ny * T, nx * T, Cn)
+
+
+def message_views(msg, per_rank: int, T: int, with_depth: bool):
+    """A rank's one gather message: its packed colour tiles [per_rank, T, T, 4] followed by their
+    r32f depth tiles [per_rank, T, T] (INW writes both images per dispatch, 01_BVH...glsl:667-668;
+    In-Next-Week/base.h:148-173), as views of one flat buffer."""
+    n = per_rank * T * T
+    col = msg[:4 * n].view(per_rank, T, T, 4)
+    dep = msg[4 * n:5 * n].view(per_rank, T, T) if with_depth else None
+    return col, dep
+
+
+def assemble_message(gathered, lists, nx: int, ny: int, per_rank: int, T: int, with_depth: bool):
+    """Rank 0: the gathered messages (one per rank) -> the [ny*T, nx*T, 4] colour frame and the
+    [ny*T, nx*T] depth frame (None without depth)."""
+    views = [message_views(g, per_rank, T, with_depth) for g in gathered]
+    img = assemble_lists(torch.stack([v[0] for v in views], 0), lists, nx, ny)
+    dimg = None
+    if with_depth:
+        dimg = assemble_lists(torch.stack([v[1] for v in views], 0).unsqueeze(-1), lists, nx, ny)[..., 0]
+    return img, dimg
 
 
 def assemble_frame(src, order, nx: int, ny: int):
@@ -239,6 +261,105 @@ def block_parity(rect, ref_rgba, ref_depth, img, dep) -> dict:
             "oracle": "oracle/librt_oracle.so render of the same block at the same spp (the cpu_baseline run)"}
 
 
+def apply_opts(opts):
+    """--opt FIELD=VALUE: set rt_options fields (rejecting names the struct lacks)."""
+    if not opts:
+        return
+    o = R.get_options()
+    fields = dict(R.RtOptions._fields_)
+    for kv in opts:
+        k, sep, v = kv.partition("=")
+        if not sep or k not in fields or k == "size":  # a ctypes Structure would accept any name
+            raise SystemExit(f"--opt {kv!r}: not FIELD=VALUE with an rt_options field "
+                             f"({', '.join(f for f in fields if f != 'size')})")
+        setattr(o, k, float(v) if k == "spec_max_gb" else int(v))
+    R.set_options(o)
+
+
+def main_group(args):
+    """--group: the C ABI's multi-GPU path (rt_multi.hip) timed from one process -- the host a C++
+    OnUpdateBase replacement would be.  The scene is replicated on devices
+    0..gpus-1, rt_render_multi_async deals the frame's 16x16 tiles across them (rt_tile_deal), every
+    device renders its share on its own stream and one grouped RCCL send/recv brings the colour,
+    depth and counter tiles to device 0, which assembles the W x H images.  Timed like main():
+    warm-up frames, then K frames between device synchronisations of every group device."""
+    n = args.gpus
+    if n < 1 or n > torch.cuda.device_count():
+        raise SystemExit(f"--group --gpus {n}: {torch.cuda.device_count()} devices visible")
+    lib = R.load()
+    apply_opts(args.opt)
+    cfg = "c3" if args.config == "c4" else args.config
+    preset, seed, n_hint, base_over, wl1, wln, data = CONFIGS[cfg]
+    over = {k: v for k, v in (("spp", args.spp), ("width", args.width), ("height", args.height)) if v}
+    sc = R.make_scene(getattr(R, "PRESET_" + preset), seed, n_hint, **{**base_over, **over})
+    if sc.stage == R.RT_STAGE_IOW03:
+        raise SystemExit("--group: INW configs (c3 / c4 / c5)")
+    W, H, spp = sc.params.width, sc.params.height, sc.params.spp
+    lt = sc.lights if sc.lights is not None and len(sc.lights) else None
+    scenes = []
+    for d in range(n):
+        s_ = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, sc.layout, R.fptr(sc.nodes), R.fptr(lt), sc.n_lights, spp, d)
+        if not s_:
+            raise RuntimeError(f"rt_dev_scene_inw on device {d} failed")
+        scenes.append(s_)
+    grp = lib.rt_group_create((C.c_int * n)(*range(n)), n)
+    if not grp:
+        raise RuntimeError("rt_group_create failed")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    img = torch.zeros((H, W, 4), dtype=torch.float32, device=dev)
+    dep = torch.zeros((H, W), dtype=torch.float32, device=dev)
+    ctr = torch.zeros(6, dtype=torch.int64, device=dev)
+    sl = (C.c_void_p * n)(*scenes)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def frame():
+        rc = lib.rt_render_multi_async(grp, sl, C.byref(sc.camera), C.byref(sc.params), TILE_MULTI, img.data_ptr(),
+                                       dep.data_ptr(), ctr.data_ptr(), stream)
+        if rc != 0:
+            raise RuntimeError(f"rt_render_multi_async -> {rc}")
+
+    def sync_all():
+        for d in range(n):
+            torch.cuda.synchronize(d)
+
+    for _ in range(args.warmup):
+        frame()
+    sync_all()
+    ctr.zero_()
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame()
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    c = [int(v) for v in ctr.cpu().tolist()]
+    st = dict(zip(("segments", "node_visits", "prim_tests", "shadow_queries", "stack_drops", "nan_drops"), c))
+    per_step = {k: v // args.steps for k, v in st.items()}
+    path = R.debug_path(scenes[0])
+    out = {
+        "metric": METRIC, "value": round(st["segments"] / elapsed / 1e6, 3), "unit": "Mrays/s", "n_gpus": n,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data,
+        "config": {"workload": (wl1 if n == 1 else wln.format(n=n)) + " (--group: one process, C-ABI device group)",
+                   "width": W, "height": H, "spp": spp, "max_bounces": sc.params.max_bounces, "objects": sc.n,
+                   "tile": TILE_MULTI, "parallelism": f"group{n}+rccl_send_recv"},
+        "mean_bounces": round(st["segments"] / (W * H * spp * args.steps), 3),
+        "rays_per_step": per_step["segments"], "counters_per_step": per_step, "path": path,
+        "options": {k: v for k, v in R.get_options().as_dict().items()
+                    if v != R.default_options().as_dict()[k]} or "defaults",
+        "timed_region": "rt_render_multi_async of one full frame per step: every device's share, the grouped "
+                        "RCCL send/recv of colour + depth + counters to device 0, its unpack kernel",
+    }
+    print(json.dumps(out), flush=True)
+    if args.save_image:
+        np.save(args.save_image, img.cpu().numpy())
+        np.save(os.path.splitext(args.save_image)[0] + ".depth.npy", dep.cpu().numpy())
+    lib.rt_group_free(grp)
+    for s_ in scenes:
+        lib.rt_dev_scene_free(s_)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -266,10 +387,16 @@ def main():
                          "descriptions, then rt_dev_scene_inw_update with the LBVH built on the device, then the frame")
     ap.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
                     help="set an rt_options field for this run (A/B of the exact strategies; recorded in the line)")
+    ap.add_argument("--group", action="store_true",
+                    help="one process drives --gpus devices through the C ABI's device group "
+                         "(rt_group_create + rt_render_multi_async: tiles dealt across the devices, one "
+                         "grouped RCCL send/recv of colour, depth and counters to device 0); INW configs")
     ap.add_argument("--config", default="c3", choices=("c3", "c4", "c2", "c5", "ns"),
                     help="c3 (= c4): BASELINE configs[2] / configs[3], the headline; c2: configs[1]; "
                          "c5: configs[4]; ns: the north star's IOW-03 workload")
     args = ap.parse_args()
+    if args.group:
+        return main_group(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -291,16 +418,7 @@ def main():
     host_coll = world > 1 and backend != "nccl"
 
     lib = R.load()
-    if args.opt:
-        o = R.get_options()
-        fields = dict(R.RtOptions._fields_)
-        for kv in args.opt:
-            k, sep, v = kv.partition("=")
-            if not sep or k not in fields or k == "size":  # a ctypes Structure would accept any name
-                raise SystemExit(f"--opt {kv!r}: not FIELD=VALUE with an rt_options field "
-                                 f"({', '.join(f for f in fields if f != 'size')})")
-            setattr(o, k, float(v) if k == "spec_max_gb" else int(v))
-        R.set_options(o)
+    apply_opts(args.opt)
     over = {}
     if args.spp:
         over["spp"] = args.spp
@@ -342,13 +460,15 @@ def main():
     buf = {}
 
     def use_tiles(my_tiles, per_rank):
-        """(Re)allocate this rank's tile list and packed buffers (outside the timed region)."""
+        """(Re)allocate this rank's tile list and packed buffers (outside the timed region): one flat
+        message of the packed colour tiles and (INW) their r32f depth tiles, gathered in one call."""
         buf["mine"] = my_tiles
+        buf["per_rank"] = per_rank
         buf["d_tiles"] = torch.tensor(my_tiles, dtype=torch.int32, device=dev).reshape(-1, 2).contiguous()
-        buf["packed"] = torch.zeros((per_rank, T, T, 4), dtype=torch.float32, device=dev)
-        buf["depth"] = torch.zeros((per_rank, T, T), dtype=torch.float32, device=dev) if inw else None  # r32f image
+        buf["msg"] = torch.zeros(per_rank * T * T * (5 if inw else 4), dtype=torch.float32, device=dev)
+        buf["packed"], buf["depth"] = message_views(buf["msg"], per_rank, T, inw)
         buf["px_rays"] = torch.zeros(max(1, len(my_tiles)) * T * T, dtype=torch.int32, device=dev)
-        buf["gathered"] = [torch.empty_like(buf["packed"]) for _ in range(world)] if (world > 1 and rank == 0) else None
+        buf["gathered"] = [torch.empty_like(buf["msg"]) for _ in range(world)] if (world > 1 and rank == 0) else None
 
     per_rank = max(len(v) for v in lists)
     use_tiles(lists[part], per_rank)
@@ -360,6 +480,7 @@ def main():
     if args.occupancy:
         lib.rt_debug_counters(dbg.data_ptr())
     image = torch.empty((ny * T, nx * T, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+    dimage = torch.empty((ny * T, nx * T), dtype=torch.float32, device=dev) if rank == 0 and inw else None
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     def rebuild():
@@ -400,17 +521,20 @@ def main():
                 raise RuntimeError(f"rt_render_tiles_async -> {rc}")
         if evp is not None:
             evp[1].record(stream)
-        if world > 1 and not host_coll:  # the one exchange step: RCCL gather of the packed tiles to rank 0
-            dist.gather(packed, gathered, dst=0)
+        msg = buf["msg"]
+        if world > 1 and not host_coll:  # the one exchange step: RCCL gather of colour + depth tiles to rank 0
+            dist.gather(msg, gathered, dst=0)
         elif world > 1:
-            hg = [torch.empty_like(packed, device="cpu") for _ in range(world)] if rank == 0 else None
-            dist.gather(packed.cpu(), hg, dst=0)
+            hg = [torch.empty_like(msg, device="cpu") for _ in range(world)] if rank == 0 else None
+            dist.gather(msg.cpu(), hg, dst=0)
             if rank == 0:
                 for g_, h_ in zip(gathered, hg):
                     g_.copy_(h_)
         if rank == 0 and not shard:  # assemble the frame: tile t of rank r is lists[r][t]
-            src = torch.stack(gathered, 0) if world > 1 else packed.unsqueeze(0)
-            image.copy_(assemble_lists(src, lists, nx, ny))
+            img, dimg = assemble_message(gathered if world > 1 else [msg], lists, nx, ny, buf["per_rank"], T, inw)
+            image.copy_(img)
+            if dimage is not None:
+                dimage.copy_(dimg)
 
     def barrier():
         if world > 1:
@@ -515,6 +639,14 @@ def main():
     per_step = {k: v / args.steps for k, v in st.items()}
 
     path = R.debug_path(scene)  # the kernel and the exact shortcuts the last frame ran (rt_debug_path)
+    if inw:  # the last frame's closest-hit queries handed to the reference's LBVH walks (rt_path_info.ref_walks)
+        q = per_step["segments"] + per_step["shadow_queries"]
+        rw_all = path["ref_walks"]
+        if world > 1:
+            t_ = torch.tensor([rw_all], dtype=torch.float64, device="cpu" if host_coll else dev)
+            dist.all_reduce(t_)
+            rw_all = int(t_.item())
+        path["ref_walk_frac"] = round(rw_all / q, 6) if q else None
     launches = max(1, path["launches"])  # main-kernel launches per frame (planned)
     kname = path["kernel"]
     # the main kernel's own launches in the last timed frame, each bracketed by HIP events on its
@@ -571,9 +703,11 @@ def main():
                 if ([rj["config"]["width"], rj["config"]["height"], rj["config"]["spp"]] == [W, H, spp]
                         and rc["segments"] == int(per_step["segments"])):
                     fr = algorithmic_flops(rc) / launches
-                    ref_walk = {"flops_per_launch": fr, "achieved": round(fr / avg_s / 1e12, 3),
-                                "frac": round(fr / avg_s / 1e12 / FP32_PEAK_TFLOPS, 4),
+                    ref_walk = {"flops_per_launch": fr, "equivalent_TFLOPs": round(fr / avg_s / 1e12, 3),
+                                "equivalent_frac": round(fr / avg_s / 1e12 / FP32_PEAK_TFLOPS, 4),
                                 "node_visits": rc["node_visits"], "prim_tests": rc["prim_tests"],
+                                "note": "NOT achieved: the reference LBVH walk's flops for this frame over this "
+                                        "kernel's time -- work the kernel did not do (its own walk is 'frac')",
                                 "source": "profiles/" + os.path.basename(rw)}
             except Exception:  # noqa: BLE001
                 ref_walk = None
@@ -589,10 +723,7 @@ def main():
                 cpu, ref = cpu_baseline(sc, cores, args.cpu_spp or sc.params.spp, bw=16 if cfg == "ns" else 64)
             rect, ref_rgba, ref_depth, ref_spp = ref
             if ref_spp == spp and not shard:  # the oracle rendered the same block at the frame's spp
-                dimg = None
-                if inw and buf["depth"] is not None:  # the last timed frame's depth tiles, assembled
-                    d = buf["depth"].unsqueeze(0).unsqueeze(-1).expand(-1, -1, -1, -1, 4).contiguous()
-                    dimg = assemble_lists(d, lists, nx, ny)[..., 0].cpu().numpy()
+                dimg = dimage.cpu().numpy() if dimage is not None else None  # the last timed frame's depth
                 parity = block_parity(rect, ref_rgba, ref_depth, image.cpu().numpy(), dimg)
         out = {
             "metric": METRIC,
@@ -625,7 +756,8 @@ def main():
                                  "achieved = SURVEY 8d F_alg per launch / average launch time (HIP events "
                                  "on the launch stream); F_alg counts this build's own node visits and object "
                                  "tests (4-wide culling walk, pixel beams), so it shrinks as the walk improves; "
-                                 "ref_walk = the same with the reference LBVH walk's counts of this frame; "
+                                 "ref_walk.equivalent_frac = the reference LBVH walk's flops of this frame over "
+                                 "this kernel's time (not achieved work); "
                                  "lane_issue_frac = VALU busy x lane utilisation (PMC); traffic = PMC HBM "
                                  "bytes per launch"},
             "valu": valu,
@@ -694,6 +826,8 @@ def main():
         print(json.dumps(out), flush=True)
         if args.save_image:
             np.save(args.save_image, image[:H, :W].cpu().numpy())
+            if dimage is not None:  # the r32f depth image beside it (<path>.depth.npy)
+                np.save(os.path.splitext(args.save_image)[0] + ".depth.npy", dimage[:H, :W].cpu().numpy())
     lib.rt_dev_scene_free(scene)
     if world > 1:
         dist.destroy_process_group()

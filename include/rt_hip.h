@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* status codes */
 #define RT_OK            0
@@ -125,6 +125,11 @@ typedef struct rt_options {
                                the host from the read-back LBVH, as rt_dev_scene_inw does) */
     int inw_claim_xcd;      /* pixel-major claims from 8 queues, one per XCD (an 8x8 block's pixels are
                                written by one XCD's L2, whole lines), idle XCDs taking from the others */
+    int inw_qnodes;         /* 1: pixel-major INW-01 frames with the fused cull run k_inw_pm's GQ instance
+                               (DESIGN.md §5.1): the reference's 40-float stacks in global memory with the
+                               top ray in registers, the wide walk's node stack and the top of the culling
+                               BVH in LDS (quantised 64-B nodes, 1,168 of them); 0 (default, measured faster):
+                               the FStack instance */
     /* IOW-03 (In-One-Weekend 03) */
     int iow_spec;           /* sample-parallel speculation (0: the sequential per-pixel kernel) */
     int iow_linear;         /* [build] the shader's linear object loop instead of the culling BVH */
@@ -323,6 +328,11 @@ typedef struct rt_path_info {
     int ring_lds;         /* 1: the fold ring was in LDS (k_inw_pm: inw_ring_pm = 0; k_inw_sm: inw_ring_sm = 0 and a BVH top of <= 5 nodes) */
     int stackless;        /* 1: the reference LBVH walks ran stackless where no push could drop */
     int lbvh_lds_nodes;   /* LBVH nodes the stackless walks read from LDS (no wide walk) */
+    int qnodes;           /* 1: the wide closest-hit walks read quantised nodes (inw_qnodes) */
+    int global_stack;     /* 1: the reference's 40-float stacks lived in global memory, not in LDS */
+    int walk_stack;       /* entries of the wide walks' own node stack per lane (LDS) */
+    uint64_t ref_walks;   /* INW: the last frame's closest-hit queries (segments + shadow rays) that the wide
+                             walk or beam list handed to the reference's LBVH walks (stackless or stack) */
 } rt_path_info;
 int rt_debug_path(rt_dev_scene *s, rt_path_info *out);
 
@@ -450,10 +460,15 @@ int rt_debug_time_kernels(int on);
 int rt_debug_check_fastmath(int which, uint64_t *mismatches, uint32_t *first_bad);
 int rt_debug_kernel_time(rt_dev_scene *s, double *ms_total, int *launches);
 /* The INW scene's walk structures (synchronises): info = {wide nodes, dfs_high, wide depth, RI grid
- * built, RI cells, stackless layout, objects, 0}; rank_out (2n, may be NULL) receives the objects'
+ * built, RI cells, stackless layout, objects, where the walk structures were built: 0 host, 1 device,
+ * 2 host after the device build ran past its level cap}; rank_out (2n, may be NULL) receives the objects'
  * depth-first ranks (invert 0, then 1) when the wide walk is built.  Lets the tests compare the
  * device build (rt_dev_scene_inw_update) with the host build of a fresh scene. */
 int rt_debug_wide_info(rt_dev_scene *s, uint32_t info[8], uint32_t *rank_out);
+/* Test hook: the device build of the walk structures (rt_dev_scene_inw_update) launches at most
+ * `levels` SAH / collapse levels (0 = its own cap, 256); a deeper tree is built on the host instead
+ * (rt_debug_wide_info info[7] = 2), which lets a test reach that fallback with an ordinary scene. */
+int rt_debug_build_level_cap(int levels);
 
 #ifdef __cplusplus
 }

@@ -29,8 +29,9 @@ constexpr int kB = 256;
 constexpr int kBins = 32;
 constexpr int kLevelBatch = 8;   // levels launched between two reads of the pending-task count
 constexpr int kSahFirst = 20;    // the binary SAH levels launched before the first read (C3's tree: ~20)
-constexpr int kMaxLevels = 256;  // binary SAH levels (a chain over n objects is at most n deep; the
-                                 // binned split halves a degenerate range, so depth <= ~2 log2 n)
+constexpr int kMaxLevels = 256;  // binary SAH levels launched at most; a deeper tree (a chain-like scene,
+                                 // where a split peels one object off per level) returns
+                                 // hipErrorNotSupported and the caller builds on the host (rt_capi.hip)
 
 // orderable bits of a float (a < b <=> ford(a) < ford(b)) for atomic min / max
 __device__ __forceinline__ uint32_t ford(float f) {
@@ -577,11 +578,15 @@ __global__ __launch_bounds__(kB) void k_ri_cells(const float4 *leafbox, uint32_t
                                                  uint32_t *fill, uint32_t *ids, uint32_t *flag) {
     const uint32_t g = blockIdx.x * kB + threadIdx.x;
     if (g >= n) return;  // no cross-lane work in this kernel
+    // pass 0 stops once a cell is known to list more than 64 objects (the grid is dropped then, as
+    // the host build stops at the first such cell): the count does not grow to O(n x cells) atomics
+    if (pass == 0 && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     const float4 n0 = leafbox[2 * g], n1 = leafbox[2 * g + 1];
     const float lo[3] = {n0.x, n0.y, n0.z}, hi[3] = {n0.w, n1.x, n1.y};
     int r0[3], r1[3];
     for (int a = 0; a < 3; a++) ri_range(d, lo[a], hi[a], a, r0[a], r1[a]);
-    for (int z = r0[2]; z <= r1[2]; z++)
+    for (int z = r0[2]; z <= r1[2]; z++) {
+        if (pass == 0 && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
         for (int y = r0[1]; y <= r1[1]; y++)
             for (int x = r0[0]; x <= r1[0]; x++) {
                 const size_t c = ((size_t)z * (size_t)d.dim[1] + (size_t)y) * (size_t)d.dim[0] + (size_t)x;
@@ -591,11 +596,95 @@ __global__ __launch_bounds__(kB) void k_ri_cells(const float4 *leafbox, uint32_t
                     ids[atomicAdd(fill + c, 1u)] = g;
                 }
             }
+    }
 }
 
 inline uint32_t nblk(size_t n) { return (uint32_t)((n + kB - 1) / kB); }
 
+// ---- quantised wide nodes (InwScene::qnodes, DESIGN.md §5.2 "Quantised nodes")
+// Per node and axis: origin o (a float at or below the lowest child plane minus the margin m) and
+// scale s >= 1e-4 (o + 255 s at or above the highest plane plus m); a child's low plane becomes
+// the byte q with o + q s <= lo - m, its high plane the byte with o + q s >= hi + m (real
+// arithmetic, checked in double on the exact float values).  An empty slot (link 1e9) gets low
+// bytes 255 and high bytes 0: an interval reversed by 255 s >= 0.0255, which no rounding of the
+// walk's fma closes.  The walk computes t = fma(q, s / d, (o - ray origin) / d); DESIGN.md §2 bounds
+// its error below m / |d| while every coordinate and ray origin lies within 1000 of the origin (the
+// fused cull's condition, required for these nodes), so the decoded boxes stay conservative.
+__device__ __forceinline__ float f32_next_up(float f) {  // finite f: the next float above
+    if (f == 0.0f) return __uint_as_float(1u);
+    const uint32_t u = __float_as_uint(f);
+    return __uint_as_float(f > 0.0f ? u + 1u : u - 1u);
+}
+__device__ __forceinline__ float f32_next_down(float f) { return -f32_next_up(-f); }
+__device__ __forceinline__ float f32_down(double x) {
+    float f = (float)x;
+    if ((double)f > x) f = f32_next_down(f);
+    return f;
+}
+__device__ __forceinline__ float f32_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = f32_next_up(f);
+    return f;
+}
+__global__ __launch_bounds__(kB) void k_quantize_wnodes(const float4 *wn, uint32_t nw, float4 *qn, float margin) {
+    const uint32_t w = blockIdx.x * kB + threadIdx.x;
+    if (w >= nw) return;  // no cross-lane work in this kernel
+    const float4 *nd = wn + (size_t)w * 10;
+    const float4 pl4[6] = {nd[0], nd[1], nd[2], nd[3], nd[4], nd[5]};
+    const float4 lk = nd[9];
+    auto comp = [](const float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
+    bool empty[4];
+    for (int k = 0; k < 4; k++) empty[k] = __float_as_int(comp(lk, k)) == 1000000000;
+    const double m = (double)margin;
+    float org[3], scl[3];
+    uint32_t qlo[3] = {0u, 0u, 0u}, qhi[3] = {0u, 0u, 0u};
+    for (int a = 0; a < 3; a++) {
+        double nlo = 0.0, nhi = 0.0;
+        bool any = false;
+        for (int k = 0; k < 4; k++) {
+            if (empty[k]) continue;
+            const double lo = comp(pl4[a], k), hi = comp(pl4[3 + a], k);
+            nlo = any ? fmin(nlo, lo) : lo;
+            nhi = any ? fmax(nhi, hi) : hi;
+            any = true;
+        }
+        const float o = f32_down(nlo - m);
+        float s = f32_up(fmax(((nhi + m) - (double)o) / 255.0, 1e-4));
+        while ((double)o + 255.0 * (double)s < nhi + m) s = f32_next_up(s);
+        org[a] = o;
+        scl[a] = s;
+        for (int k = 0; k < 4; k++) {
+            uint32_t ql = 255u, qh = 0u;
+            if (!empty[k]) {
+                const double lo = (double)comp(pl4[a], k) - m, hi = (double)comp(pl4[3 + a], k) + m;
+                int q = (int)floor((lo - (double)o) / (double)s);
+                q = q < 0 ? 0 : (q > 255 ? 255 : q);
+                while (q > 0 && (double)o + (double)q * (double)s > lo) q--;
+                int r = (int)ceil((hi - (double)o) / (double)s);
+                r = r < 0 ? 0 : (r > 255 ? 255 : r);
+                while (r < 255 && (double)o + (double)r * (double)s < hi) r++;
+                ql = (uint32_t)q;
+                qh = (uint32_t)r;
+            }
+            qlo[a] |= ql << (8 * k);
+            qhi[a] |= qh << (8 * k);
+        }
+    }
+    float4 *o4 = qn + (size_t)w * kQNodeF4;
+    o4[0] = make_float4(org[0], org[1], org[2], scl[0]);
+    o4[1] = make_float4(scl[1], scl[2], __uint_as_float(qlo[0]), __uint_as_float(qlo[1]));
+    o4[2] = make_float4(__uint_as_float(qlo[2]), __uint_as_float(qhi[0]), __uint_as_float(qhi[1]), __uint_as_float(qhi[2]));
+    o4[3] = lk;
+}
+
 }  // namespace
+
+hipError_t inw_quantize_wnodes(const float4 *wnodes, uint32_t nw, float4 *qnodes, float margin, hipStream_t s) {
+    if (!nw) return hipSuccess;
+    if (!wnodes || !qnodes || !(margin > 0.0f)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_quantize_wnodes, dim3(nblk(nw)), dim3(kB), 0, s, wnodes, nw, qnodes, margin);
+    return hipGetLastError();
+}
 
 // workspace carve-up (256-B aligned pieces)
 struct BuildWs {
@@ -642,7 +731,8 @@ size_t inw_build_workspace_bytes(uint32_t n) { return n ? carve(reinterpret_cast
     } while (0)
 
 hipError_t inw_wide_build_device(const float4 *nodes, const uint32_t *lcnt, uint32_t n, void *ws, size_t ws_bytes,
-                                 InwWideDev &out, hipStream_t s) {
+                                 InwWideDev &out, hipStream_t s, int max_levels) {
+    const int lvl_cap = max_levels > 0 && max_levels < kMaxLevels ? max_levels : kMaxLevels;
     if (n < 2 || !nodes || !lcnt || !ws || ws_bytes < inw_build_workspace_bytes(n) || !out.wnodes || !out.rank || !out.leafbox)
         return hipErrorInvalidValue;
     BuildWs w;
@@ -667,7 +757,7 @@ hipError_t inw_wide_build_device(const float4 *nodes, const uint32_t *lcnt, uint
     BUILD_HIP(hipMemcpyAsync(w.lvl_cnt, &one, 4, hipMemcpyHostToDevice, s));
     int lvl = 0;
     for (int batch = kSahFirst;; batch = kLevelBatch) {
-        for (int k = 0; k < batch && lvl < kMaxLevels; k++, lvl++)
+        for (int k = 0; k < batch && lvl < lvl_cap; k++, lvl++)
             hipLaunchKernelGGL(k_sah_level, dim3(1024), dim3(kB), 0, s, w.task[lvl & 1], w.lvl_cnt + lvl,
                                w.task[(lvl + 1) & 1], w.lvl_cnt + lvl + 1, (lvl & 1) ? w.ids2 : w.ids,
                                (lvl & 1) ? w.ids : w.ids2, w.box, w.cen, w.bin);
@@ -676,7 +766,7 @@ hipError_t inw_wide_build_device(const float4 *nodes, const uint32_t *lcnt, uint
         BUILD_HIP(hipMemcpyAsync(&pending, w.lvl_cnt + lvl, 4, hipMemcpyDeviceToHost, s));
         BUILD_HIP(hipStreamSynchronize(s));
         if (pending == 0) break;
-        if (lvl >= kMaxLevels) return hipErrorNotSupported;  // deeper than any binned split makes
+        if (lvl >= lvl_cap) return hipErrorNotSupported;  // deeper than the cap: the caller builds on the host
     }
     // 4-wide collapse; meta[1] = wide node counter (1: the root, from binary node 0)
     const uint2 wroot = make_uint2(0u, 0u);
@@ -685,7 +775,7 @@ hipError_t inw_wide_build_device(const float4 *nodes, const uint32_t *lcnt, uint
     BUILD_HIP(hipMemcpyAsync(w.meta + 1, &one, 4, hipMemcpyHostToDevice, s));
     int wl = 0;
     for (;;) {
-        for (int k = 0; k < kLevelBatch && wl < kMaxLevels; k++, wl++)
+        for (int k = 0; k < kLevelBatch && wl < lvl_cap; k++, wl++)
             hipLaunchKernelGGL(k_collapse_level, dim3(nblk(n)), dim3(kB), 0, s, w.wtask[wl & 1], w.wlvl_cnt, wl,
                                w.wtask[(wl + 1) & 1], w.bin, out.wnodes, w.meta);
         BUILD_HIP(hipGetLastError());
@@ -707,7 +797,7 @@ hipError_t inw_wide_build_device(const float4 *nodes, const uint32_t *lcnt, uint
             for (int a = 0; a < 3; a++) { out.ri_lo[a] = dec(b[a]); out.ri_hi[a] = dec(b[3 + a]); }
             break;
         }
-        if (wl >= kMaxLevels) return hipErrorNotSupported;
+        if (wl >= lvl_cap) return hipErrorNotSupported;
     }
     return hipSuccess;
 }

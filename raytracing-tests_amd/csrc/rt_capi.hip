@@ -33,7 +33,7 @@ rt_options default_options() {
     o.size = sizeof(rt_options);
     o.inw_wide_walk = 1; o.inw_order = 0; o.inw_beams = 1; o.inw_ri_grid = 1; o.inw_lds_nodes = 1;
     o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 0; o.inw_ring_sm = 0; o.inw_stackless = 1;
-    o.inw_device_build = 1; o.inw_claim_xcd = 1;
+    o.inw_device_build = 1; o.inw_claim_xcd = 1; o.inw_qnodes = 0;
     o.iow_spec = 1; o.iow_linear = 0; o.iow_narrow = 0; o.iow_lds_bvh = 1;
     o.iow_leaf_batch = 32;  // 32 measured 2.5% faster on the bench frame than 65 (round 2)
     o.iow_coop_max = 4; o.iow_chunks_lpt = 0;
@@ -56,6 +56,7 @@ bool options_ok(const rt_options *o) {
 }
 rt_options g_opt = default_options();
 unsigned *g_px_rays = nullptr;        // rt_debug_pixel_rays(): rays per work unit
+int g_build_levels = 0;               // rt_debug_build_level_cap(): the device build's level cap (0 = 256)
 
 #define HIP_OK(expr)                                             \
     do {                                                         \
@@ -172,6 +173,9 @@ struct rt_dev_scene {
     DevBuf obox;  // IOW-03: per-object culling boxes (2 float4 each) for wave-cooperative queries
     DevBuf tex, tex_info;  // INW-04 material textures (float4 texels, (first, w, h, 0) per texture)
     DevBuf wnodes, wrank, wleaf;  // INW wide walk: culling BVH, depth-first ranks, LBVH leaf boxes
+    DevBuf qnodes;                // ... the culling BVH quantised (4 float4 per node, rtk::inw_quantize_wnodes)
+    DevBuf gstk;                  // k_inw_pm's GQ instance: the reference's 40-float stacks, 160 B per lane
+    DevBuf walk_ctr;              // the last frame's closest-hit queries handed to the LBVH walks (u64)
     DevBuf ri_cells, ri_ids;      // INW surrounding-RI grid (cell offsets, object ids)
     float ri_lo[3] = {}, ri_hi[3] = {}, ri_inv[3] = {};
     int ri_dim[3] = {};
@@ -185,6 +189,7 @@ struct rt_dev_scene {
     uint32_t last_force = 0;      // ... its forced order (0: the probe's pick, read back from inw_mode)
     bool last_lring = false;      // ... k_inw_pm's fold ring was in LDS
     bool last_lring_sm = false;   // ... k_inw_sm's
+    bool last_gq = false;         // ... k_inw_pm's GQ instance (quantised nodes, global stacks)
     char kname[64] = {0};         // the fold kernel's instance name (rt_debug_launches)
     uint32_t last_ring[2] = {0, 0};  // ... its fold windows (pixel-major, sample-major)
     uint32_t ring_frame = 0;         // frames rendered with the current fold rings (their tag epoch)
@@ -193,6 +198,8 @@ struct rt_dev_scene {
     float wbound = 0.0f;          // largest |coordinate| of the INW culling boxes (the fused cull's condition)
     uint32_t dfs_high = 0;        // the reference walk's stack high-water mark (0: no walkable LBVH)
     bool sl_ok = false;           // the node buffer has the stackless walks' layout (lbvh_walk_info)
+    uint32_t wbuild = 0;          // where the walk structures were built: 0 host, 1 device, 2 host after the
+                                  // device build ran past its level cap (rt_debug_wide_info info[7])
     uint32_t n_tex = 0;
     // chunked-render workspace, sized for `ws_units` pixel units (grown on demand)
     uint32_t ws_units = 0;
@@ -368,6 +375,18 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     }
 }
 
+// The quantised culling BVH (DESIGN.md §5.2 "Quantised nodes") from the scene's wide nodes, on the
+// device: planes rounded outward by kQMargin beyond the wide nodes' own (the error bound of the
+// walk's decode is below it while every coordinate lies within 1000 of the origin, the fused
+// cull's condition, which the launch checks per frame)
+constexpr float kQMargin = 2e-3f;
+int make_qnodes(rt_dev_scene *s) {
+    if (!s->n_wnodes) return RT_OK;
+    HIP_OK(s->qnodes.reserve(size_t(s->n_wnodes) * rtk::kQNodeF4 * sizeof(float4)));
+    HIP_OK(rtk::inw_quantize_wnodes(s->wnodes.as<float4>(), s->n_wnodes, s->qnodes.as<float4>(), kQMargin, nullptr));
+    return RT_OK;
+}
+
 // The wide walk's structures and the RI grid, built on the host (rtamd::inw_wide_build,
 // rtamd::ri_grid_build) and uploaded.
 // ms (may be null): host time of the builds, then of the uploads
@@ -406,6 +425,7 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n, double *ms = 
     s->sl_ok = sl;
     s->wdepth = w.depth;
     s->wbound = w.wbound;
+    if (int rc = make_qnodes(s); rc != RT_OK) return rc;
     if (ms) ms[1] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     return RT_OK;
 }
@@ -471,8 +491,12 @@ int make_inw_wide_device(rt_dev_scene *s, uint32_t n, double *ms) {
     const size_t wsb = rtk::inw_build_workspace_bytes(n);
     HIP_OK(s->build_ws.reserve(wsb));
     rtk::InwWideDev out{s->wnodes.as<float4>(), s->wrank.as<uint32_t>(), s->wleaf.as<float4>(), 0, 0, 0, 0.0f, {}, {}};
-    HIP_OK(rtk::inw_wide_build_device(s->nodes.as<float4>(), s->lcnt.as<uint32_t>(), n, s->build_ws.p,
-                                      s->build_ws.bytes, out, nullptr));
+    {
+        const hipError_t be = rtk::inw_wide_build_device(s->nodes.as<float4>(), s->lcnt.as<uint32_t>(), n,
+                                                         s->build_ws.p, s->build_ws.bytes, out, nullptr, g_build_levels);
+        if (be == hipErrorNotSupported) return RT_E_UNSUPPORTED;  // deeper than its level cap: the caller builds on the host
+        HIP_OK(be);
+    }
     if (s->opt.inw_wide_walk) {
         double dlo[3], dhi[3], inv[3];
         int dim[3];
@@ -500,6 +524,7 @@ int make_inw_wide_device(rt_dev_scene *s, uint32_t n, double *ms) {
         s->n_wnodes = out.n_wnodes;
         s->wdepth = out.depth;
         s->wbound = out.wbound;
+        if (int rc = make_qnodes(s); rc != RT_OK) return rc;
     }
     HIP_OK(hipDeviceSynchronize());
     s->dfs_high = out.dfs_high;
@@ -564,8 +589,22 @@ int update_inw(rt_dev_scene *s, const float *geom, uint32_t n, const float *node
     lap(1);
     double w[2] = {0.0, 0.0};
     if (device_build) {
-        if (int rc = make_inw_wide_device(s, n, w); rc != RT_OK) return rc;
-    } else if (int rc = make_inw_wide(s, nodes, n, w); rc != RT_OK) return rc;
+        int rc = make_inw_wide_device(s, n, w);
+        s->wbuild = 1;
+        if (rc == RT_E_UNSUPPORTED) {
+            // the binned SAH tree ran past the device build's level cap (a chain-like scene: a split
+            // can peel one object off per level); the host builders have no such limit, so read the
+            // device LBVH back and build the walk structures there, as rt_dev_scene_inw does
+            host_nodes.resize(nbytes / sizeof(float));
+            HIP_OK(hipMemcpy(host_nodes.data(), s->nodes.p, nbytes, hipMemcpyDeviceToHost));
+            rc = make_inw_wide(s, host_nodes.data(), n, w);
+            s->wbuild = 2;
+        }
+        if (rc != RT_OK) return rc;
+    } else {
+        if (int rc = make_inw_wide(s, nodes, n, w); rc != RT_OK) return rc;
+        s->wbuild = 0;
+    }
     if (ms) { ms[2] = w[0]; ms[3] = w[1]; }
     s->n = n;
     s->n_lights = nl;
@@ -659,12 +698,14 @@ int ensure_lanes(rt_dev_scene *s, int groups, size_t temp_bytes) {
 // reuse a freed scene's memory never takes that scene's records for its own (the same render of
 // the full frame, then of one tile alone, found the full frame's records at its own indices and
 // returned their colours), and a scene clears its flags when its tag comes round again.
-unsigned next_spec_epoch(rt_dev_scene *s) {
+// The clear goes on the render's stream st, ordered after the scene's earlier frames on that stream
+// (a null-stream memset would not wait for a non-blocking caller stream).
+unsigned next_spec_epoch(rt_dev_scene *s, hipStream_t st) {
     static std::atomic<unsigned> g{0};
     unsigned v;
     do v = (g.fetch_add(1u) + 1u) & 0xffffu; while (v == 0u);
     if (v <= s->epoch && s->sp_col.p)  // wrapped since this scene's last frame: forget its tags
-        (void)hipMemset(s->sp_col.p, 0, s->sp_col.bytes);
+        (void)hipMemsetAsync(s->sp_col.p, 0, s->sp_col.bytes, st);
     s->epoch = v;
     return v;
 }
@@ -720,6 +761,11 @@ int launch_scene(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     f.coop_max = s->opt.iow_coop_max;
     f.narrow = s->opt.iow_narrow;
     s->last_path = rt_path_info{};
+    if (s->kind != 3) {  // the frame's closest-hit queries that fell back to the LBVH walks (rt_debug_path)
+        HIP_OK(s->walk_ctr.reserve(sizeof(unsigned long long)));
+        HIP_OK(hipMemsetAsync(s->walk_ctr.p, 0, sizeof(unsigned long long), st));
+        f.walk_ctr = s->walk_ctr.as<unsigned long long>();
+    }
     if (s->kind == 3 && s->opt.iow_spec && !rtk::iow_narrow(f) && s->s_stop > 0 &&
         ensure_spec(s, rtk::units_of(f), uint32_t(s->s_stop)))
         return launch_scene_spec(s, f, st);
@@ -861,7 +907,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     unsigned *sc = s->sp_counts.as<unsigned>();  // group g: [32g] list count, [32g+16] fallback count
     rtk::SpecRecs R{s->sp_col.as<float4>(), s->sp_fin.as<float4>(), s->sp_ctr.as<uint4>(),
                           s->sp_assume.as<float4>(), P, S, s->sp_list.as<uint32_t>(), sc, s->sp_fb.as<uint32_t>(),
-                          sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), next_spec_epoch(s),
+                          sc + 16, s->ws_order.as<uint32_t>(), 0, 0, s->sp_pstate.as<uint4>(), next_spec_epoch(s, st),
                           s->sp_front.as<uint4>(), s->sp_sorder.as<uint32_t>(),
                           uint32_t(o.spec_probe),
                           S > 2 && groups == 1 ? uint32_t(std::min(int(S) - 2, o.spec_heavy >= 0 ? o.spec_heavy
@@ -1286,6 +1332,22 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                           2.0f + std::fabs(f.aperture);
         sc.fused = (o.inw_fused_cull && f.n_focus == 0 && std::fmax(cam, s->wbound) <= 1000.0f) ? 1 : 0;
     }
+    // GQ: k_inw_pm over the quantised nodes with the reference's stacks in global
+    // memory -- INW-01, the LDS ring instances, the fused cull's error bound (the quantised decode
+    // is argued under it)
+    if (o.inw_qnodes && s->layout != 4 && lring && sc.fused && sc.wnodes && s->qnodes.p) {
+        const uint32_t gb = uint32_t(s->cus * rtk::resident_blocks_per_cu(19));
+        const size_t need = size_t(gb) * rtk::kGqSub * rtk::kBlock * (rtk::kFStack / 4) * sizeof(float4);
+        if (s->gstk.bytes < need) {
+            s->gstk.~DevBuf();
+            new (&s->gstk) DevBuf();
+            if (s->gstk.alloc(need) != hipSuccess) { s->gstk.bytes = 0; return RT_E_HIP; }
+        }
+        if (rtk::kGqQn) sc.qnodes = s->qnodes.as<float4>();
+        sc.gstk = s->gstk.as<float4>();
+        sc.gq_blocks = gb;
+    }
+    s->last_gq = sc.gstk != nullptr;
     const uint32_t force = (o.inw_order == 1 || o.inw_order == 2) ? uint32_t(o.inw_order) : 0u;
     s->last_force = force;
     s->last_ring[0] = ring_pm;
@@ -1338,6 +1400,11 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         P.lbvh_lds_nodes = s->last_ln && sc.sl && !sc.wnodes
                                ? int(std::min<uint32_t>(2 * s->n - 1, uint32_t(rtk::kInwLdsNodes * 10 / 2))) : 0;
         P.claim_order = cost != nullptr;
+        P.qnodes = sc.qnodes != nullptr;
+        P.global_stack = sc.gstk != nullptr;
+        P.walk_stack = sc.gstk ? rtk::kWStack : rtk::kFStack - 3;
+        if (sc.gstk)
+            P.lds_nodes = int(std::min<uint32_t>(s->n_wnodes, uint32_t(rtk::kGqQn ? rtk::kQLdsNodes : rtk::kInwLdsNodes)));
     }
     if (epoch == 0) e = hipMemsetAsync(s->inw_ring.p, 0xff, s->inw_ring.bytes, st);
     if (e == hipSuccess) s->ring_frame = epoch + 1;
@@ -1479,6 +1546,9 @@ template <class F> int timed(F &&fn, double *ms) {
 extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
+}  // extern "C"
+int rtamd::scene_device(const rt_dev_scene *s) { return s ? s->device : -1; }
+extern "C" {
 
 void rt_options_default(rt_options *o) {
     if (o) *o = default_options();
@@ -1520,13 +1590,19 @@ int rt_dev_scene_set_options(rt_dev_scene *s, const rt_options *o) {
     return RT_OK;
 }
 
+int rt_debug_build_level_cap(int levels) {
+    if (levels < 0) return RT_E_ARG;
+    g_build_levels = levels;
+    return RT_OK;
+}
+
 int rt_debug_wide_info(rt_dev_scene *s, uint32_t info[8], uint32_t *rank_out) {
     if (!s || s->kind == 3 || !info) return RT_E_ARG;
     HIP_OK(hipSetDevice(s->device));
     HIP_OK(hipDeviceSynchronize());
     const uint32_t cells = s->ri_ok ? uint32_t(s->ri_dim[0]) * uint32_t(s->ri_dim[1]) * uint32_t(s->ri_dim[2]) : 0u;
     const uint32_t v[8] = {s->n_wnodes, s->dfs_high, uint32_t(s->wdepth), s->ri_ok ? 1u : 0u, cells,
-                           s->sl_ok ? 1u : 0u, s->n, 0u};
+                           s->sl_ok ? 1u : 0u, s->n, s->wbuild};
     std::memcpy(info, v, sizeof(v));
     if (rank_out && s->n_wnodes)
         HIP_OK(hipMemcpy(rank_out, s->wrank.p, size_t(s->n) * 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -1541,11 +1617,17 @@ int rt_debug_path(rt_dev_scene *s, rt_path_info *out) {
     rt_path_info P = s->last_path;
     std::memcpy(P.kernel, name, sizeof(P.kernel));
     P.launches = n;
+    P.ref_walks = 0;
+    if (s->kind != 3 && s->walk_ctr.p) {
+        unsigned long long v = 0;
+        HIP_OK(hipMemcpy(&v, s->walk_ctr.p, sizeof(v), hipMemcpyDeviceToHost));
+        P.ref_walks = v;
+    }
     if (std::strncmp(name, "k_inw_pm", 8) == 0) {
         P.order = 1;
         P.ring_entries = int(s->last_ring[0]);
         P.ring_lds = s->last_lring ? 1 : 0;
-        if (s->last_lring) { P.lds_nodes = 0; P.lbvh_lds_nodes = 0; }  // the ring instances stage no nodes
+        if (s->last_lring && !s->last_gq) { P.lds_nodes = 0; P.lbvh_lds_nodes = 0; }  // the FStack ring instances stage no nodes
     }
     else if (std::strncmp(name, "k_inw_sm", 8) == 0) {
         P.order = 2;
@@ -1553,6 +1635,10 @@ int rt_debug_path(rt_dev_scene *s, rt_path_info *out) {
         P.ring_lds = s->last_lring_sm ? 1 : 0;
         if (s->last_lring_sm) P.lds_nodes = std::min(P.lds_nodes, int(rtk::kPmLdsNodes));
         if (s->last_lring_sm) P.lbvh_lds_nodes = std::min(P.lbvh_lds_nodes, int(rtk::kPmLdsNodes * 10 / 2));
+        if (s->last_gq) {  // the GQ instance is pixel-major only: k_inw_sm ran the 236-node FStack kernel
+            P.qnodes = 0; P.global_stack = 0; P.walk_stack = rtk::kFStack - 3;
+            P.lds_nodes = s->last_lring_sm ? std::min(s->n_wnodes, rtk::kPmLdsNodes) : std::min(s->n_wnodes, uint32_t(rtk::kInwLdsNodes));
+        }
     }
     if (P.order != 1) { P.beams = 0; P.claim_order = 0; }  // both serve the pixel-major kernel only
     *out = P;

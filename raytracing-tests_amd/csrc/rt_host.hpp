@@ -174,4 +174,7 @@ int scene_preset(int preset, uint32_t seed, int n_hint, std::vector<rt_geom_desc
 // bench.py deal_order is the same function.
 std::vector<std::pair<int, int>> tile_deal(int W, int H, int T, int n_dev);
 
+// the device a device scene was built on (rt_capi.hip; the multi-GPU group checks its scene list)
+int scene_device(const struct rt_dev_scene *s);
+
 }  // namespace rtamd

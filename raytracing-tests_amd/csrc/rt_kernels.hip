@@ -13,6 +13,7 @@
 //   k_inw   <- In-Next-Week/01_BoundingVolumeHierarchy/computeShaderSrc.glsl:230-675 (LIGHTS=false)
 //              In-Next-Week/04_Lights_Camera_And_Action/computeShaderSrc.glsl:243-773 (LIGHTS=true)
 #include <cstdlib>
+#include <type_traits>
 
 #include "rt_kernels.hpp"
 #include "rt_math.hpp"
@@ -56,6 +57,7 @@ enum { kOccSeg = 0, kOccWalk = 2, kOccNode = 4, kOccLeaf = 6, kOccBeam = 8, kOcc
        kOccUni = 16, kOccSlots = 18 };
 struct Ctr {
     uint32_t seg = 0, nodes = 0, prims = 0, shadow = 0, drops = 0, nans = 0;
+    uint32_t refw = 0;  // INW closest-hit queries the wide walk / beam list handed to the LBVH walks (Frame::walk_ctr)
     unsigned long long *wdbg = nullptr;  // diagnostics: this wave's kDbg* row in LDS, or null
 #ifdef RT_DIAG_SPLIT
     unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // INW phase cycles of this wave (k_inw_pm/sm)
@@ -134,6 +136,10 @@ __device__ __forceinline__ void flush(const Frame &f, const Ctr &c) {
     for (int i = 0; i < 6; i++) {
         unsigned long long s = wave_sum(v[i]);
         if ((threadIdx.x & 63) == 0 && s) atomicAdd(f.counters + i, s);
+    }
+    if (f.walk_ctr) {
+        const unsigned long long s = wave_sum((unsigned long long)c.refw);
+        if ((threadIdx.x & 63) == 0 && s) atomicAdd(f.walk_ctr, s);
     }
 }
 
@@ -1651,7 +1657,6 @@ __global__ __launch_bounds__(kBlock) void k_iow03_resolve(Frame f, SpecRecs R, i
 }
 
 // ============================================================================ INW
-constexpr int kFStack = 40;  // stack_capacity, 01_BVH...glsl:80
 constexpr float kMaxT = 32000.0f;
 
 struct FStack {  // FLT_STACK (01_BVH...glsl:81-107) in LDS, [slot][thread]
@@ -1668,6 +1673,92 @@ struct FStack {  // FLT_STACK (01_BVH...glsl:81-107) in LDS, [slot][thread]
             at(size + 6) = contrib; at(size + 7) = bounced;
             size += 8;
         } else c.drops++;
+    }
+    // the top ray (8 floats: origin, direction, contribution, bounced) off the stack
+    __device__ __forceinline__ void pop_ray(f3 &o, f3 &d, float &contrib, float &bounced) {
+        size -= 8;
+        o = f3{at(size), at(size + 1), at(size + 2)};
+        d = f3{at(size + 3), at(size + 4), at(size + 5)};
+        contrib = at(size + 6);
+        bounced = at(size + 7);
+    }
+    __device__ __forceinline__ void reset(uint32_t n) { size = n; }
+    // the top entry is a primary ray (bounced == 0)
+    __device__ __forceinline__ bool top_primary() { return size >= 8u && at(size - 1u) == 0.0f; }
+    // the wide walks' node stack: the free part above the stack (+ extra floats), kBlock apart;
+    // cap = entries left after `spare` slots for branch-free pushes
+    __device__ __forceinline__ float *walk_stack(uint32_t extra, int spare, int &cap) {
+        cap = kFStack - spare - (int)(size + extra);
+        return &at(size + extra);
+    }
+};
+
+// The same stack for k_inw_pm's GQ instance (DESIGN.md §5.1 "GQ"): the 40 floats in global memory
+// ([slot4][lane] float4 columns, `stride` lanes apart; touched about once per segment), the top ray
+// in registers -- a segment pops the ray the one before pushed last, so most pops read no memory
+// -- and the wide walks' node stack in LDS (kWStack entries per lane, kBlock apart).  The
+// capacity and drop semantics are FStack's: size counts every float, pushes drop when it is full.
+// Invariant: a primary ray (bounced 0) is only ever the register top (pushed at a sample's start or
+// by the MULTIFOCUS chain, popped by the next segment), so top_primary reads no memory.
+struct GStack {
+    float4 *col;        // this lane's column: slot4 k at col[k * stride]
+    uint32_t stride;
+    uint32_t size;
+    float *ws;          // LDS node stack of the wide walks
+    bool rc;            // the top 8 floats are the register ray (r0, r1); their memory is stale
+    float4 r0, r1;      // o.xyz d.x | d.yz contrib bounced
+    __device__ __forceinline__ float &at(uint32_t k) {
+        return reinterpret_cast<float *>(col + (size_t)(k >> 2) * stride)[k & 3u];
+    }
+    __device__ __forceinline__ void flush() {  // the register ray to its slots size - 8 .. size - 1
+        const uint32_t b = size - 8u;
+        if ((b & 3u) == 0u) {
+            col[(size_t)(b >> 2) * stride] = r0;
+            col[(size_t)((b >> 2) + 1u) * stride] = r1;
+        } else {
+            at(b) = r0.x; at(b + 1) = r0.y; at(b + 2) = r0.z; at(b + 3) = r0.w;
+            at(b + 4) = r1.x; at(b + 5) = r1.y; at(b + 6) = r1.z; at(b + 7) = r1.w;
+        }
+        rc = false;
+    }
+    __device__ __forceinline__ void push(float v, Ctr &c) {
+        if (size < kFStack) {
+            if (rc) flush();
+            at(size) = v;
+            size++;
+        } else c.drops++;
+    }
+    __device__ __forceinline__ void push_ray(f3 o, f3 d, float contrib, float bounced, Ctr &c) {
+        if (size < kFStack - 7) {
+            if (rc) flush();
+            r0 = make_float4(o.x, o.y, o.z, d.x);
+            r1 = make_float4(d.y, d.z, contrib, bounced);
+            rc = true;
+            size += 8;
+        } else c.drops++;
+    }
+    __device__ __forceinline__ void pop_ray(f3 &o, f3 &d, float &contrib, float &bounced) {
+        size -= 8;
+        if (!rc) {
+            if ((size & 3u) == 0u) {
+                r0 = col[(size_t)(size >> 2) * stride];
+                r1 = col[(size_t)((size >> 2) + 1u) * stride];
+            } else {
+                r0 = make_float4(at(size), at(size + 1), at(size + 2), at(size + 3));
+                r1 = make_float4(at(size + 4), at(size + 5), at(size + 6), at(size + 7));
+            }
+        }
+        rc = false;
+        o = f3{r0.x, r0.y, r0.z};
+        d = f3{r0.w, r1.x, r1.y};
+        contrib = r1.z;
+        bounced = r1.w;
+    }
+    __device__ __forceinline__ void reset(uint32_t n) { size = n; rc = false; }
+    __device__ __forceinline__ bool top_primary() { return rc && r1.w == 0.0f; }
+    __device__ __forceinline__ float *walk_stack(uint32_t, int spare, int &cap) {
+        cap = kWStack - spare;
+        return ws;
     }
 };
 
@@ -1738,8 +1829,8 @@ __device__ __forceinline__ bool test_aabb_te(float4 n0, float4 n1, f3 o, f3 id, 
 }
 
 // closest-hit LBVH DFS (01_BVH...glsl:431-473, 04...glsl:524-563, shadow 620-657)
-template <bool WANT_NORMAL, bool EO = true>
-__device__ float inw_traverse(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
+template <bool WANT_NORMAL, bool EO = true, class KS = FStack>
+__device__ float inw_traverse(const InwScene &S, KS &K, f3 o, f3 d, float ratio, bool invert,
                               float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c) {
     float final_geom = init_geom;
     const uint32_t I = K.size;
@@ -1788,7 +1879,8 @@ __device__ float inw_traverse(const InwScene &S, FStack &K, f3 o, f3 d, float ra
 }
 
 // Surrounding refractive index (01_BVH...glsl:272-345, 486-502)
-__device__ float inw_surrounding_ri(const InwScene &S, FStack &K, f3 hp, float ratio, Ctr &c) {
+template <class KS = FStack>
+__device__ float inw_surrounding_ri(const InwScene &S, KS &K, f3 hp, float ratio, Ctr &c) {
     float acc = 0.0f;
     uint32_t cnt = 0;
     const uint32_t I = K.size;
@@ -1871,6 +1963,34 @@ __device__ __forceinline__ void inw_wnode_nf(const InwScene &S, int cur, uint32_
     const float4 *px = nd + ox, *py = nd + oy, *pz = nd + oz;
     nx = px[0]; fx = px[3]; ny = py[0]; fy = py[3]; nz = pz[0]; fz = pz[3]; lk = nd[9];
 }
+// The same fetch from global memory as buffer loads: the node's byte offset is 32 bits (a node
+// index times 160), the octant offsets and the far planes' +48 / the links' +144 fold into the
+// instructions, so a node step spends 4 VALU on addresses instead of the 64-bit pointer sums (~10)
+// (RT_INW_BUFLOAD experiment)
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wnode_rsrc(const InwScene &S) {
+    // dword 3 = 0x00020000: the gfx9-family raw-buffer format word; num_records bounds the nodes
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(S.wnodes), (short)0,
+                                             (int)(S.n_wnodes * (uint32_t)kInwNodeF4 * 16u), 0x00020000);
+}
+template <bool LN>
+__device__ __forceinline__ void inw_wnode_nf_buf(const InwScene &S, __amdgpu_buffer_rsrc_t rs, int cur, uint32_t oxb,
+                                                 uint32_t oyb, uint32_t ozb, float4 &nx, float4 &ny, float4 &nz,
+                                                 float4 &fx, float4 &fy, float4 &fz, float4 &lk) {
+    if (LN && (uint32_t)(cur - 1) < S.n_lnodes) {
+        const float4 *nd = g_inw_lnodes + kInwNodeF4 * (cur - 1);
+        const float4 *px = nd + (oxb >> 4), *py = nd + (oyb >> 4), *pz = nd + (ozb >> 4);
+        nx = px[0]; fx = px[3]; ny = py[0]; fy = py[3]; nz = pz[0]; fz = pz[3]; lk = nd[9];
+        return;
+    }
+    const uint32_t b = __umul24((uint32_t)(cur - 1), (uint32_t)(kInwNodeF4 * 16));  // v_mul_u32_u24 (ids < 2^24)
+    nx = bload4(rs, b + oxb); fx = bload4(rs, b + oxb + 48u);
+    ny = bload4(rs, b + oyb); fy = bload4(rs, b + oyb + 48u);
+    nz = bload4(rs, b + ozb); fz = bload4(rs, b + ozb + 48u);
+    lk = bload4(rs, b + 144u);
+}
 // FU: one fused multiply-add per plane, plane * (1/d) + (-o * (1/d)), the second term computed
 // once per ray (noid).  Its rounding error in t is at most |o| * 2^-23 * |1/d| per axis, against a
 // culling-box inflation of e >= 1e-3 (x |1/d| in t), so it stays conservative while
@@ -1914,6 +2034,51 @@ __device__ __forceinline__ void cull4nf(const float4 nx, const float4 ny, const 
     t1 = one(a[0].y, a[2].y, a[4].y, a[6].y, a[8].y, a[10].y);
     t2 = one(a[1].x, a[3].x, a[5].x, a[7].x, a[9].x, a[11].x);
     t3 = one(a[1].y, a[3].y, a[5].y, a[7].y, a[9].y, a[11].y);
+}
+
+// ---------------------------------------------------------------- quantised wide nodes (GQ)
+// DESIGN.md §5.2 "Quantised nodes": 4 float4 per node instead of 10 (InwScene::qnodes; built by
+// rt_build.hip: k_quantize_wnodes), so a node step is 4 loads (64 B, half a cache line) instead of 7
+// (112 B), and 1,168 nodes fit the LDS the global FStack frees.  k_inw_pm's GQ instance stages the
+// first n_lnodes of them (the top levels, breadth first) in g_inw_qlds.
+__shared__ float4 g_inw_qlds[kQLdsNodes * kQNodeF4];
+template <bool LN>
+__device__ __forceinline__ void inw_qnode(const InwScene &S, int cur, float4 &a, float4 &b, float4 &c, float4 &lk) {
+    if (LN && (uint32_t)(cur - 1) < S.n_lnodes) {  // ds_read_b128
+        const float4 *nd = g_inw_qlds + kQNodeF4 * (cur - 1);
+        a = nd[0]; b = nd[1]; c = nd[2]; lk = nd[3];
+        return;
+    }
+    const float4 *nd = S.qnodes + kQNodeF4 * (cur - 1);
+    a = nd[0]; b = nd[1]; c = nd[2]; lk = nd[3];
+}
+// The fused cull of a quantised node: per axis sf = s * (1/d), of = fma(o, 1/d, -ray.o * (1/d)),
+// and each plane's t = fma(byte, sf, of) (one v_cvt_f32_ubyte per plane, pairs of fma packed).
+// hx/hy/hz: the ray's direction is negative on that axis, so its near planes are the high ones.
+__device__ __forceinline__ float ub(uint32_t v, int k) { return (float)((v >> (8 * k)) & 0xffu); }
+__device__ __forceinline__ void cull4q(const float4 a, const float4 b, const float4 c, bool hx, bool hy, bool hz, f3 fid,
+                                      f3 noid, float lim, float &t0, float &t1, float &t2, float &t3) {
+    const float sf[3] = {a.w * fid.x, b.x * fid.y, b.y * fid.z};
+    const float of[3] = {__builtin_fmaf(a.x, fid.x, noid.x), __builtin_fmaf(a.y, fid.y, noid.y),
+                         __builtin_fmaf(a.z, fid.z, noid.z)};
+    const uint32_t lx = __float_as_uint(b.z), ly = __float_as_uint(b.w), lz = __float_as_uint(c.x);
+    const uint32_t ux = __float_as_uint(c.y), uy = __float_as_uint(c.z), uz = __float_as_uint(c.w);
+    const uint32_t q[6] = {hx ? ux : lx, hy ? uy : ly, hz ? uz : lz, hx ? lx : ux, hy ? ly : uy, hz ? lz : uz};
+    pf2 t[12];  // t[2p + h]: plane p (near x, y, z, far x, y, z) of children 2h, 2h + 1
+#pragma unroll
+    for (int p = 0; p < 6; p++) {
+        const pf2 s2 = pk(sf[p % 3], sf[p % 3]), o2 = pk(of[p % 3], of[p % 3]);
+        t[2 * p] = __builtin_elementwise_fma(pk(ub(q[p], 0), ub(q[p], 1)), s2, o2);
+        t[2 * p + 1] = __builtin_elementwise_fma(pk(ub(q[p], 2), ub(q[p], 3)), s2, o2);
+    }
+    auto one = [&](float n0, float n1, float n2, float f0, float f1, float f2) {
+        const float te = fmaxf(fmaxf(n0, n1), n2), tx = fminf(fminf(f0, f1), f2);
+        return fmaxf(te, -1e-3f) <= fminf(tx, lim) ? te : kMiss;
+    };
+    t0 = one(t[0].x, t[2].x, t[4].x, t[6].x, t[8].x, t[10].x);
+    t1 = one(t[0].y, t[2].y, t[4].y, t[6].y, t[8].y, t[10].y);
+    t2 = one(t[1].x, t[3].x, t[5].x, t[7].x, t[9].x, t[11].x);
+    t3 = one(t[1].y, t[3].y, t[5].y, t[7].y, t[9].y, t[11].y);
 }
 
 // An empty asm that reads the object-space ray: the compiler must have it (so the object record's
@@ -1962,10 +2127,12 @@ struct WalkPark {
     bool resume;    // the walk was parked in an earlier iteration: restore it
     bool parked;    // out: parked again
 };
-template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false>
-__device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
+// QN: the quantised nodes (S.qnodes, cull4q; requires FU), LN then meaning the staged ones in g_inw_qlds.
+template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false, bool QN = false, class KS = FStack>
+__device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
                                    f3 &normal, float &extra, float init_geom, Ctr &c, bool &ok,
                                    WalkPark *wp = nullptr) {
+    static_assert(!QN || FU, "quantised nodes are culled with the fused planes");
     const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};  // the reference's reciprocals (test_aabb)
     ok = S.wnodes != nullptr && K.size + S.dfs_high <= (uint32_t)kFStack && __builtin_isfinite(id.x) &&
          __builtin_isfinite(id.y) && __builtin_isfinite(id.z) && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
@@ -1982,8 +2149,12 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
     // such a ray takes the reference walk
     if (FU) ok = ok && __builtin_isfinite(noid.x) && __builtin_isfinite(noid.y) && __builtin_isfinite(noid.z);
     // 3 spare slots for branch-free pushes; PK: the segment's ray (8 floats) stays below the walk
-    const int base = (int)K.size + (PK ? 8 : 0), cap = kFStack - 3 - base;
+    int cap;
+    float *const wsb = K.walk_stack(PK ? 8u : 0u, 3, cap);  // entry p at wsb[p * kBlock]
     const uint32_t ox = d.x < 0.0f ? 3u : 0u, oy = d.y < 0.0f ? 4u : 1u, oz = d.z < 0.0f ? 5u : 2u;
+#ifdef RT_INW_BUFLOAD
+    const __amdgpu_buffer_rsrc_t wrs = wnode_rsrc(S);
+#endif
     int sp = 0, pend = -1, cur = S.wroot;
     bool walking = ok, ovf = false;
     float lim = bt * 1.0001f + 1e-3f;
@@ -2032,20 +2203,31 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
         if (walking) {
             bool pop;
             if (cur > 0) {
-                float4 nx, ny, nz, fx, fy, fz, lk;
-                inw_wnode_nf<LN>(S, cur, ox, oy, oz, nx, ny, nz, fx, fy, fz, lk);
-                c.nodes += 4;
+                float4 lk;
                 float t0, t1, t2, t3;
-                cull4nf<FU>(nx, ny, nz, fx, fy, fz, o, fid, noid, lim, t0, t1, t2, t3);
+                if constexpr (QN) {
+                    float4 qa, qb, qc;
+                    inw_qnode<LN>(S, cur, qa, qb, qc, lk);
+                    cull4q(qa, qb, qc, ox != 0u, oy != 1u, oz != 2u, fid, noid, lim, t0, t1, t2, t3);
+                } else {
+                    float4 nx, ny, nz, fx, fy, fz;
+#ifdef RT_INW_BUFLOAD
+                    inw_wnode_nf_buf<LN>(S, wrs, cur, ox * 16u, oy * 16u, oz * 16u, nx, ny, nz, fx, fy, fz, lk);
+#else
+                    inw_wnode_nf<LN>(S, cur, ox, oy, oz, nx, ny, nz, fx, fy, fz, lk);
+#endif
+                    cull4nf<FU>(nx, ny, nz, fx, fy, fz, o, fid, noid, lim, t0, t1, t2, t3);
+                }
+                c.nodes += 4;
                 int k0 = __float_as_int(lk.x), k1 = __float_as_int(lk.y), k2 = __float_as_int(lk.z),
                     k3 = __float_as_int(lk.w);
                 cswap(t0, k0, t1, k1); cswap(t2, k2, t3, k3);
                 cswap(t0, k0, t2, k2); cswap(t1, k1, t3, k3);
                 cswap(t1, k1, t2, k2);
                 int p = sp;  // branch-free pushes, farthest first (a miss is overwritten before a pop)
-                K.at((uint32_t)(base + p)) = __int_as_float(k3); p += t3 != kMiss;
-                K.at((uint32_t)(base + p)) = __int_as_float(k2); p += t2 != kMiss;
-                K.at((uint32_t)(base + p)) = __int_as_float(k1); p += t1 != kMiss;
+                wsb[p * kBlock] = __int_as_float(k3); p += t3 != kMiss;
+                wsb[p * kBlock] = __int_as_float(k2); p += t2 != kMiss;
+                wsb[p * kBlock] = __int_as_float(k1); p += t1 != kMiss;
                 if (p > cap) { ovf = true; p = cap; }
                 sp = p;
                 cur = k0;
@@ -2056,7 +2238,7 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
             }
             if (pop) {
                 if (sp == 0) walking = false;
-                else cur = __float_as_int(K.at((uint32_t)(base + (--sp))));
+                else cur = __float_as_int(wsb[(--sp) * kBlock]);
             }
             if (ovf) walking = false;
         }
@@ -2108,8 +2290,8 @@ __device__ float inw_traverse_wide(const InwScene &S, FStack &K, f3 o, f3 d, flo
 // the exact test, the leaf-entry guard, the (t, depth-first rank) rule), so the winner is the
 // wide walk's and the reference walk's.  ok = false: the list does not decide this ray (no list,
 // the wide walk's conditions fail, or candidates beyond the stored ones could still win).
-template <bool WANT_NORMAL>
-__device__ float inw_closest_beam(const InwScene &S, const FStack &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
+template <bool WANT_NORMAL, class KS = FStack>
+__device__ float inw_closest_beam(const InwScene &S, const KS &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
                                   f3 &normal, float &extra, float init_geom, Ctr &c, uint32_t unit, bool &ok) {
     const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};  // the reference's reciprocals (test_aabb)
     const uint32_t nw = S.beam_n[unit], n = nw & 0xffu;  // k_inw_beam: offset in the block's region << 8 | count
@@ -2194,11 +2376,12 @@ __device__ float inw_closest_beam(const InwScene &S, const FStack &K, f3 o, f3 d
 // whose leaf box holds the point (inclusive, as the reference compares) and whose inside test
 // passes, found by a walk of the culling BVH and summed in rank order.  ok = false: fall back.
 constexpr int kRiMax = 8;
-template <bool LN = false>
-__device__ float inw_surrounding_ri_wide(const InwScene &S, FStack &K, f3 hp, float ratio, Ctr &c, bool &ok) {
+template <bool LN = false, class KS = FStack>
+__device__ float inw_surrounding_ri_wide(const InwScene &S, KS &K, f3 hp, float ratio, Ctr &c, bool &ok) {
     ok = S.wnodes != nullptr && K.size + S.dfs_high <= (uint32_t)kFStack;
     if (!__any(ok)) return 1.0f;
-    const int base = (int)K.size, cap = kFStack - 4 - base;
+    int cap;
+    float *const wsb = K.walk_stack(0u, 4, cap);  // entry p at wsb[p * kBlock]
     uint32_t rk[kRiMax];
     float rv[kRiMax];
     int nin = 0;
@@ -2214,10 +2397,10 @@ __device__ float inw_surrounding_ri_wide(const InwScene &S, FStack &K, f3 hp, fl
             const bool i2 = hp.x >= lx.z && hp.x <= hx.z && hp.y >= ly.z && hp.y <= hy.z && hp.z >= lz.z && hp.z <= hz.z;
             const bool i3 = hp.x >= lx.w && hp.x <= hx.w && hp.y >= ly.w && hp.y <= hy.w && hp.z >= lz.w && hp.z <= hz.w;
             int p = sp;
-            K.at((uint32_t)(base + p)) = lk.x; p += i0;
-            K.at((uint32_t)(base + p)) = lk.y; p += i1;
-            K.at((uint32_t)(base + p)) = lk.z; p += i2;
-            K.at((uint32_t)(base + p)) = lk.w; p += i3;
+            wsb[p * kBlock] = lk.x; p += i0;
+            wsb[p * kBlock] = lk.y; p += i1;
+            wsb[p * kBlock] = lk.z; p += i2;
+            wsb[p * kBlock] = lk.w; p += i3;
             if (p > cap) { ok = false; break; }
             sp = p;
         } else {
@@ -2242,7 +2425,7 @@ __device__ float inw_surrounding_ri_wide(const InwScene &S, FStack &K, f3 hp, fl
             }
         }
         if (sp == 0) walking = false;
-        else cur = __float_as_int(K.at((uint32_t)(base + (--sp))));
+        else cur = __float_as_int(wsb[(--sp) * kBlock]);
     }
     if (!ok) return 1.0f;
     // sum in the reference's order (insertion sort by rank; a handful of objects at most)
@@ -2433,22 +2616,26 @@ __device__ float inw_surrounding_ri_sl(const InwScene &S, f3 hp, float ratio, Ct
 }
 
 // EO: the reference walks' box test with the shader's early outs (INW-01) or all axes (INW-04)
-template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false, bool EO = true>
-__device__ __forceinline__ float inw_closest(const InwScene &S, FStack &K, f3 o, f3 d, float ratio, bool invert,
+// QN: the wide walk reads the quantised nodes (LN: the staged ones); the LBVH walks then read no
+// staged node (their LDS is not filled in the GQ instance)
+template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false, bool EO = true, bool QN = false,
+          class KS = FStack>
+__device__ __forceinline__ float inw_closest(const InwScene &S, KS &K, f3 o, f3 d, float ratio, bool invert,
                                              float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c,
                                              WalkPark *wp = nullptr) {
     bool ok = false;
-    const float g = inw_traverse_wide<WANT_NORMAL, LN, FU, PK>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom,
-                                                               c, ok, wp);
+    const float g = inw_traverse_wide<WANT_NORMAL, LN, FU, PK, QN>(S, K, o, d, ratio, invert, tlim, normal, extra,
+                                                                   init_geom, c, ok, wp);
     if (PK && wp->parked) return g;
     OCC_TALLY(c, kOccRef, !ok);
     if (ok) return g;
+    c.refw++;
     if (S.sl && K.size + S.dfs_high <= (uint32_t)kFStack)  // no push of the reference walk could drop
-        return inw_traverse_sl<WANT_NORMAL, LN, EO>(S, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
+        return inw_traverse_sl<WANT_NORMAL, LN && !QN, EO>(S, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
     return inw_traverse<WANT_NORMAL, EO>(S, K, o, d, ratio, invert, tlim, normal, extra, init_geom, c);
 }
-template <bool LN = false>
-__device__ __forceinline__ float inw_ri(const InwScene &S, FStack &K, f3 hp, float ratio, Ctr &c) {
+template <bool LN = false, class KS = FStack>
+__device__ __forceinline__ float inw_ri(const InwScene &S, KS &K, f3 hp, float ratio, Ctr &c) {
     bool ok = false;
     if (S.ri_cells && K.size + S.dfs_high <= (uint32_t)kFStack) {  // no push of the walk could drop
         const float g = inw_ri_grid(S, hp, ratio, c, ok);
@@ -2489,8 +2676,9 @@ __device__ __forceinline__ f3 inw_pixel_dir(const Frame &F, int px, int py) {
     return normalize((D * F.screen_dist + cr * srx) + cu * sry);
 }
 // cd: the pixel's direction (inw_pixel_dir), which callers that keep it per pixel pass in
-__device__ __forceinline__ void inw_start_sample_cd(const InwScene &S, const Frame &F, FStack &K, f3 cd, int s, Ctr &c) {
-    K.size = 0;
+template <class KS>
+__device__ __forceinline__ void inw_start_sample_cd(const InwScene &S, const Frame &F, KS &K, f3 cd, int s, Ctr &c) {
+    K.reset(0);
     const f3 up = f3{0, 1, 0};
     f3 co = mk(F.pos[0], F.pos[1], F.pos[2]);
     float ox = S.sunflower[2 * s] * (F.aperture * 0.5f), oy = S.sunflower[2 * s + 1] * (F.aperture * 0.5f);
@@ -2509,7 +2697,8 @@ __device__ __forceinline__ void inw_start_sample_cd(const InwScene &S, const Fra
     f3 la = normalize((co + cd * F.focus) - tip);
     K.push_ray(tip - la, la, 1.0f, 0.0f, c);
 }
-__device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame &F, FStack &K, int px, int py, int s,
+template <class KS>
+__device__ __forceinline__ void inw_start_sample(const InwScene &S, const Frame &F, KS &K, int px, int py, int s,
                                                  Ctr &c) {
     inw_start_sample_cd(S, F, K, inw_pixel_dir(F, px, py), s, c);
 }
@@ -2563,9 +2752,12 @@ __device__ f3 inw_tex_color(const InwScene &S, uint32_t k, f3 lp) {
 // bunit: the lane's pixel unit when its primary ray may use the pixel's beam list (k_inw_pm), else kBeamOff
 // PK (walk parking, above): wp->resume continues a parked walk of this segment (its ray still
 // sits above K.size); wp->parked on return: the walk parked again and the segment is not done.
-template <bool LIGHTS, bool LN = false, bool FU = false, bool PK = false>
-__device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s, f3 &color, float &depth, Ctr &c,
+// QN (k_inw_pm's GQ instance): the wide closest-hit walks read the quantised nodes (inw_closest)
+template <bool LIGHTS, bool LN = false, bool FU = false, bool PK = false, bool QN = false, class KS = FStack>
+__device__ void inw_segment(const InwScene &S, const Frame &F, KS &K, int s, f3 &color, float &depth, Ctr &c,
                             uint32_t bunit = kBeamOff, WalkPark *wp = nullptr) {
+    static_assert(!PK || !QN, "walk parking keeps the segment's ray in the stack (FStack only)");
+    constexpr bool RLN = LN && !QN;  // the LBVH / RI walks' staged nodes (none in the GQ instance)
     const f3 D = mk(F.dir[0], F.dir[1], F.dir[2]);
     const float ratio = (float)s * F.inv_spp;
     const bool invert = dot(D, f3{1, 1, 1}) > 0.0f;
@@ -2575,10 +2767,17 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
 #endif
     do {
         const bool resumed = PK && wp->resume;
-        if (!resumed) K.size -= 8;
-        const uint32_t b = K.size;
-        f3 co = mk(K.at(b), K.at(b + 1), K.at(b + 2)), cd = mk(K.at(b + 3), K.at(b + 4), K.at(b + 5));
-        float contribution = K.at(b + 6), bounced = (float)(int)K.at(b + 7);
+        f3 co, cd;
+        float contribution, bounced;
+        if (!resumed) K.pop_ray(co, cd, contribution, bounced);
+        else {  // a parked walk: its ray still sits above K.size
+            const uint32_t b = K.size;
+            co = mk(K.at(b), K.at(b + 1), K.at(b + 2));
+            cd = mk(K.at(b + 3), K.at(b + 4), K.at(b + 5));
+            contribution = K.at(b + 6);
+            bounced = K.at(b + 7);
+        }
+        bounced = (float)(int)bounced;
         if (!resumed) c.seg++;
         // SET LIMIT (01_BVH...glsl:424-428): a MULTIFOCUS primary ray stops at the lens
         const bool mf0 = !LIGHTS && F.n_focus > 0 && (int)(bounced + 0.1f) == 0;
@@ -2593,8 +2792,8 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
             fg = inw_closest_beam<true>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c, bunit,
                                         beam_ok);
         if (!beam_ok) {
-            fg = inw_closest<true, LN, FU, PK, !LIGHTS>(S, K, co, cd, ratio, invert, tlim, normal, extra, LIGHTS ? -1.0f : 0.0f, c,
-                                               wp);
+            fg = inw_closest<true, LN, FU, PK, !LIGHTS, QN>(S, K, co, cd, ratio, invert, tlim, normal, extra,
+                                                            LIGHTS ? -1.0f : 0.0f, c, wp);
             if (PK && wp->parked) return;  // the walk goes on in the next iteration
         }
         INW_CYC(c, 0, t_ch);
@@ -2613,13 +2812,13 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
                                   0.5f;
                 else K.at(4) = kMaxT - mult * K.at(4);
                 K.at(5) = K.at(5) + 1.0f;
-                K.size = 6;
+                K.reset(6);
                 K.push_ray(no, nd, 1.0f, 0.0f, c);
                 break;
             }
             color = color + background(cd, LIGHTS && S.n_lights > 0) * contribution;
             depth = tlim;
-            if (mf0) K.size = 0;  // 01_BVH...glsl:531-535
+            if (mf0) K.reset(0);  // 01_BVH...glsl:531-535
             break;
         }
         const float4 m0 = S.cold[2 * (int)fg], m1 = S.cold[2 * (int)fg + 1];
@@ -2647,13 +2846,13 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
         {
             INW_T0(t_ri);
             OCC_TALLY(c, kOccRi, true);
-            surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
+            surr = inw_ri<RLN>(S, K, hitpoint + normal * 0.001f, ratio, c);
             INW_CYC(c, 1, t_ri);
         }
 #ifdef RT_DIAG_SPLIT
         t_tail = clock64();
 #endif
-        if (mf0) K.size = 0;  // 01_BVH...glsl:544-549: the lens record goes after a primary hit
+        if (mf0) K.reset(0);  // 01_BVH...glsl:544-549: the lens record goes after a primary hit
         if (LIGHTS) {  // 04...glsl:604-665
             uint32_t is_lit = S.n_lights > 0 ? 0u : (uint32_t)is_lit_geom(S, f2u(fg + 0.1f));
             if (is_lit == 0) {
@@ -2665,17 +2864,18 @@ __device__ void inw_segment(const InwScene &S, const Frame &F, FStack &K, int s,
                     f3 sd = normalize((bmin + (bmax - bmin) * ratio) - so);
                     c.shadow++;
                     f3 dummy_n; float dummy_e;
-                    float sg = inw_closest<false, LN, FU, false, !LIGHTS>(S, K, so, sd, ratio, invert, sl, dummy_n, dummy_e, -1.0f, c);
+                    float sg = inw_closest<false, LN, FU, false, !LIGHTS, QN>(S, K, so, sd, ratio, invert, sl, dummy_n,
+                                                                              dummy_e, -1.0f, c);
                     is_lit += (uint32_t)is_lit_geom(S, f2u(sg + 0.1f));
                 }
                 const uint32_t nl = S.n_lights > 1 ? S.n_lights : 1u;
                 contribution *= (float)is_lit * rcp((float)nl);
                 if (ri_forced || (ri_read && contribution > 0.01f && bounced < (float)F.max_bounces))
-                    surr = inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
+                    surr = inw_ri<RLN>(S, K, hitpoint + normal * 0.001f, ratio, c);
             } else {
-                if (ri_forced) (void)inw_ri<LN>(S, K, hitpoint + normal * 0.001f, ratio, c);
+                if (ri_forced) (void)inw_ri<RLN>(S, K, hitpoint + normal * 0.001f, ratio, c);
                 color = f3{1, 1, 1};
-                K.size = 0;
+                K.reset(0);
                 break;
             }
         }
@@ -3085,11 +3285,32 @@ __global__ __launch_bounds__(kBlock) void k_inw_order_scatter(const uint32_t *ke
 // pixel-major stream (see above): entry g = (claimed pixel ordinal j, sample s).  LN: 768-lane
 // blocks (3 waves per SIMD) that stage the top of the wide BVH in the LDS their three 256-lane
 // stacks leave free (kInwLdsNodes nodes)
-template <bool LIGHTS, bool LN = false, bool FU = false, bool LRING = false>
-__global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_waves_per_eu(LN ? 3 : (LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES)))) void k_inw_pm(Frame f, InwScene S0, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force, const uint32_t *border) {
+// GQ (DESIGN.md §5.1 "GQ"; LN, FU, LRING and INW-01 only): the reference's 40-float stacks in
+// global memory (GStack, S.gstk), the wide walks' node stacks in LDS (kWStack entries per lane), the
+// closest-hit walks over the quantised nodes, the top kQLdsNodes of them staged in LDS
+#ifndef RT_GQ_STAGE
+#define RT_GQ_STAGE 1
+#endif
+#ifdef RT_GQ_FSTACK
+constexpr bool kGqGlobalStack = false;
+#else
+constexpr bool kGqGlobalStack = true;
+#endif
+constexpr bool kGqStage = RT_GQ_STAGE != 0;
+static_assert(kGqLdsFree >= kInwLdsNodes * kInwNodeF4 * 16, "GQ: room for the 236 full nodes");
+template <bool LN, bool GQ>
+constexpr int pm_sub() { return GQ && kGqGlobalStack ? kGqSub : (LN ? 3 : 1); }
+template <bool LIGHTS, bool LN = false, bool FU = false, bool LRING = false, bool GQ = false>
+__global__ __launch_bounds__((pm_sub<LN, GQ>() * kBlock)) __attribute__((amdgpu_waves_per_eu((LN ? pm_sub<LN, GQ>() : (LIGHTS ? RT_INW_WAVES : RT_INW01_WAVES))))) void k_inw_pm(Frame f, InwScene S0, float4 *ring, uint32_t rmask, unsigned *counter, const uint32_t *mode, uint32_t force, const uint32_t *border) {
+    static_assert(!GQ || (LN && FU && LRING && !LIGHTS), "GQ: the C3 instance only");
     if (inw_sample_major(mode, force)) return;  // the probe picked k_inw_sm for this frame
-    constexpr int SUB = LN ? 3 : 1;
-    __shared__ float lds[SUB * kFStack * kBlock];
+    constexpr int SUB = pm_sub<LN, GQ>();
+    // GS: the global 40-float stacks (GQ; the RT_GQ_FSTACK experiment keeps FStack), GST: the top
+    // of the culling BVH staged in the LDS that frees (RT_GQ_STAGE=0: none, an experiment), QN:
+    // quantised nodes (else the full ones, 236 in g_inw_lnodes)
+    constexpr bool GS = GQ && kGqGlobalStack, GST = GS && kGqStage, QN = GQ && kGqQn;
+    // FStack instances: the three 256-lane 40-float stacks; GS: the wide walks' node stacks
+    __shared__ float lds[SUB * (GS ? kWStack : kFStack) * kBlock];
     // per wave: the middle sample's depth of claimed ordinal j (slot j % 64; at most 64 ordinals lie
     // between the fold and the issue), written out with the pixel's colour
     __shared__ float s_pdep[SUB * kBlock];
@@ -3099,31 +3320,58 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
     constexpr bool LR = LN && LRING;
     // WLN: the walks read staged nodes.  The LDS-ring instances stage none: the top 5 nodes the
     // ring leaves room for sit in L1 anyway, and the walk loop without the LDS branch (its exec
-    // masking and the base pointer kept in a VGPR lane) ran C3 2% faster
-    constexpr bool WLN = LN && !LR;
-    if constexpr (WLN) {
-        const uint32_t cap = (uint32_t)kInwLdsNodes;
-        const uint32_t n = S.wnodes ? (S.n_wnodes < cap ? S.n_wnodes : cap) : 0u;
-        for (uint32_t i = threadIdx.x; i < n * (uint32_t)kInwNodeF4; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
-        // no wide walk: the stackless LBVH walks read the top of the LBVH (2 float4 per node) there
-        const uint32_t nb = (!S.wnodes && S.sl) ? min(2u * S.n - 1u, cap * (uint32_t)kInwNodeF4 / 2u) : 0u;
-        for (uint32_t i = threadIdx.x; i < 2u * nb; i += SUB * kBlock) g_inw_lnodes[i] = S.nodes[i];
-        __syncthreads();
-        S.n_lnodes = n;
-        S.n_blds = nb;
+    // masking and the base pointer kept in a VGPR lane) ran C3 2% faster.  GQ
+    // stages kQLdsNodes quantised nodes beside its ring
+    constexpr bool WLN = LN && (!LR || GST);
+    float *lr;  // LR: this wave's ring, three planes (r, g, b) of kPmLdsRing floats
+    if constexpr (GS) {
+        __shared__ float s_ring[SUB * kBlock / 64 * 3 * kPmLdsRing];
+        lr = s_ring + uni((threadIdx.x >> 6) * (3u * kPmLdsRing));
+        if constexpr (GST && QN) {
+            const uint32_t n = S.qnodes ? (S.n_wnodes < (uint32_t)kQLdsNodes ? S.n_wnodes : (uint32_t)kQLdsNodes) : 0u;
+            for (uint32_t i = threadIdx.x; i < n * (uint32_t)kQNodeF4; i += SUB * kBlock) g_inw_qlds[i] = S.qnodes[i];
+            __syncthreads();
+            S.n_lnodes = n;
+        } else if constexpr (GST) {
+            const uint32_t n = S.wnodes ? (S.n_wnodes < (uint32_t)kInwLdsNodes ? S.n_wnodes : (uint32_t)kInwLdsNodes) : 0u;
+            for (uint32_t i = threadIdx.x; i < n * (uint32_t)kInwNodeF4; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
+            __syncthreads();
+            S.n_lnodes = n;
+        }
+    } else {
+        lr = reinterpret_cast<float *>(g_inw_lnodes + kPmLdsNodes * kInwNodeF4) + uni((threadIdx.x >> 6) * (3u * kPmLdsRing));
+        if constexpr (WLN) {
+            const uint32_t cap = (uint32_t)kInwLdsNodes;
+            const uint32_t n = S.wnodes ? (S.n_wnodes < cap ? S.n_wnodes : cap) : 0u;
+            for (uint32_t i = threadIdx.x; i < n * (uint32_t)kInwNodeF4; i += SUB * kBlock) g_inw_lnodes[i] = S.wnodes[i];
+            // no wide walk: the stackless LBVH walks read the top of the LBVH (2 float4 per node) there
+            const uint32_t nb = (!S.wnodes && S.sl) ? min(2u * S.n - 1u, cap * (uint32_t)kInwNodeF4 / 2u) : 0u;
+            for (uint32_t i = threadIdx.x; i < 2u * nb; i += SUB * kBlock) g_inw_lnodes[i] = S.nodes[i];
+            __syncthreads();
+            S.n_lnodes = n;
+            S.n_blds = nb;
+        }
     }
     Ctr c;
 #ifdef RT_DIAG_SPLIT
     const unsigned long long t_start = wall_clock64();  // the tail split (tools/inw_split.py)
     unsigned long long t_qd = 0;
 #endif
-    FStack K{lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock), 0};
+    using KS = std::conditional_t<GS, GStack, FStack>;
+    KS K;
+    if constexpr (GS) {
+        K.col = S.gstk + ((size_t)blockIdx.x * (SUB * kBlock) + threadIdx.x);
+        K.stride = gridDim.x * (SUB * kBlock);
+        K.ws = lds + (threadIdx.x / kBlock) * (kWStack * kBlock) + (threadIdx.x % kBlock);
+        K.rc = false;
+    } else {
+        K.base = lds + (threadIdx.x / kBlock) * (kFStack * kBlock) + (threadIdx.x % kBlock);
+    }
+    K.size = 0;
     const uint32_t lane = threadIdx.x & 63u;
     if constexpr (LR) rmask = kPmLdsRing - 1u;
     const uint32_t rsize = rmask + 1u;
     float4 *wr = ring + (size_t)uni((blockIdx.x * (SUB * kBlock) + threadIdx.x) >> 6) * rsize;
-    // LR: this wave's ring, three planes (r, g, b) of kPmLdsRing floats
-    float *lr = reinterpret_cast<float *>(g_inw_lnodes + kPmLdsNodes * kInwNodeF4) + uni((threadIdx.x >> 6) * (3u * kPmLdsRing));
     float *pdep = s_pdep + (threadIdx.x & ~63u);
     const uint32_t spp = (uint32_t)f.spp, mid = spp / 2u, total = units_total(f);
     const float inv = rcp((float)f.spp);
@@ -3366,12 +3614,12 @@ __global__ __launch_bounds__(LN ? 3 * kBlock : kBlock) __attribute__((amdgpu_wav
         constexpr int kRounds = LIGHTS ? 1 : 2;
 #pragma unroll 1
         for (int round = 2 - kRounds; round < 2; round++) {
-            const bool prim = bu != kBeamOff && !parked && K.size >= 8u && K.at(K.size - 1u) == 0.0f;
+            const bool prim = bu != kBeamOff && !parked && K.top_primary();
             const bool go = busy && (round == 0 ? prim : (parked || K.size > 0u));
             if (go) {
                 WalkPark wp{pslot, parked, false};
                 if (f.px_rays && !parked) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
-                inw_segment<LIGHTS, WLN, FU, PK>(S, f, K, s, col, dep, c, bu, &wp);
+                inw_segment<LIGHTS, WLN, FU, PK, QN>(S, f, K, s, col, dep, c, bu, &wp);
                 parked = PK && wp.parked;
             }
             if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
@@ -3636,6 +3884,8 @@ int resident_blocks_per_cu(int kind) {
     else if (kind == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<true>, kBlock, 0);
     else if (kind == 17) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<false, true>, 3 * kBlock, 0);
     else if (kind == 18) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<true, true>, 3 * kBlock, 0);
+    else if (kind == 19)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw_pm<false, true, true, true, true>, pm_sub<true, true>() * kBlock, 0);
     else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_inw<false>, kBlock, 0);
     return (e == hipSuccess && nb > 0) ? nb : 2;
 }
@@ -3918,7 +4168,10 @@ hipError_t launch_inw_fold(const Frame &f, const InwScene &sc, float4 *ring, uin
         else if (sc.lring_sm) hipLaunchKernelGGL((k_inw_sm<L, true, F, true>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border); \
         else hipLaunchKernelGGL((k_inw_sm<L, true, F>), g, b, 0, s, f, sc, ring, rm, ctr, mode, force, border);        \
     } while (0)
-            if (sc.layout == 4) {
+            if (k == 0 && sc.layout != 4 && sc.fused && sc.lring && sc.gstk && sc.gq_blocks)  // GQ
+                hipLaunchKernelGGL((k_inw_pm<false, true, true, true, true>), dim3(sc.gq_blocks),
+                                   dim3(pm_sub<true, true>() * kBlock), 0, s, f, sc, ring, rm, ctr, mode, force, border);
+            else if (sc.layout == 4) {
                 if (sc.fused) RT_INW_LN_LAUNCH(true, true);
                 else RT_INW_LN_LAUNCH(true, false);
             } else {

@@ -30,6 +30,7 @@ struct Frame {
     int n_focus;
     float focus_list[9];
     int narrow;               // rt_options.iow_narrow (host side: iow_narrow)
+    unsigned long long *walk_ctr;  // INW: closest-hit queries that fell back to the LBVH walks (added to; may be null)
 };
 // lane-occupancy counters (per wave-iteration: 1 and popcount of the participating lanes)
 enum { kDbgOuter = 0, kDbgOuterLanes, kDbgTrav, kDbgTravLanes, kDbgLeaf, kDbgLeafLanes, kDbgSeg, kDbgSegLanes,
@@ -94,6 +95,15 @@ struct InwScene {
     uint32_t xcdq = 0;        // k_inw_pm claims from per-XCD queues (rt_options.inw_claim_xcd)
     uint32_t ring_epoch = 0;  // fold-ring tags: the frame's epoch (0..62) << 26 (ring_tag, rt_kernels.hip)
     float4 *park = nullptr;   // RT_INW_PARK builds: 2 float4 of parked walk state per lane of the fold grid
+    // Quantised wide nodes (DESIGN.md §5.2 "Quantised nodes"; null = off): the culling BVH of
+    // wnodes as 4 float4 per node -- origin.xyz, scale.x | scale.yz, low-plane bytes x, y | low z,
+    // high x, y, z (byte k = child k) | links -- each plane rounded outward (rt_build.hip:
+    // k_quantize_wnodes).  Read by the wide closest-hit walk of the k_inw_pm<..., GQ> instance, which
+    // also stages the first n_lnodes of them in LDS and keeps the reference's 40-float stack in
+    // global memory (gstk: kFStack / 4 float4 per lane of the grid, [slot4][lane]).
+    const float4 *qnodes = nullptr;
+    float4 *gstk = nullptr;
+    uint32_t gq_blocks = 0;  // the GQ instance's grid (kGqSub * kBlock lanes per block, resident blocks)
     // Pixel beams (DESIGN.md §5 "Pixel beams"; null beam = off): for each pixel unit, the objects
     // whose culling box the beam of its primary rays can cross, sorted by the entry t of the
     // central ray into the box inflated by beam_R (k_inw_beam).  The 64 lists of an 8x8 block are
@@ -201,6 +211,25 @@ constexpr int kBlock = 256;      // threads per block of every render kernel
 constexpr int kInwLdsNodes = 236;        // wide BVH nodes the INW fold kernels stage in LDS (rt_kernels.hip)
 constexpr uint32_t kPmLdsRing = 256;     // k_inw_pm's LDS fold ring: entries per wave (InwScene::lring) ...
 constexpr uint32_t kPmLdsNodes = 5;      // ... and the nodes it leaves staged
+// k_inw_pm's GQ instance (DESIGN.md §5.1 "GQ": the reference's 40-float stacks in global memory):
+// kGqSub 256-lane sub-blocks per block (= waves per SIMD; 1 block per CU), per block the wide walks'
+// node stacks in LDS (kWStack entries per lane), the fold rings (3 KB per wave), the depth slots,
+// and in the rest of the CU's 160 KB the top of the culling BVH: kQLdsNodes quantised nodes
+// (kGqQn; 64 B each) or the 236 full ones of g_inw_lnodes
+constexpr int kFStack = 40;  // stack_capacity (FLT_STACK, 01_BVH...glsl:80)
+constexpr int kWStack = 16;
+constexpr int kQNodeF4 = 4;
+#ifndef RT_GQ_SUB
+#define RT_GQ_SUB 3
+#endif
+#ifndef RT_GQ_QN
+#define RT_GQ_QN 1
+#endif
+constexpr int kGqSub = RT_GQ_SUB;
+constexpr bool kGqQn = RT_GQ_QN != 0;
+constexpr int kGqLdsFree = 163840 - kGqSub * kWStack * kBlock * 4 - kGqSub * 4 * 3 * (int)kPmLdsRing * 4 -
+                           kGqSub * kBlock * 4;
+constexpr int kQLdsNodes = kGqLdsFree / 64;
 constexpr int kParkBelow = 32;    // park when fewer than half the wave's lanes are busy
 constexpr int kContSlots = 13;    // float4 per parked lane
 struct Cont {
@@ -265,8 +294,13 @@ struct InwWideDev {
 };
 size_t inw_build_workspace_bytes(uint32_t n);
 // nodes: the device LBVH (lbvh_build_device), lcnt: its leaf counts (lbvh_build_device's lcnt)
+// max_levels (0 = 256): the binary SAH and collapse levels launched at most; a deeper tree returns
+// hipErrorNotSupported (the caller then builds on the host)
 hipError_t inw_wide_build_device(const float4 *nodes, const uint32_t *lcnt, uint32_t n, void *ws, size_t ws_bytes,
-                                 InwWideDev &out, hipStream_t s);
+                                 InwWideDev &out, hipStream_t s, int max_levels = 0);
+// the quantised form of nw wide nodes (InwScene::qnodes): 4 float4 per node, planes rounded
+// outward by at least `margin` beyond the wide node's (rt_build.hip)
+hipError_t inw_quantize_wnodes(const float4 *wnodes, uint32_t nw, float4 *qnodes, float margin, hipStream_t s);
 // the surrounding-RI grid on the device (rtamd::ri_grid_build's cells and ids) over the extent
 // inw_wide_build_device returned: per-cell counts scanned into cells[0..nc] with the total and an
 // over-64 flag read back (synchronises), then the ids

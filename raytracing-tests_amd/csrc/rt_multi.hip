@@ -134,9 +134,15 @@ struct rt_group {
 namespace {
 
 // the deal of a W x H frame in T x T tiles over g's devices, uploaded to every device's tile list
-// and to device 0's gathered order
-int set_deal(rt_group *g, int W, int H, int T) {
+// and to device 0's gathered order.  The buffers are reused when large enough, so an earlier frame
+// still running on the group's streams (device 0: the caller's stream s0) is waited for first: the
+// API is asynchronous, and a null-stream copy does not wait for non-blocking streams
+int set_deal(rt_group *g, int W, int H, int T, hipStream_t s0) {
     if (g->W == W && g->H == H && g->T == T) return RT_OK;
+    for (int r = 0; r < g->n; r++) {
+        MULTI_HIP(hipSetDevice(g->dev[size_t(r)]));
+        MULTI_HIP(hipStreamSynchronize(r == 0 ? s0 : g->st[size_t(r)]));
+    }
     const std::vector<std::pair<int, int>> order = rtamd::tile_deal(W, H, T, g->n);
     std::vector<std::vector<int>> lists(size_t(g->n));
     for (size_t k = 0; k < order.size(); k++) {
@@ -240,14 +246,16 @@ int rt_render_multi_async(rt_group *g, rt_dev_scene *const *scenes, const rt_cam
     if (!g || !scenes || !cam || !p || !d_rgba || p->width <= 0 || p->height <= 0 || tile_size <= 0 ||
         tile_size % 16 != 0)
         return RT_E_ARG;
+    // every scene must live on its group device (its buffers are that device's; a scene of another
+    // device would launch there with this device's stream)
     for (int r = 0; r < g->n; r++)
-        if (!scenes[r]) return RT_E_ARG;
+        if (!scenes[r] || rtamd::scene_device(scenes[r]) != g->dev[size_t(r)]) return RT_E_ARG;
     DeviceGuard guard;
-    if (int rc = set_deal(g, p->width, p->height, tile_size); rc != RT_OK) {
+    const hipStream_t s0 = static_cast<hipStream_t>(stream);
+    if (int rc = set_deal(g, p->width, p->height, tile_size, s0); rc != RT_OK) {
         g->W = 0;  // rebuild the deal next time
         return rc;
     }
-    const hipStream_t s0 = static_cast<hipStream_t>(stream);
     auto stream_of = [&](int r) { return r == 0 ? s0 : g->st[size_t(r)]; };
     const size_t area = size_t(tile_size) * size_t(tile_size);
     rt_params q = *p;
@@ -264,30 +272,35 @@ int rt_render_multi_async(rt_group *g, rt_dev_scene *const *scenes, const rt_cam
         if (rc != RT_OK) return rc;
     }
     // the one exchange step: every device's packed tiles, depth and counters to device 0
-    // (device 0 sends to itself too, so one code path serves every group size)
+    // (device 0 sends to itself too, so one code path serves every group size).  An error inside
+    // the group still ends it, so later RCCL calls of this thread are not left inside an open group
     MULTI_NCCL(ncclGroupStart());
-    for (int r = 0; r < g->n; r++) {
+    ncclResult_t nr = ncclSuccess;
+    auto call = [&](ncclResult_t r_) { if (nr == ncclSuccess) nr = r_; };
+    for (int r = 0; r < g->n && nr == ncclSuccess; r++) {
         auto &S = *g->share[size_t(r)];
         if (S.n_tiles) {
-            MULTI_NCCL(ncclSend(S.packed.p, size_t(S.n_tiles) * area * 4, ncclFloat32, 0, g->comm[size_t(r)], stream_of(r)));
+            call(ncclSend(S.packed.p, size_t(S.n_tiles) * area * 4, ncclFloat32, 0, g->comm[size_t(r)], stream_of(r)));
             if (d_depth)
-                MULTI_NCCL(ncclSend(S.depth.p, size_t(S.n_tiles) * area, ncclFloat32, 0, g->comm[size_t(r)], stream_of(r)));
+                call(ncclSend(S.depth.p, size_t(S.n_tiles) * area, ncclFloat32, 0, g->comm[size_t(r)], stream_of(r)));
         }
-        MULTI_NCCL(ncclSend(S.counters.p, 6, ncclUint64, 0, g->comm[size_t(r)], stream_of(r)));
+        call(ncclSend(S.counters.p, 6, ncclUint64, 0, g->comm[size_t(r)], stream_of(r)));
     }
-    for (int r = 0; r < g->n; r++) {
+    for (int r = 0; r < g->n && nr == ncclSuccess; r++) {
         auto &S = *g->share[size_t(r)];
         const size_t o = g->off[size_t(r)];
         if (S.n_tiles) {
-            MULTI_NCCL(ncclRecv(g->recv.as<float>() + o * area * 4, size_t(S.n_tiles) * area * 4, ncclFloat32, r,
-                                g->comm[0], s0));
+            call(ncclRecv(g->recv.as<float>() + o * area * 4, size_t(S.n_tiles) * area * 4, ncclFloat32, r, g->comm[0],
+                          s0));
             if (d_depth)
-                MULTI_NCCL(ncclRecv(g->recv_depth.as<float>() + o * area, size_t(S.n_tiles) * area, ncclFloat32, r,
-                                    g->comm[0], s0));
+                call(ncclRecv(g->recv_depth.as<float>() + o * area, size_t(S.n_tiles) * area, ncclFloat32, r,
+                              g->comm[0], s0));
         }
-        MULTI_NCCL(ncclRecv(g->recv_ctr.as<unsigned long long>() + size_t(r) * 6, 6, ncclUint64, r, g->comm[0], s0));
+        call(ncclRecv(g->recv_ctr.as<unsigned long long>() + size_t(r) * 6, 6, ncclUint64, r, g->comm[0], s0));
     }
-    MULTI_NCCL(ncclGroupEnd());
+    const ncclResult_t ne = ncclGroupEnd();
+    MULTI_NCCL(nr);
+    MULTI_NCCL(ne);
     // device 0 assembles the frame
     MULTI_HIP(hipSetDevice(g->dev[0]));
     const uint32_t n_px = uint32_t(size_t(g->off[size_t(g->n)]) * area);

@@ -165,6 +165,11 @@ def _same_frames(over, w, h, spp, scene):
     ({"inw_claim_order": 0}, INW1, 192, 108, 24),
     ({"inw_claim_xcd": 0}, INW1, 192, 108, 24),          # one claim queue (default: one per XCD)
     ({"inw_claim_xcd": 0, "inw_claim_order": 0}, INW1, 97, 43, 7),
+    # k_inw_pm's GQ instance (the 40-float stacks in global memory, the walk's node stack and the
+    # top of the culling BVH in LDS, quantised nodes) against the default FStack instance
+    ({"inw_qnodes": 1}, INW1, 192, 108, 24),
+    ({"inw_qnodes": 1, "inw_order": 1}, INW1, 97, 43, 7),
+    ({"inw_qnodes": 1, "inw_order": 1}, INW1, 160, 96, 300),
     ({"inw_beams": 0, "inw_order": 1}, INW4, 128, 128, 16),
     ({"inw_fused_cull": 0, "inw_order": 1}, INW4, 128, 128, 16),
     ({"inw_ri_grid": 0, "inw_order": 1}, INW4, 128, 128, 16),

@@ -175,6 +175,51 @@ def test_repeated_frames_on_one_device_scene(gpu):
         assert n == ost["segments"], i
 
 
+def test_scene_update_deep_tree_falls_back_to_host_build(gpu):
+    """the device build of the walk structures stops at its level cap (a chain-like
+    scene can split one object off per SAH level); the update then builds them on the host from
+    the device LBVH instead of failing and leaving the scene unrenderable.  The cap is lowered
+    (rt_debug_build_level_cap) so an ordinary scene is 'too deep': the update succeeds, reports the
+    host fallback (info[7] = 2), and its frame equals a fresh scene's and the oracle's."""
+    import ctypes as C
+
+    import torch
+
+    b = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 3000, width=64, height=36, spp=8)
+    lib = R.load()
+    dev = torch.device("cuda")
+
+    def frame(s):
+        img = torch.zeros((36, 64, 4), dtype=torch.float32, device=dev)
+        dep = torch.zeros((36, 64), dtype=torch.float32, device=dev)
+        ctr = torch.zeros(6, dtype=torch.int64, device=dev)
+        assert lib.rt_render_image_async(s, C.byref(b.camera), C.byref(b.params), img.data_ptr(), dep.data_ptr(),
+                                         ctr.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        return img.cpu().numpy(), dep.cpu().numpy(), int(ctr[0].item())
+
+    s = lib.rt_dev_scene_inw(R.fptr(b.geom), b.n, 1, R.fptr(b.nodes), None, 0, b.params.spp, -1)
+    f = lib.rt_dev_scene_inw(R.fptr(b.geom), b.n, 1, R.fptr(b.nodes), None, 0, b.params.spp, -1)
+    assert s and f
+    try:
+        for cap, site in ((4, 2), (0, 1)):  # a cap below the tree's depth, then the default
+            assert lib.rt_debug_build_level_cap(cap) == 0
+            tm = (C.c_double * 4)()
+            assert lib.rt_dev_scene_inw_update(s, R.fptr(b.geom), b.n, None, R.fptr(b.aabbs), None, 0, tm) == 0
+            info = (C.c_uint32 * 8)()
+            assert lib.rt_debug_wide_info(s, info, None) == 0
+            assert info[7] == site and info[0] > 0, list(info)
+            g, gd, gs = frame(s)
+            h, hd, hs = frame(f)
+            assert compare(g, h)["exact_frac"] == 1.0 and compare(gd, hd)["exact_frac"] == 1.0 and gs == hs
+    finally:
+        lib.rt_debug_build_level_cap(0)
+        lib.rt_dev_scene_free(s)
+        lib.rt_dev_scene_free(f)
+    o, od, ost = O.render(b)
+    assert compare(g, o)["exact_frac"] == 1.0 and gs == ost["segments"]
+
+
 @pytest.mark.parametrize("device_lbvh,n_new", [(False, 3000), (True, 3000), (True, 3600), (False, 2200)])
 def test_scene_update_matches_fresh_scene(gpu, device_lbvh, n_new):
     """rt_dev_scene_inw_update (the per-redraw work of RT_Base::OnUpdateBase, In-Next-Week/base.h:
@@ -252,8 +297,8 @@ def test_debug_path_reports_the_fold_ring(gpu):
     assert s
     paths = {}
     try:
-        for name, over in (("lds", {"inw_order": 1}), ("global", {"inw_order": 1, "inw_ring_pm": 1024}),
-                           ("sm", {"inw_order": 2})):
+        for name, over in (("lds", {"inw_order": 1, "inw_qnodes": 0}), ("gq", {"inw_order": 1, "inw_qnodes": 1}),
+                           ("global", {"inw_order": 1, "inw_ring_pm": 1024}), ("sm", {"inw_order": 2})):
             o = R.default_options()
             for k, v in over.items():
                 setattr(o, k, v)
@@ -270,7 +315,11 @@ def test_debug_path_reports_the_fold_ring(gpu):
     print(paths)
     p = paths["lds"]
     assert p["kernel"].startswith("k_inw_pm") and p["ring_lds"] == 1 and p["ring_entries"] == 256
-    assert p["lds_nodes"] == 0  # the LDS-ring instances read every node from L1 / L2
+    assert p["lds_nodes"] == 0  # the FStack LDS-ring instances read every node from L1 / L2
+    assert p["qnodes"] == 0 and p["global_stack"] == 0 and p["walk_stack"] == 37
+    p = paths["gq"]  # GQ: quantised nodes, the top ones staged in LDS, the 40-float stacks in global memory
+    assert p["kernel"].startswith("k_inw_pm") and p["ring_lds"] == 1 and p["ring_entries"] == 256
+    assert p["qnodes"] == 1 and p["global_stack"] == 1 and p["walk_stack"] == 16 and p["lds_nodes"] > 5
     p = paths["global"]
     assert p["kernel"].startswith("k_inw_pm") and p["ring_lds"] == 0 and p["ring_entries"] == 1024
     assert p["lds_nodes"] > 5

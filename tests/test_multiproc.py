@@ -54,6 +54,47 @@ def _worker(rank, world, port, W, H, T, q):
         dist.destroy_process_group()
 
 
+def _worker_msg(rank, world, port, W, H, T, q):
+    """bench.py's one gather message per rank: the colour tiles and their r32f depth tiles in one
+    flat buffer (bench.message_views), assembled on rank 0 by bench.assemble_message."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        allt, mine, per_rank = bench.tiles_for_rank(W, H, world, rank, T)
+        ref = _pattern(W, H)
+        dref = ref[..., 2] * 0.5 + 7.0  # a depth pattern distinct from every colour channel
+        msg = torch.zeros(per_rank * T * T * 5)
+        col, dep = bench.message_views(msg, per_rank, T, True)
+        for k, (tx, ty) in enumerate(mine):
+            y0, x0 = ty * T, tx * T
+            blk, dblk = ref[y0:y0 + T, x0:x0 + T], dref[y0:y0 + T, x0:x0 + T]
+            col[k, :blk.shape[0], :blk.shape[1]] = blk
+            dep[k, :dblk.shape[0], :dblk.shape[1]] = dblk
+        gathered = [torch.empty_like(msg) for _ in range(world)] if rank == 0 else None
+        dist.gather(msg, gathered, dst=0)
+        if rank == 0:
+            nx, ny = math.ceil(W / T), math.ceil(H / T)
+            lists = [allt[r::world] for r in range(world)]
+            img, dimg = bench.assemble_message(gathered, lists, nx, ny, per_rank, T, True)
+            q.put(bool(torch.equal(img[:H, :W], ref)) and bool(torch.equal(dimg[:H, :W], dref)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H,T", [(2, 200, 130, 16), (3, 200, 130, 16), (3, 97, 43, 64)])
+def test_gather_message_assembles_colour_and_depth(world, W, H, T):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_msg, args=(r, world, port, W, H, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True
+
+
 @pytest.mark.parametrize("world,W,H,T", [(2, 1200, 800, 16), (2, 1200, 800, 64), (3, 200, 130, 16),
                                          (3, 200, 130, 64), (2, 64, 64, 64)])
 def test_gather_assembles_frame(world, W, H, T):

@@ -15,8 +15,14 @@ done
 python -c "
 import numpy as np
 a = np.load('$O/f1.npy')
+import os
+da = np.load('$O/f1.depth.npy') if os.path.exists('$O/f1.depth.npy') else None
 for n in (2, 3):
     b = np.load('$O/f%d.npy' % n)
-    print('ranks', n, 'bit-identical to 1 rank:', np.array_equal(a.view(np.uint32), b.view(np.uint32)), a.shape)
+    line = 'ranks %d bit-identical to 1 rank: %s %s' % (n, np.array_equal(a.view(np.uint32), b.view(np.uint32)), a.shape)
+    if da is not None:
+        db = np.load('$O/f%d.depth.npy' % n)
+        line += ' depth: %s' % np.array_equal(da.view(np.uint32), db.view(np.uint32))
+    print(line)
 " | tee $O/check.txt
 rm -f $O/f*.npy  # frames are 33 MB each: keep gpurun_out under its copy-back limit
