@@ -1966,7 +1966,7 @@ __device__ __forceinline__ void inw_wnode_nf(const InwScene &S, int cur, uint32_
 // The same fetch from global memory as buffer loads: the node's byte offset is 32 bits (a node
 // index times 160), the octant offsets and the far planes' +48 / the links' +144 fold into the
 // instructions, so a node step spends 4 VALU on addresses instead of the 64-bit pointer sums (~10)
-// (RT_INW_BUFLOAD experiment)
+// (C3 185.9 -> 184.2 ms on one box, profiles/r06_ab2_gq.json; -DRT_INW_NO_BUFLOAD: the pointer form)
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
@@ -2122,6 +2122,10 @@ __device__ __forceinline__ void keep_before_branch(f3 to, f3 td) {
 #define RT_INW_PARK_MIN 4
 #endif
 constexpr int kParkLanes = RT_INW_PARK_LANES, kParkMinTrips = RT_INW_PARK_MIN;
+#ifndef RT_INW_LEAF_BATCH
+#define RT_INW_LEAF_BATCH 65
+#endif
+constexpr int kInwLeafBatch = RT_INW_LEAF_BATCH;
 struct WalkPark {
     float4 *slot;   // this lane's 2 float4
     bool resume;    // the walk was parked in an earlier iteration: restore it
@@ -2142,7 +2146,9 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
     int bg = -1;
     uint32_t br = 0xffffffffu;
     const uint32_t *rank = S.rank + (invert ? S.n : 0u);
-    const f3 fid = f3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
+    // the culling planes use the reference's (correctly rounded) reciprocals too: no second set of
+    // three (round 5 took v_rcp approximations), C3 184.6 -> 184.0 ms (profiles/r06_ab_walk_tweaks.json)
+    const f3 fid = id;
     const f3 noid = f3{-(o.x * fid.x), -(o.y * fid.y), -(o.z * fid.z)};  // the fused cull's per-ray term (FU)
     // the fused planes need a finite per-ray term: a direction component near the smallest normal
     // float with |o| ~ 10^3 overflows it, and every fma would be -inf or NaN (every child culled);
@@ -2152,7 +2158,7 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
     int cap;
     float *const wsb = K.walk_stack(PK ? 8u : 0u, 3, cap);  // entry p at wsb[p * kBlock]
     const uint32_t ox = d.x < 0.0f ? 3u : 0u, oy = d.y < 0.0f ? 4u : 1u, oz = d.z < 0.0f ? 5u : 2u;
-#ifdef RT_INW_BUFLOAD
+#ifndef RT_INW_NO_BUFLOAD
     const __amdgpu_buffer_rsrc_t wrs = wnode_rsrc(S);
 #endif
     int sp = 0, pend = -1, cur = S.wroot;
@@ -2211,7 +2217,7 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
                     cull4q(qa, qb, qc, ox != 0u, oy != 1u, oz != 2u, fid, noid, lim, t0, t1, t2, t3);
                 } else {
                     float4 nx, ny, nz, fx, fy, fz;
-#ifdef RT_INW_BUFLOAD
+#ifndef RT_INW_NO_BUFLOAD
                     inw_wnode_nf_buf<LN>(S, wrs, cur, ox * 16u, oy * 16u, oz * 16u, nx, ny, nz, fx, fy, fz, lk);
 #else
                     inw_wnode_nf<LN>(S, cur, ox, oy, oz, nx, ny, nz, fx, fy, fz, lk);
@@ -2242,7 +2248,10 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
             }
             if (ovf) walking = false;
         }
-        if (__all(!walking || pend >= 0)) {
+        // postponed leaves are tested once every walking lane holds one (RT_INW_LEAF_BATCH < 65: or
+        // once that many lanes hold one, an experiment)
+        if (__all(!walking || pend >= 0) ||
+            (kInwLeafBatch < 65 && __popcll(__ballot(pend >= 0)) >= (unsigned)kInwLeafBatch)) {
             OCC_TALLY(c, kOccLeaf, pend >= 0);
             if (pend >= 0) { leaf(pend); pend = -1; }
             if (__all(!walking)) break;
@@ -3291,6 +3300,10 @@ __global__ __launch_bounds__(kBlock) void k_inw_order_scatter(const uint32_t *ke
 #ifndef RT_GQ_STAGE
 #define RT_GQ_STAGE 1
 #endif
+#ifndef RT_INW_R1_MIN
+#define RT_INW_R1_MIN 0
+#endif
+constexpr int kR1Min = RT_INW_R1_MIN;  // k_inw_pm: round 1 waits for this many lanes with a ray (0 = off)
 #ifdef RT_GQ_FSTACK
 constexpr bool kGqGlobalStack = false;
 #else
@@ -3634,6 +3647,19 @@ __global__ __launch_bounds__((pm_sub<LN, GQ>() * kBlock)) __attribute__((amdgpu_
                 }
                 if ((uint32_t)s == mid) pdep[pj] = dep;  // 01_BVH...glsl:667-668, stored with the pixel's colour
                 busy = false;
+            }
+            // Bounce-walk fill: the wide walk of round 1 costs a wave the same
+            // trips however few of its lanes hold a bounce ray, and primary rays (beam lists) are
+            // cheap.  While fewer than kR1Min lanes hold a ray for round 1 and free lanes could take
+            // more samples, skip round 1: the next iteration issues samples to the free lanes and
+            // runs their primaries, and the bounce rays pile up for one fuller walk.  Every
+            // iteration issues at least one entry while that holds, so the loop always advances.
+            if (kR1Min > 0 && round == 0) {
+                const uint32_t nb = (uint32_t)__popcll(__ballot(busy && K.size > 0u));
+                const bool nfree = __ballot(!busy) != 0ull;
+                const bool more = nfree && (uint64_t)(nclaimed - ji) * spp - si + (qdone ? 0u : 1u) > 0u &&
+                                  gi - gf < rsize;
+                if (nb < (uint32_t)kR1Min && more) break;
             }
         }
         INW_CYC(c, 4, t_seg);

@@ -85,3 +85,95 @@ def test_group_rejects_bad_device_lists(gpu):
     assert not lib.rt_group_create((C.c_int * 2)(0, 0), 2)   # one rank per device
     assert not lib.rt_group_create((C.c_int * 1)(4096), 1)   # no such device
     assert not lib.rt_group_create(None, 1)
+
+
+def test_bench_group_mode_matches_single_device(gpu, tmp_path):
+    """bench.py --group (the C-ABI device group timed from one process, rt_render_multi_async) on a
+    reduced C3 frame: its assembled colour and depth images equal a single-device render of the
+    same scene bit for bit, and the line reports the frame's ray count."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    img = str(tmp_path / "g.npy")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--group", "--gpus", "1", "--config", "c3",
+                        "--width", "96", "--height", "54", "--spp", "6", "--steps", "1", "--warmup", "1",
+                        "--save-image", img], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["config"]["parallelism"] == "group1+rccl_send_recv"
+    sc = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 10_000, width=96, height=54, spp=6)
+    g, gd, gst = R.render(sc)
+    assert compare(np.load(img), g)["exact_frac"] == 1.0
+    assert compare(np.load(str(tmp_path / "g.depth.npy")), gd)["exact_frac"] == 1.0
+    assert line["rays_per_step"] == gst["segments"]
+
+
+def test_group_refuses_a_scene_of_another_device(gpu):
+    """rt_render_multi_async checks that scenes[r] was built on the group's device r (a scene's
+    buffers belong to its device).  With one GPU the mismatch is a scene list whose entry is not
+    on device 0 -- here a null entry and, when a second device exists, a scene built there."""
+    import torch
+
+    lib = R.load()
+    sc = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 500, width=32, height=16, spp=2)
+    grp = lib.rt_group_create((C.c_int * 1)(0), 1)
+    assert grp
+    dev = torch.device("cuda", 0)
+    img = torch.zeros((16, 32, 4), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    other = None
+    try:
+        assert lib.rt_render_multi_async(grp, (C.c_void_p * 1)(None), C.byref(sc.camera), C.byref(sc.params), 16,
+                                         img.data_ptr(), None, None, stream) == R.RT_E_ARG
+        if torch.cuda.device_count() > 1:
+            other = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, 1, R.fptr(sc.nodes), None, 0, sc.params.spp, 1)
+            assert other
+            assert lib.rt_render_multi_async(grp, (C.c_void_p * 1)(other), C.byref(sc.camera), C.byref(sc.params),
+                                             16, img.data_ptr(), None, None, stream) == R.RT_E_ARG
+        mine = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, 1, R.fptr(sc.nodes), None, 0, sc.params.spp, 0)
+        assert mine
+        try:
+            assert lib.rt_render_multi_async(grp, (C.c_void_p * 1)(mine), C.byref(sc.camera), C.byref(sc.params), 16,
+                                             img.data_ptr(), None, None, stream) == 0
+            torch.cuda.synchronize()
+        finally:
+            lib.rt_dev_scene_free(mine)
+    finally:
+        if other:
+            lib.rt_dev_scene_free(other)
+        lib.rt_group_free(grp)
+
+
+def test_group_frame_size_changes_between_async_frames(gpu):
+    """a new frame or tile size re-deals the tiles; the re-upload waits for the group's
+    earlier frame, so two async frames of different sizes with no host sync between them are both
+    bit-identical to single-device renders."""
+    import torch
+
+    lib = R.load()
+    sc = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 2000, width=80, height=48, spp=5)
+    s = lib.rt_dev_scene_inw(R.fptr(sc.geom), sc.n, 1, R.fptr(sc.nodes), None, 0, sc.params.spp, 0)
+    grp = lib.rt_group_create((C.c_int * 1)(0), 1)
+    assert s and grp
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    try:
+        outs = []
+        for (w, h, tile) in ((80, 48, 16), (64, 40, 32), (80, 48, 16)):
+            p = R.RtParams.from_buffer_copy(sc.params)
+            p.width, p.height = w, h
+            img = torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
+            assert lib.rt_render_multi_async(grp, (C.c_void_p * 1)(s), C.byref(sc.camera), C.byref(p), tile,
+                                             img.data_ptr(), None, None, stream) == 0
+            outs.append((w, h, img))
+        torch.cuda.synchronize()
+        for w, h, img in outs:
+            ref = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 2000, width=w, height=h, spp=5)
+            g, _, _ = R.render(ref)
+            assert compare(img.cpu().numpy(), g)["exact_frac"] == 1.0, (w, h)
+    finally:
+        lib.rt_group_free(grp)
+        lib.rt_dev_scene_free(s)
