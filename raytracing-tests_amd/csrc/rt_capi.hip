@@ -209,6 +209,7 @@ struct rt_dev_scene {
     DevBuf cont[2], cont_count;
     // sample-parallel IOW-03 records, sized for spec_cap (pixel units x samples)
     size_t spec_cap = 0, spec_units = 0;
+    uint32_t spec_P = 0, spec_S = 0;  // the last sample-parallel render's P and S (its record layout, SpecRecs::ix)
     DevBuf sp_col, sp_fin, sp_ctr, sp_assume, sp_list, sp_fb, sp_counts;
     DevBuf sp_keys, sp_keys2, sp_list2, sp_temp;  // longest-first ordering of the re-execution list
     DevBuf sp_pstate;  // asynchronous windows: per-pixel frontier state
@@ -913,6 +914,9 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
                           S > 2 && groups == 1 ? uint32_t(std::min(int(S) - 2, o.spec_heavy >= 0 ? o.spec_heavy
                                                                                                 : heavy_auto))
                                                : 0u};
+    R.pmag = rtk::spec_pmag(P);
+    s->spec_P = P;
+    s->spec_S = S;
     s->launch_seq = 0;
 #ifdef RT_DIAG
     if (env_int("RT_DEBUG_TIMES", 0) != 0) {  // diagnostic builds only (rt_debug_spec_times)
@@ -1198,6 +1202,7 @@ int launch_scene_spec(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         if (o.spec_validate != 0) {  // reuse the records that are still exact
             ch.rec_col = R.col; ch.rec_fin = R.fin; ch.rec_assume = R.assume; ch.rec_ctr = R.ctr;
             ch.rec_P = P;
+            ch.rec_S = S;
         }
         if (e == hipSuccess)
             pass(L, [&, ch](const Lane &q, const rtk::Cont &ct, uint32_t n) {
@@ -1682,8 +1687,8 @@ int rt_debug_spec_list_hist(rt_dev_scene *s, uint64_t *out) {
     DevBuf d;
     HIP_OK(d.alloc(66 * sizeof(uint64_t)));
     HIP_OK(hipMemset(d.p, 0, 66 * sizeof(uint64_t)));
-    HIP_OK(rtk::spec_list_hist(s->sp_ctr.as<uint4>(), s->sp_list.as<uint32_t>(), s->sp_counts.as<unsigned>(),
-                               d.as<unsigned long long>(), nullptr));
+    HIP_OK(rtk::spec_list_hist(s->sp_ctr.as<uint4>(), s->spec_P, s->spec_S, s->sp_list.as<uint32_t>(),
+                               s->sp_counts.as<unsigned>(), d.as<unsigned long long>(), nullptr));
     HIP_OK(hipMemcpy(out, d.p, 66 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
@@ -1695,16 +1700,16 @@ int rt_debug_spec_list_stale(rt_dev_scene *s, uint64_t *out) {
     DevBuf d;
     HIP_OK(d.alloc(32 * sizeof(uint64_t)));
     HIP_OK(hipMemset(d.p, 0, 32 * sizeof(uint64_t)));
-    HIP_OK(rtk::spec_list_stale(s->sp_ctr.as<uint4>(), s->sp_list.as<uint32_t>(), s->sp_counts.as<unsigned>(),
-                                d.as<unsigned long long>(), nullptr));
+    HIP_OK(rtk::spec_list_stale(s->sp_ctr.as<uint4>(), s->spec_P, s->spec_S, s->sp_list.as<uint32_t>(),
+                                s->sp_counts.as<unsigned>(), d.as<unsigned long long>(), nullptr));
     HIP_OK(hipMemcpy(out, d.p, 32 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 
 int rt_debug_spec_pixels(rt_dev_scene *s, uint32_t *out, uint32_t cap_units) {
     if (!s || !out) return RT_E_ARG;
-    if (!s->spec_cap || !s->spec_units || s->spec_units > cap_units) return RT_E_ARG;
-    const uint32_t P = s->spec_units, S = uint32_t(s->spec_cap / P);
+    if (!s->spec_cap || !s->spec_P || s->spec_P > cap_units) return RT_E_ARG;
+    const uint32_t P = s->spec_P, S = s->spec_S;  // the last render's record layout
     DevBuf d;
     HIP_OK(d.alloc(size_t(P) * 16));
     HIP_OK(rtk::spec_pixels(s->sp_ctr.as<uint4>(), P, S, s->ws_order.as<uint32_t>(), d.as<uint32_t>(), nullptr));
@@ -1715,12 +1720,12 @@ int rt_debug_spec_pixels(rt_dev_scene *s, uint32_t *out, uint32_t cap_units) {
 int rt_debug_spec_dump(rt_dev_scene *s, uint32_t *rays_out, size_t cap, uint32_t *list_out, uint32_t list_cap,
                        uint32_t *dims) {
     if (!s || !rays_out || !dims) return RT_E_ARG;
-    if (!s->spec_cap || !s->spec_units) return RT_E_ARG;
-    const uint32_t P = uint32_t(s->spec_units), S = uint32_t(s->spec_cap / P);
+    if (!s->spec_cap || !s->spec_P) return RT_E_ARG;
+    const uint32_t P = s->spec_P, S = s->spec_S;  // the last render's record layout (SpecRecs::ix)
     if (size_t(P) * S > cap) return RT_E_ARG;
     std::vector<uint4> h(size_t(P) * S);
     HIP_OK(hipMemcpy(h.data(), s->sp_ctr.p, h.size() * sizeof(uint4), hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < h.size(); i++) rays_out[i] = h[i].x;
+    for (size_t u = 0; u < h.size(); u++) rays_out[u] = h[rtk::spec_rec_ix(u, P, S)].x;  // in unit order s * P + pu
     unsigned cnt[32] = {};
     HIP_OK(hipMemcpy(cnt, s->sp_counts.p, sizeof(cnt), hipMemcpyDeviceToHost));
     const uint32_t nl = std::min(cnt[0], list_cap);
@@ -1749,15 +1754,15 @@ int rt_debug_launches(rt_dev_scene *s, char *name_out, int name_cap) {
         const uint32_t ord = s->last_force;  // the order the launch used (0: the probe's verdict)
         const bool sm = ord == 2 || (ord != 1 && m[0] > 0 && 2 * m[1] >= m[0]);
         // the template instance's name as rocprofv3 prints it, every template argument:
-        // <LIGHTS, LN (LDS-staged BVH top), FU (fused cull)[, LRING (k_inw_pm: the fold ring in LDS)]>
+        // <LIGHTS, LN (LDS-staged BVH top), FU (fused cull), LRING (the fold ring in LDS)[, GQ (k_inw_pm)]>
         auto tf = [](bool b) { return b ? "true" : "false"; };
         const bool fu = s->last_fu, ln = s->last_ln, lights = s->layout == 4;
         if (sm)
             std::snprintf(s->kname, sizeof(s->kname), "k_inw_sm<%s, %s, %s, %s>", tf(lights), tf(ln), tf(fu),
                           tf(s->last_lring_sm));
         else
-            std::snprintf(s->kname, sizeof(s->kname), "k_inw_pm<%s, %s, %s, %s>", tf(lights), tf(ln), tf(fu),
-                          tf(s->last_lring));
+            std::snprintf(s->kname, sizeof(s->kname), "k_inw_pm<%s, %s, %s, %s, %s>", tf(lights), tf(ln), tf(fu),
+                          tf(s->last_lring || s->last_gq), tf(s->last_gq));
         s->last_kernel = s->kname;
     }
     if (name_out && name_cap > 0) {

@@ -954,7 +954,7 @@ __device__ __forceinline__ void iow03_body(const Frame &f, const IowScene &S, co
             // take every following sample whose speculative record assumed the exact stack
             // state (the RI of the entries it read before writing them) from its record
             while (busy && K.size == 0 && s < s_end) {
-                const size_t u = (size_t)s * ch.rec_P + unit;
+                const size_t u = (size_t)unit * ch.rec_S + s;  // the record of unit s * rec_P + unit
                 const float4 cl = ch.rec_col[u], a = ch.rec_assume[u];
                 const uint32_t fl = __float_as_uint(cl.w), rm = fl & 15u, wm = (fl >> 4) & 15u;
                 if (((rm & 2u) && __float_as_uint(a.x) != __float_as_uint(K.at(1, 7))) ||
@@ -1067,10 +1067,10 @@ __device__ uint32_t alt_adopt(const SpecRecs &R, uint32_t u, uint32_t E1, uint32
         if (((rm & 2u) && __float_as_uint(A.assume.x) != E1) || ((rm & 4u) && __float_as_uint(A.assume.y) != E2) ||
             ((rm & 8u) && __float_as_uint(A.assume.z) != E3))
             continue;
-        R.assume[u] = A.assume;
-        R.fin[u] = A.fin;
-        R.ctr[u] = A.ctr;
-        R.col[u] = make_float4(A.col.x, A.col.y, A.col.z,
+        R.assume[R.ix(u)] = A.assume;
+        R.fin[R.ix(u)] = A.fin;
+        R.ctr[R.ix(u)] = A.ctr;
+        R.col[R.ix(u)] = make_float4(A.col.x, A.col.y, A.col.z,
                                __uint_as_float((fl & ~(63u << 10)) | ((tag_launch & 63u) << 10)));
         return fk.x + i + 1u;
     }
@@ -1200,7 +1200,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 alt_slot = slot + 1u;
             } else if (q < nin && ct.in[(size_t)q * kContSlots + 12].y != 0.0f) {  // doomed while parked: restart exact
                 u = __float_as_uint(ct.in[(size_t)q * kContSlots].x);
-                begin(u, R.assume[u]);
+                begin(u, R.assume[R.ix(u)]);
                 exact = ct.chain != 0;
                 alt_slot = 0;
             } else if (q < nin) {  // resume a parked lane
@@ -1234,12 +1234,12 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                     else if (ct.fresh_mode == 2) { s_ = R.sorder[qf / n_px]; rank = qf % n_px; }
                     else { s_ = R.sorder[R.n_heavy + qf % nr]; rank = qf / nr; }
                     u = s_ * R.P + R.order[R.order_base + rank];
-                    const uint32_t tag = __float_as_uint(R.col[u].w);
+                    const uint32_t tag = __float_as_uint(R.col[R.ix(u)].w);
                     fresh = !((tag >> 16) == (R.epoch & 0xffffu) && (tag & 0x300u) != 0u);
                 }
                 if (fresh && unit_pixel(f, u % R.P).in_image) {
-                    if (ct.fresh_mode != 0) R.col[u].w = ubits(started_tag);
-                    begin(u, mode == kSpecFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : R.assume[u]);
+                    if (ct.fresh_mode != 0) R.col[R.ix(u)].w = ubits(started_tag);
+                    begin(u, mode == kSpecFirst ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : R.assume[R.ix(u)]);
                     exact = false;
                     alt_slot = 0;
                 }
@@ -1278,10 +1278,10 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
             alt_slot = 0;
         }
         if (busy && K.size == 0) {  // sample done: record it
-            R.col[u] = make_float4(sample.x, sample.y, sample.z,
+            R.col[R.ix(u)] = make_float4(sample.x, sample.y, sample.z,
                                    ubits(K.rmask | (K.wmask << 4) | done_tag | ((ct.launch_id & 63u) << 10)));
-            R.fin[u] = make_float4(K.at(1, 7), K.at(2, 7), K.at(3, 7), ubits(c.prims));
-            R.ctr[u] = make_uint4(c.seg, c.drops, c.nans, c.nodes);
+            R.fin[R.ix(u)] = make_float4(K.at(1, 7), K.at(2, 7), K.at(3, 7), ubits(c.prims));
+            R.ctr[R.ix(u)] = make_uint4(c.seg, c.drops, c.nans, c.nodes);
 #ifdef RT_DIAG
             if (R.dbg_end) R.dbg_end[u] = ct.launch_id;
 #endif
@@ -1307,14 +1307,14 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                 };
                 for (uint32_t t = u / R.P + 1u; t < R.S; t++) {
                     const uint32_t v = t * R.P + pu;
-                    unsigned *flp = reinterpret_cast<unsigned *>(&R.col[v].w);
-                    const unsigned fl = ld(&R.col[v].w);
+                    unsigned *flp = reinterpret_cast<unsigned *>(&R.col[R.ix(v)].w);
+                    const unsigned fl = ld(&R.col[R.ix(v)].w);
                     if ((fl & 0xffff0100u) != done_tag || ((fl >> 10) & 63u) == (ct.launch_id & 63u)) break;
                     const unsigned rm = fl & 15u, wm = (fl >> 4) & 15u;
-                    const unsigned a1 = ld(&R.assume[v].x), a2 = ld(&R.assume[v].y), a3 = ld(&R.assume[v].z);
-                    const unsigned f1 = ld(&R.fin[v].x), f2 = ld(&R.fin[v].y), f3v = ld(&R.fin[v].z);
+                    const unsigned a1 = ld(&R.assume[R.ix(v)].x), a2 = ld(&R.assume[R.ix(v)].y), a3 = ld(&R.assume[R.ix(v)].z);
+                    const unsigned f1 = ld(&R.fin[R.ix(v)].x), f2 = ld(&R.fin[R.ix(v)].y), f3v = ld(&R.fin[R.ix(v)].z);
                     __atomic_thread_fence(__ATOMIC_ACQUIRE);
-                    if (ld(&R.col[v].w) != fl) break;
+                    if (ld(&R.col[R.ix(v)].w) != fl) break;
                     if (((rm & 2u) && a1 != E1) || ((rm & 4u) && a2 != E2) || ((rm & 8u) && a3 != E3)) {
                         unsigned expect = fl;
                         if (!__hip_atomic_compare_exchange_strong(flp, &expect, started_tag, __ATOMIC_ACQ_REL,
@@ -1330,7 +1330,7 @@ __device__ __forceinline__ void iow03s_body(const Frame &f, const IowScene &S, c
                             continue;
                         }
                         const float4 e = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
-                        R.assume[v] = e;
+                        R.assume[R.ix(v)] = e;
                         begin(v, e);
                         break;
                     }
@@ -1366,23 +1366,23 @@ __global__ __launch_bounds__(kBlock) void k_iow03_prep(Frame f, SpecRecs R, unsi
     if (pu >= R.P) return;  // no cross-lane work in this kernel
     const UnitPix px = unit_pixel(f, pu);
     if (!px.in_image) { key[pu] = 0; return; }
-    const uint32_t wm = (__float_as_uint(R.col[pu].w) >> 4) & 15u;
-    const float4 fn = R.fin[pu];
+    const uint32_t wm = (__float_as_uint(R.col[R.ix(pu)].w) >> 4) & 15u;
+    const float4 fn = R.fin[R.ix(pu)];
     const float4 e0 = make_float4((wm & 2u) ? fn.x : 0.0f, (wm & 4u) ? fn.y : 0.0f, (wm & 8u) ? fn.z : 0.0f, 0.0f);
     // From prior_from on every entry is guessed as the prior: sample 0 starts from the all-zero
     // stack no later sample sees (a stale 0 makes target_RI 0 and forces TIR, 03...glsl:316-327),
     // so the values it leaves are a worse guess of the steady state than the scene's most common
     // RI (tests/analysis/fork_stats.py: mispredicted rays 2.6% -> 0.8% on C2).
     const float4 e1 = make_float4(prior, prior, prior, 0.0f);
-    for (uint32_t s = 1; s < R.S; s++) R.assume[(size_t)s * R.P + pu] = s >= prior_from ? e1 : e0;
+    for (uint32_t s = 1; s < R.S; s++) R.assume[R.ix((size_t)s * R.P + pu)] = s >= prior_from ? e1 : e0;
 #ifdef RT_DIAG
     if (R.exact && (R.exact_mode & 2))
-        for (uint32_t s = 1; s < R.S; s++) R.assume[(size_t)s * R.P + pu] = R.exact[(size_t)s * R.P + pu];
+        for (uint32_t s = 1; s < R.S; s++) R.assume[R.ix((size_t)s * R.P + pu)] = R.exact[(size_t)s * R.P + pu];
 #endif
     if (R.front)  // sample 0 is exact: the frontier starts at sample 1 with its final entries
         R.front[pu] = make_uint4(1u, __float_as_uint(e0.x), __float_as_uint(e0.y), __float_as_uint(e0.z));
     if (R.front2) R.front2[pu] = make_uint4(0xffffffffu, 0u, 0u, 0u);
-    key[pu] = R.ctr[pu].x;
+    key[pu] = R.ctr[R.ix(pu)].x;
 }
 
 // ---------------------------------------------------------------- checkpoint rounds
@@ -1407,8 +1407,8 @@ __global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, 
     auto requeue = [&](size_t u, uint32_t e1, uint32_t e2, uint32_t e3) {
         const uint32_t slot = atomicAdd(count, 1u);
         if (slot >= cap) { atomicSub(count, 1u); return; }  // full: leave it to the resolve after the pass
-        R.assume[u] = make_float4(__uint_as_float(e1), __uint_as_float(e2), __uint_as_float(e3), 0.0f);
-        R.col[u].w = __uint_as_float((1u << 9) | ((R.epoch & 0xffffu) << 16));  // queued: unfinished
+        R.assume[R.ix(u)] = make_float4(__uint_as_float(e1), __uint_as_float(e2), __uint_as_float(e3), 0.0f);
+        R.col[R.ix(u)].w = __uint_as_float((1u << 9) | ((R.epoch & 0xffffu) << 16));  // queued: unfinished
         float4 *p = cont + (size_t)slot * kContSlots;
         p[0] = make_float4(__uint_as_float((uint32_t)u), 0.0f, 0.0f, 0.0f);
         p[12] = make_float4(0.0f, 1.0f, 0.0f, 0.0f);  // restart with the (now exact) assumption
@@ -1417,17 +1417,17 @@ __global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, 
     bool queued = false;
     for (; s < R.S; s++) {
         const size_t u = (size_t)s * R.P + pu;
-        unsigned fl = __float_as_uint(R.col[u].w);
+        unsigned fl = __float_as_uint(R.col[R.ix(u)].w);
         if ((fl & 0xffff0100u) != done_tag) {  // still running (or queued): an alternative may hold it
             if (!R.alt || !alt_adopt(R, (uint32_t)u, st.y, st.z, st.w, 0xffffffffu, 0u)) break;
-            fl = __float_as_uint(R.col[u].w);
+            fl = __float_as_uint(R.col[R.ix(u)].w);
         }
-        const float4 a = R.assume[u];
+        const float4 a = R.assume[R.ix(u)];
         const unsigned rm = fl & 15u, wm = (fl >> 4) & 15u;
         if (((rm & 2u) && __float_as_uint(a.x) != st.y) || ((rm & 4u) && __float_as_uint(a.y) != st.z) ||
             ((rm & 8u) && __float_as_uint(a.z) != st.w)) {
             if (R.alt && alt_adopt(R, (uint32_t)u, st.y, st.z, st.w, 0xffffffffu, 0u)) {
-                fl = __float_as_uint(R.col[u].w);  // the adopted alternative is exact: go on
+                fl = __float_as_uint(R.col[R.ix(u)].w);  // the adopted alternative is exact: go on
             } else {
                 requeue(u, st.y, st.z, st.w);
                 queued = true;
@@ -1436,7 +1436,7 @@ __global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, 
         }
         const unsigned wm2 = (fl >> 4) & 15u;
         (void)wm;
-        const float4 fn = R.fin[u];
+        const float4 fn = R.fin[R.ix(u)];
         if (wm2 & 2u) st.y = __float_as_uint(fn.x);
         if (wm2 & 4u) st.z = __float_as_uint(fn.y);
         if (wm2 & 8u) st.w = __float_as_uint(fn.z);
@@ -1462,7 +1462,7 @@ __global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, 
         const uint32_t k_end = min(R.S, s + 1u + R.scan_max);
         for (uint32_t k = s + 1u; k < k_end; k++) {
             const size_t u = (size_t)k * R.P + pu;
-            const unsigned fl = __float_as_uint(R.col[u].w);
+            const unsigned fl = __float_as_uint(R.col[R.ix(u)].w);
             if ((fl & 0xffff0100u) != done_tag) {  // unfinished: fixf may patch the first one
                 if (known == 14u && f2.x == 0xffffffffu) f2 = make_uint4(k, E[1], E[2], E[3]);
                 known = 0;  // its outputs are unknown; later anchors restore knowledge
@@ -1470,21 +1470,21 @@ __global__ __launch_bounds__(kBlock) void k_iow03_frontier(Frame f, SpecRecs R, 
             }
             const unsigned rm = fl & 14u, wm = (fl >> 4) & 14u;
             if (rm & ~known) { known &= ~wm; continue; }  // read an unknown entry: its writes are unknown
-            const float4 a = R.assume[u];
+            const float4 a = R.assume[R.ix(u)];
             const bool bad = ((rm & 2u) && __float_as_uint(a.x) != E[1]) ||
                              ((rm & 4u) && __float_as_uint(a.y) != E[2]) ||
                              ((rm & 8u) && __float_as_uint(a.z) != E[3]);
             unsigned wmx = wm;
             if (bad) {  // mispredicted: adopt an alternative, or re-run it now if the whole state is known
                 if (known == 14u && R.alt && alt_adopt(R, (uint32_t)u, E[1], E[2], E[3], 0xffffffffu, 0u)) {
-                    wmx = (__float_as_uint(R.col[u].w) >> 4) & 14u;
+                    wmx = (__float_as_uint(R.col[R.ix(u)].w) >> 4) & 14u;
                 } else {
                     if (known == 14u) requeue(u, E[1], E[2], E[3]);
                     known = 0;
                     continue;
                 }
             }
-            const float4 fn = R.fin[u];
+            const float4 fn = R.fin[R.ix(u)];
             if (wmx & 2u) E[1] = __float_as_uint(fn.x);
             if (wmx & 4u) E[2] = __float_as_uint(fn.y);
             if (wmx & 8u) E[3] = __float_as_uint(fn.z);
@@ -1509,14 +1509,14 @@ __global__ __launch_bounds__(kBlock) void k_iow03_altspawn(Frame f, SpecRecs R, 
     const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
     for (uint32_t s = R.front[pu].x; s < R.S; s++) {
         const uint32_t u = s * R.P + pu;
-        const unsigned fl = __float_as_uint(R.col[u].w);
+        const unsigned fl = __float_as_uint(R.col[R.ix(u)].w);
         if ((fl & 0xffff0100u) != done_tag) continue;
         const unsigned rm = fl & 14u;
         if (rm == 0u || (rm & (rm - 1u)) != 0u) continue;  // exactly one stale entry read
-        if (R.ctr[u].x < R.alt_min_seg) continue;
+        if (R.ctr[R.ix(u)].x < R.alt_min_seg) continue;
         if (alt_find(R, u).y != 0u) continue;
         const int e = rm == 2u ? 0 : (rm == 4u ? 1 : 2);
-        const float4 a = R.assume[u];
+        const float4 a = R.assume[R.ix(u)];
         const float ae = e == 0 ? a.x : (e == 1 ? a.y : a.z);
         uint32_t k = 0;
         for (int v = 0; v < R.n_alt_vals; v++) k += __float_as_uint(R.alt_vals[v]) != __float_as_uint(ae);
@@ -1568,13 +1568,13 @@ __global__ __launch_bounds__(kBlock) void k_iow03_fixf(Frame f, SpecRecs R, floa
     }
     const unsigned E[3] = {st.y, st.z, st.w};
     const unsigned masks = __float_as_uint(p[0].w), wm = masks & 15u, rm = masks >> 4;
-    float4 a = R.assume[u];
+    float4 a = R.assume[R.ix(u)];
     float *av = &a.x;
     bool doomed = false;
     for (int k = 1; k <= 3; k++)
         if (((rm >> k) & 1u) && __float_as_uint(av[k - 1]) != E[k - 1]) doomed = true;
     if (doomed) {
-        R.assume[u] = make_float4(__uint_as_float(E[0]), __uint_as_float(E[1]), __uint_as_float(E[2]), 0.0f);
+        R.assume[R.ix(u)] = make_float4(__uint_as_float(E[0]), __uint_as_float(E[1]), __uint_as_float(E[2]), 0.0f);
         p[12].y = 1.0f;
         return;
     }
@@ -1584,7 +1584,7 @@ __global__ __launch_bounds__(kBlock) void k_iow03_fixf(Frame f, SpecRecs R, floa
             fl[k * 9 + 7] = __uint_as_float(E[k - 1]);
             av[k - 1] = __uint_as_float(E[k - 1]);
         }
-    R.assume[u] = a;
+    R.assume[R.ix(u)] = a;
 }
 
 // Replay of each pixel's samples in order (one lane per pixel unit; records are [s][pu], so
@@ -1602,9 +1602,9 @@ __global__ __launch_bounds__(kBlock) void k_iow03_resolve(Frame f, SpecRecs R, i
     uint32_t s = 0;
     for (; work && s < R.S; s++) {
         const size_t u = (size_t)s * R.P + pu;
-        float4 cl = R.col[u];
+        float4 cl = R.col[R.ix(u)];
         uint32_t fl = __float_as_uint(cl.w), rm = fl & 15u, wm = (fl >> 4) & 15u;
-        float4 a = R.assume[u];
+        float4 a = R.assume[R.ix(u)];
 #ifdef RT_DIAG
         if (final_pass && R.exact && (R.exact_mode & 1) && first_bad < 0)
             R.exact[u] = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
@@ -1612,24 +1612,24 @@ __global__ __launch_bounds__(kBlock) void k_iow03_resolve(Frame f, SpecRecs R, i
         bool bad = ((rm & 2u) && __float_as_uint(a.x) != E1) || ((rm & 4u) && __float_as_uint(a.y) != E2) ||
                    ((rm & 8u) && __float_as_uint(a.z) != E3);
         if (bad && first_bad < 0 && R.alt && alt_adopt(R, (uint32_t)u, E1, E2, E3, 0xffffffffu, 0u)) {
-            cl = R.col[u];  // an alternative run under the exact state: adopted
+            cl = R.col[R.ix(u)];  // an alternative run under the exact state: adopted
             fl = __float_as_uint(cl.w); rm = fl & 15u; wm = (fl >> 4) & 15u;
-            a = R.assume[u];
+            a = R.assume[R.ix(u)];
             bad = false;
         }
         if (bad) {
             if (first_bad < 0) first_bad = (int)s;
             if (final_pass) break;  // the sequential kernel takes over from here
-            R.assume[u] = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
+            R.assume[R.ix(u)] = make_float4(__uint_as_float(E1), __uint_as_float(E2), __uint_as_float(E3), 0.0f);
             R.list[atomicAdd(R.list_count, 1u)] = (uint32_t)u;
         }
         if (first_bad < 0) {  // still exact: accumulate in sample order
             fc = fc + f3{cl.x, cl.y, cl.z};
-            const uint4 ct4 = R.ctr[u];
+            const uint4 ct4 = R.ctr[R.ix(u)];
             seg += ct4.x; drops += ct4.y; nans += ct4.z; nodes += ct4.w;
-            prims += __float_as_uint(R.fin[u].w);
+            prims += __float_as_uint(R.fin[R.ix(u)].w);
         }
-        const float4 fn = R.fin[u];  // the record's own outputs (a guess while it is queued)
+        const float4 fn = R.fin[R.ix(u)];  // the record's own outputs (a guess while it is queued)
         if (wm & 2u) E1 = __float_as_uint(fn.x);
         if (wm & 4u) E2 = __float_as_uint(fn.y);
         if (wm & 8u) E3 = __float_as_uint(fn.z);
@@ -3964,10 +3964,10 @@ __global__ void k_spec_pixels(const uint4 *ctr, uint32_t P, uint32_t S, const ui
     if (pu >= P) return;  // no cross-lane work in this kernel
     uint32_t mx = 0, arg = 0;
     for (uint32_t s = 0; s < S; s++) {
-        const uint32_t v = ctr[(size_t)s * P + pu].x;
+        const uint32_t v = ctr[(size_t)pu * S + s].x;
         if (v > mx) { mx = v; arg = s; }
     }
-    out[4 * (size_t)pu] = ctr[pu].x;
+    out[4 * (size_t)pu] = ctr[(size_t)pu * S].x;
     out[4 * (size_t)pu + 1] = mx;
     out[4 * (size_t)pu + 2] = arg;
     out[4 * (size_t)order[pu] + 3] = pu;  // out[.3] of row r = the pixel at order rank r
@@ -3979,28 +3979,28 @@ hipError_t spec_pixels(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t 
 }
 // diagnostics: where re-executed samples first read a stale entry (RT_DEBUG_FIRST_STALE runs):
 // out[b] = samples, out[16 + b] = their rays, bucket b = 16 * first_stale_segment / rays
-__global__ void k_spec_list_stale(const uint4 *ctr, const uint32_t *list, const unsigned *count,
+__global__ void k_spec_list_stale(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *list, const unsigned *count,
                                   unsigned long long *out) {
     const unsigned n = *count;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        const uint4 c = ctr[list[i]];
+        const uint4 c = ctr[spec_rec_ix(list[i], P, S)];
         if (!(c.y & 0x80000000u) || c.x == 0) continue;
         const unsigned b = min(15u, (unsigned)(((unsigned long long)(c.y & 0x7fffffffu) * 16ull) / c.x));
         atomicAdd(out + b, 1ull);
         atomicAdd(out + 16 + b, (unsigned long long)c.x);
     }
 }
-hipError_t spec_list_stale(const uint4 *ctr, const uint32_t *list, const unsigned *count, unsigned long long *d_out,
-                           hipStream_t s) {
-    hipLaunchKernelGGL(k_spec_list_stale, dim3(1024), dim3(256), 0, s, ctr, list, count, d_out);
+hipError_t spec_list_stale(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *list, const unsigned *count,
+                           unsigned long long *d_out, hipStream_t s) {
+    hipLaunchKernelGGL(k_spec_list_stale, dim3(1024), dim3(256), 0, s, ctr, P, S, list, count, d_out);
     return hipGetLastError();
 }
 // diagnostics: log2 histogram of the rays of the samples on the (first) re-execution list
-__global__ void k_spec_list_hist(const uint4 *ctr, const uint32_t *list, const unsigned *count,
+__global__ void k_spec_list_hist(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *list, const unsigned *count,
                                  unsigned long long *out) {
     const unsigned n = *count;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        const unsigned v = ctr[list[i]].x;
+        const unsigned v = ctr[spec_rec_ix(list[i], P, S)].x;
         if (v == 0) continue;
         const int b = 31 - __clz(v);
         atomicAdd(out + 2 + b, 1ull);
@@ -4009,9 +4009,9 @@ __global__ void k_spec_list_hist(const uint4 *ctr, const uint32_t *list, const u
         atomicAdd(out + 1, 1ull);
     }
 }
-hipError_t spec_list_hist(const uint4 *ctr, const uint32_t *list, const unsigned *count, unsigned long long *d_out,
-                          hipStream_t s) {
-    hipLaunchKernelGGL(k_spec_list_hist, dim3(1024), dim3(256), 0, s, ctr, list, count, d_out);
+hipError_t spec_list_hist(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *list, const unsigned *count,
+                          unsigned long long *d_out, hipStream_t s) {
+    hipLaunchKernelGGL(k_spec_list_hist, dim3(1024), dim3(256), 0, s, ctr, P, S, list, count, d_out);
     return hipGetLastError();
 }
 hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipStream_t s) {
@@ -4021,7 +4021,7 @@ hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipS
 __global__ void k_spec_list_keys(SpecRecs R, unsigned *keys, size_t n) {
     const unsigned cnt = *R.list_count;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        keys[i] = i < cnt ? min(R.ctr[R.list[i]].x, 0xffffffu) : 0u;
+        keys[i] = i < cnt ? min(R.ctr[R.ix(R.list[i])].x, 0xffffffu) : 0u;
 }
 hipError_t spec_list_keys(const SpecRecs &R, unsigned *keys, size_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_spec_list_keys, dim3(4096), dim3(256), 0, s, R, keys, n);
@@ -4037,7 +4037,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_cost(SpecRecs R, unsigned lon
     unsigned long long acc = 0;
     for (uint32_t i = threadIdx.x; (size_t)i * R.probe_stride < n_px; i += kBlock) {
         const size_t u = (size_t)s * R.P + R.order[R.order_base + i * R.probe_stride];
-        if ((__float_as_uint(R.col[u].w) & 0xffff0100u) == done_tag) acc += R.ctr[u].x;
+        if ((__float_as_uint(R.col[R.ix(u)].w) & 0xffff0100u) == done_tag) acc += R.ctr[R.ix(u)].x;
     }
     acc = wave_sum(acc);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
@@ -4074,10 +4074,10 @@ __global__ __launch_bounds__(kBlock) void k_pixel_key(Frame f, SpecRecs R, unsig
     if (i >= n_px) return;  // no cross-lane work in this kernel
     const uint32_t pu = R.order[R.order_base + i];
     const unsigned done_tag = (1u << 8) | ((R.epoch & 0xffffu) << 16);
-    unsigned k = R.ctr[pu].x;  // sample 0
+    unsigned k = R.ctr[R.ix(pu)].x;  // sample 0
     for (uint32_t j = 0; j < R.n_heavy; j++) {
         const size_t u = (size_t)R.sorder[j] * R.P + pu;
-        if ((__float_as_uint(R.col[u].w) & 0xffff0100u) == done_tag) k = max(k, R.ctr[u].x);
+        if ((__float_as_uint(R.col[R.ix(u)].w) & 0xffff0100u) == done_tag) k = max(k, R.ctr[R.ix(u)].x);
     }
     key[pu] = unit_pixel(f, pu).in_image ? k : 0u;
 }

@@ -143,7 +143,7 @@ struct Chunk {
     // a sample whose record assumed the exact incoming stack state is taken from the record
     const float4 *rec_col, *rec_fin, *rec_assume;
     const uint4 *rec_ctr;
-    uint32_t rec_P;
+    uint32_t rec_P, rec_S;  // their layout: unit s * rec_P + pu at pu * rec_S + s (SpecRecs::ix)
 };
 
 // Sample-parallel IOW-03 (DESIGN.md "Sample-parallel speculation").  A unit is one (pixel,
@@ -164,6 +164,21 @@ struct SpecRecs {
     uint4 *ctr;        // segments, stack drops, NaN directions, node visits
     float4 *assume;    // assumed RI of entries 1..3 before the sample
     uint32_t P, S;     // pixel units, samples per pixel (s_stop)
+    // The record of unit u = s * P + pu sits at pu * S + s: a pixel's samples are adjacent, so the
+    // waves of the bulk pass (consecutive samples of one pixel) read and write whole lines, and the
+    // per-pixel sample walks (chain following, the frontier rounds) stay in one line for 8 samples
+    // (DESIGN.md §5.4).  u < 2^32; q = mulhi(u, pmag) is u / P or one more.
+    __host__ __device__ __forceinline__ size_t ix(size_t u) const {
+        const uint32_t uu = (uint32_t)u;
+#ifdef __HIP_DEVICE_COMPILE__
+        uint32_t q = __umulhi(uu, pmag);
+#else
+        uint32_t q = (uint32_t)(((uint64_t)uu * pmag) >> 32);
+#endif
+        int32_t r = (int32_t)(uu - q * P);
+        if (r < 0) { q--; r += (int32_t)P; }
+        return (size_t)(uint32_t)r * S + q;
+    }
     uint32_t *list;    // re-execution list (units)
     unsigned *list_count;
     uint32_t *fb_list; // pixels left to the sequential kernel after the last resolve
@@ -199,7 +214,12 @@ struct SpecRecs {
     uint32_t alt_cap = 0, alt_hcap = 0, alt_min_seg = 0;
     float alt_vals[8] = {};
     int n_alt_vals = 0;
+    uint32_t pmag = 0;  // ceil(2^32 / P) (spec_pmag): ix() divides a unit by P with one mulhi
 };
+// ceil(2^32 / P) for SpecRecs::pmag (P >= 2)
+inline uint32_t spec_pmag(uint32_t P) { return (uint32_t)(((1ull << 32) + P - 1) / P); }
+// the record index of unit u (SpecRecs::ix) by plain division (diagnostics, host reads)
+__host__ __device__ inline size_t spec_rec_ix(size_t u, uint32_t P, uint32_t S) { return (u % P) * S + u / P; }
 enum { kSpecFirst = 0, kSpecRest = 1, kSpecList = 2 };
 
 // Tail compaction between launches.  Once the work queue is empty, a wave whose busy lanes
@@ -324,9 +344,11 @@ size_t remap_workspace_bytes(int W, int H);
 hipError_t texture_remap(const uint8_t *d_in, int W, int H, int C, int load_as, uint8_t *d_out, void *d_ws,
                          hipStream_t s);
 hipError_t spec_hist(const uint4 *ctr, size_t n, unsigned long long *d_out, hipStream_t s);  // diagnostics
-hipError_t spec_list_stale(const uint4 *ctr, const uint32_t *list, const unsigned *count, unsigned long long *d_out,
+hipError_t spec_list_stale(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *list, const unsigned *count,
+                           unsigned long long *d_out,
                            hipStream_t s);  // diagnostics
-hipError_t spec_list_hist(const uint4 *ctr, const uint32_t *list, const unsigned *count, unsigned long long *d_out,
+hipError_t spec_list_hist(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *list, const unsigned *count,
+                          unsigned long long *d_out,
                           hipStream_t s);  // diagnostics
 hipError_t spec_pixels(const uint4 *ctr, uint32_t P, uint32_t S, const uint32_t *order, uint32_t *d_out,
                        hipStream_t s);  // diagnostics

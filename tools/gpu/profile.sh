@@ -1,15 +1,18 @@
 # Round-end evidence, part 2: the bench line of one config, rocprofv3 kernel trace of the same
 # command, and PMC passes (one counter group per pass), summed for the main kernel into
 # gpurun_out/prof_<cfg>/pmc_<cfg>.json (copy to profiles/ to make bench.py report roofline.traffic).
-#   gpurun -- 'bash tools/gpu/profile.sh c3'        (c3 | c2 | c5 | ns; STEPS=k for the bench line)
+#   gpurun -- 'bash tools/gpu/profile.sh c3'        (c3 | c2 | c5 | ns; STEPS=k for the bench line;
+#   BENCH_ARGS="--opt inw_qnodes=1" TAG=c3_gq: extra bench arguments, output under prof_<TAG>)
 set -o pipefail
 CFG=${1:-c3}
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp && cd "$R"
-O=gpurun_out/prof_$CFG
+TAG=${TAG:-$CFG}
+X=${BENCH_ARGS:-}
+O=gpurun_out/prof_$TAG
 rm -rf $O && mkdir -p $O
-timeout -k 10 500 python3 bench.py --config $CFG --steps ${STEPS:-10} > $O/bench.json 2> $O/bench.err || exit 1
-ARGS="--config $CFG --steps 1 --warmup 1 --no-cpu-baseline"
+timeout -k 10 500 python3 bench.py --config $CFG --steps ${STEPS:-10} $X > $O/bench.json 2> $O/bench.err || exit 1
+ARGS="--config $CFG --steps 1 --warmup 1 --no-cpu-baseline $X"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py $ARGS > $O/kt.log 2>&1 || exit 1
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
