@@ -246,6 +246,34 @@ __device__ __forceinline__ void cull4(const float4 lx, const float4 ly, const fl
     t2 = one(ax23.x, bx23.x, ay23.x, by23.x, az23.x, bz23.x);
     t3 = one(ax23.y, bx23.y, ay23.y, by23.y, az23.y, bz23.y);
 }
+// The same test with the planes already split into near and far by the ray's octant (the caller
+// loads plane a + 3 s_a as near and a + 3 (1 - s_a) as far, s_a = 1 when d_a < 0).  With a finite,
+// nonzero reciprocal the slab value (p - o) * (1/d) is monotone in p, so the near plane's value is
+// the min of the pair and the far plane's the max: te and tx have cull4's bits and the 12 min / max
+// per node are gone.  A zero component (1/d = inf) keeps at least the boxes cull4 keeps: the pair
+// form's fminf / fmaxf drop a NaN (origin on a plane) and then cull, the octant form keeps the box.
+// The culling BVH only decides which objects get the exact test (iow_launch_ray), so that is exact.
+__device__ __forceinline__ void cull4o(const float4 nx, const float4 ny, const float4 nz, const float4 fx,
+                                       const float4 fy, const float4 fz, f3 o, f3 id, float lim, float &t0,
+                                       float &t1, float &t2, float &t3) {
+    const pf2 ox = pk(o.x, o.x), oy = pk(o.y, o.y), oz = pk(o.z, o.z);
+    const pf2 ix = pk(id.x, id.x), iy = pk(id.y, id.y), iz = pk(id.z, id.z);
+    const pf2 ax01 = (pk(nx.x, nx.y) - ox) * ix, bx01 = (pk(fx.x, fx.y) - ox) * ix;
+    const pf2 ay01 = (pk(ny.x, ny.y) - oy) * iy, by01 = (pk(fy.x, fy.y) - oy) * iy;
+    const pf2 az01 = (pk(nz.x, nz.y) - oz) * iz, bz01 = (pk(fz.x, fz.y) - oz) * iz;
+    const pf2 ax23 = (pk(nx.z, nx.w) - ox) * ix, bx23 = (pk(fx.z, fx.w) - ox) * ix;
+    const pf2 ay23 = (pk(ny.z, ny.w) - oy) * iy, by23 = (pk(fy.z, fy.w) - oy) * iy;
+    const pf2 az23 = (pk(nz.z, nz.w) - oz) * iz, bz23 = (pk(fz.z, fz.w) - oz) * iz;
+    auto one = [&](float n0, float f0, float n1, float f1, float n2, float f2) {
+        const float te = fmaxf(fmaxf(n0, n1), n2);
+        const float tx = fminf(fminf(f0, f1), f2);
+        return (te <= tx && tx >= -1e-3f && te <= lim) ? te : kMiss;
+    };
+    t0 = one(ax01.x, bx01.x, ay01.x, by01.x, az01.x, bz01.x);
+    t1 = one(ax01.y, bx01.y, ay01.y, by01.y, az01.y, bz01.y);
+    t2 = one(ax23.x, bx23.x, ay23.x, by23.x, az23.x, bz23.x);
+    t3 = one(ax23.y, bx23.y, ay23.y, by23.y, az23.y, bz23.y);
+}
 __device__ __forceinline__ void cswap(float &ta, int &ka, float &tb, int &kb) {
     const bool sw = tb < ta;
     const float t = sw ? tb : ta;
@@ -392,6 +420,11 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
         // children), tests the four boxes, enters the nearest hit child and pushes the others
         // farthest-first.
         DBG_T0(F_, t_trav);
+#ifndef RT_IOW_NO_OCTANT
+        // the ray's near / far plane of each axis (cull4o): low planes are float4 0-2, high 3-5
+        const int nxo = gd.x < 0.0f ? 3 : 0, nyo = gd.y < 0.0f ? 4 : 1, nzo = gd.z < 0.0f ? 5 : 2;
+        const int fxo = 3 - nxo, fyo = 5 - nyo, fzo = 7 - nzo;
+#endif
         int sp = 0, pend = -1, cur = S.root_link;
         bool walking = true, ovf = false;  // ovf: a child was dropped by a full stack
         float lim = min_t * 1.0001f + 1e-3f;  // culling limit, follows min_t
@@ -401,11 +434,15 @@ __device__ RayRet iow_launch_ray(const IowScene &S, const Frame &F_, f3 go, f3 g
                 bool pop;
                 if (cur > 0) {
                     const float4 *nd = nodes + NS * (cur - 1);
-                    const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
                     const float4 lk = nd[6];  // child links as int bits (set_iow_bvh)
                     c.nodes += 4;
                     float t0, t1, t2, t3;
+#ifndef RT_IOW_NO_OCTANT
+                    cull4o(nd[nxo], nd[nyo], nd[nzo], nd[fxo], nd[fyo], nd[fzo], go, id, lim, t0, t1, t2, t3);
+#else
+                    const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
                     cull4(lx, ly, lz, hx, hy, hz, go, id, lim, t0, t1, t2, t3);
+#endif
                     int k0 = __float_as_int(lk.x), k1 = __float_as_int(lk.y), k2 = __float_as_int(lk.z),
                         k3 = __float_as_int(lk.w);
                     // sort (t, link) ascending; misses carry t = +inf
@@ -2291,6 +2328,32 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
     return (float)bg;
 }
 
+// Scalar loads of wave-uniform records (constant address space: s_load through the scalar cache,
+// no vector-memory / TA work): the beam lists' candidates are the same object for every active lane
+// of one pixel (they step through the list together)
+typedef float sv4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const sv4f csv4f;
+__device__ __forceinline__ float4 sload4(const float4 *p, int i) {
+    const sv4f v = ((const csv4f *)(const void *)p)[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ Xf load_xf_s(const InwScene &S, int g) {  // load_xf of a wave-uniform g
+    const float4 a = sload4(S.hot, 7 * g), b = sload4(S.hot, 7 * g + 1), c = sload4(S.hot, 7 * g + 2),
+                 d = sload4(S.hot, 7 * g + 3), e = sload4(S.hot, 7 * g + 4), f = sload4(S.hot, 7 * g + 5),
+                 q = sload4(S.hot, 7 * g + 6);
+    Xf x;
+    x.pos = mk(a.x, a.y, a.z);
+    x.R.c0 = mk(a.w, b.x, b.y); x.R.c1 = mk(b.z, b.w, c.x); x.R.c2 = mk(c.y, c.z, c.w);
+    x.scale = mk(d.x, d.y, d.z);
+    x.delta = mk(d.w, e.x, e.y);
+    x.type = (int)(e.z + 0.1f);
+    x.extra = e.w;
+    x.is = mk(f.x, f.y, f.z);
+    x.is2 = mk(f.w, q.x, q.y);
+    x.ri_acc = q.z;
+    return x;
+}
+
 // Closest hit of a primary ray from its pixel's beam list (DESIGN.md §5 "Pixel beams").  The list
 // holds every object whose culling box the beam of the pixel's primary rays can cross, in the
 // order of the central ray's entry t into the box inflated by beam_R; a sample ray hitting object
@@ -2341,8 +2404,22 @@ __device__ float inw_closest_beam(const InwScene &S, const KS &K, f3 o, f3 d, fl
             if (k + 1u < n) en = entry(k + 1u);
             const int g = (int)e.x;
             c.prims++;
-            const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
-            const Xf x = load_xf(S, g);
+            float4 n0, n1;
+            Xf x;
+#ifndef RT_INW_BEAM_VLOAD
+            // one candidate for every active lane (a wave's lanes trace samples of one pixel and step
+            // through its list together): scalar loads, C3 184.7 -> 182.5 ms
+            // (profiles/r06_ab_beam_sload_ring_il.json; -DRT_INW_BEAM_VLOAD: vector loads only)
+            const int g0 = __builtin_amdgcn_readfirstlane(g);
+            if (__ballot(g != g0) == 0ull) {
+                n0 = sload4(S.leafbox, 2 * g0); n1 = sload4(S.leafbox, 2 * g0 + 1);
+                x = load_xf_s(S, g0);
+            } else
+#endif
+            {
+                n0 = S.leafbox[2 * g]; n1 = S.leafbox[2 * g + 1];
+                x = load_xf(S, g);
+            }
             float te;
             const bool inb = test_aabb_te(n0, n1, o, id, tlim0, te);
             f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
@@ -3300,6 +3377,15 @@ __global__ __launch_bounds__(kBlock) void k_inw_order_scatter(const uint32_t *ke
 #ifndef RT_GQ_STAGE
 #define RT_GQ_STAGE 1
 #endif
+// k_inw_pm's LDS fold ring: channel c of entry e.  Planes (r, g, b of 256 entries each): the fold's
+// lanes 0, 1, 2 read one plane each at the same entry, addresses 1 KB apart, one bank: a 3-way
+// conflict per read.  RT_RING_IL interleaves the channels (3 e + c): the three lanes hit 3 banks,
+// but C3 ran 0.5% slower (185.7 against 184.7 ms, profiles/r06_ab_beam_sload_ring_il.json).
+#ifdef RT_RING_IL
+#define RIX(c, e) (3u * (e) + (c))
+#else
+#define RIX(c, e) ((c) * kPmLdsRing + (e))
+#endif
 #ifndef RT_INW_R1_MIN
 #define RT_INW_R1_MIN 0
 #endif
@@ -3433,7 +3519,7 @@ __global__ __launch_bounds__((pm_sub<LN, GQ>() * kBlock)) __attribute__((amdgpu_
                 if (n > 64u) n = 64u;
                 if (lane < n) {
                     const uint32_t e = k & rmask;
-                    v = make_float4(lr[e], lr[kPmLdsRing + e], lr[2u * kPmLdsRing + e], 0.0f);
+                    v = make_float4(lr[RIX(0u, e)], lr[RIX(1u, e)], lr[RIX(2u, e)], 0.0f);
                 }
             } else {
                 __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's ring stores have landed (same CU: L1 write-through)
@@ -3450,21 +3536,21 @@ __global__ __launch_bounds__((pm_sub<LN, GQ>() * kBlock)) __attribute__((amdgpu_
                 // LDS ring: lanes 0, 1, 2 add the r, g, b planes' entries straight from LDS, each
                 // its channel in sample order (the same float additions, two instructions per entry
                 // instead of three readlanes and three adds); the run splits at pixel ends
-                const float *pl = lr + (lane < 3u ? lane : 0u) * kPmLdsRing;
+                const uint32_t lc = lane < 3u ? lane : 0u;  // this lane's channel
                 for (uint32_t i = 0; i < n;) {
                     const uint32_t e = i + (n - i < spp - sf ? n - i : spp - sf);
                     if (lane < 3u) {
                         uint32_t j = i;
-                        if (sf == 0) { accc = pl[(gf + j) & rmask]; j++; }
+                        if (sf == 0) { accc = lr[RIX(lc, (gf + j) & rmask)]; j++; }
                         constexpr uint32_t kFU = 4;  // loads in flight, then the adds in order (8, 16: same time)
                         for (; j + kFU <= e; j += kFU) {
                             float a[kFU];
 #pragma unroll
-                            for (uint32_t u = 0; u < kFU; u++) a[u] = pl[(gf + j + u) & rmask];
+                            for (uint32_t u = 0; u < kFU; u++) a[u] = lr[RIX(lc, (gf + j + u) & rmask)];
 #pragma unroll
                             for (uint32_t u = 0; u < kFU; u++) accc = accc + a[u];
                         }
-                        for (; j < e; j++) accc = accc + pl[(gf + j) & rmask];
+                        for (; j < e; j++) accc = accc + lr[RIX(lc, (gf + j) & rmask)];
                     }
                     sf += e - i;
                     i = e;
@@ -3601,7 +3687,7 @@ __global__ __launch_bounds__((pm_sub<LN, GQ>() * kBlock)) __attribute__((amdgpu_
                         if ((uint32_t)s == mid) pdep[pj] = 0.0f;
                         if constexpr (LR) {
                             const uint32_t e = g & rmask;
-                            lr[e] = 0.0f; lr[kPmLdsRing + e] = 0.0f; lr[2u * kPmLdsRing + e] = 0.0f;
+                            lr[RIX(0u, e)] = 0.0f; lr[RIX(1u, e)] = 0.0f; lr[RIX(2u, e)] = 0.0f;
                         } else {
                             wr[g & rmask] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(ring_tag(S, g)));
                         }
@@ -3638,9 +3724,9 @@ __global__ __launch_bounds__((pm_sub<LN, GQ>() * kBlock)) __attribute__((amdgpu_
             if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
                 if constexpr (LR) {
                     const uint32_t e = g & rmask;
-                    lr[e] = __builtin_sqrtf(col.x);
-                    lr[kPmLdsRing + e] = __builtin_sqrtf(col.y);
-                    lr[2u * kPmLdsRing + e] = __builtin_sqrtf(col.z);
+                    lr[RIX(0u, e)] = __builtin_sqrtf(col.x);
+                    lr[RIX(1u, e)] = __builtin_sqrtf(col.y);
+                    lr[RIX(2u, e)] = __builtin_sqrtf(col.z);
                 } else {
                     wr[g & rmask] = make_float4(__builtin_sqrtf(col.x), __builtin_sqrtf(col.y), __builtin_sqrtf(col.z),
                                                 __uint_as_float(ring_tag(S, g)));
