@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* status codes */
 #define RT_OK            0
@@ -130,6 +130,13 @@ typedef struct rt_options {
                                top ray in registers, the wide walk's node stack and the top of the culling
                                BVH in LDS (quantised 64-B nodes, 1,168 of them); 0 (default, measured faster):
                                the FStack instance */
+    int inw_time_bins;      /* moving objects: the wide walk culls with one of this many extra culling trees,
+                               each over the boxes the objects sweep in its share of the shutter interval
+                               (the ray's time ratio picks it; DESIGN.md §5.2 "Time-binned culling trees");
+                               0 or 1: the swept tree only.  Default 2 (4 and 8 measured slower: their trees crowd
+                               the L2); scenes built on the host */
+    int inw_walk_bins;      /* 1 (default): the wide closest-hit walks use the time-bin trees */
+    int inw_beam_bins;      /* 1 (default): a pixel's beam lists per time bin, from the time-bin trees */
     /* IOW-03 (In-One-Weekend 03) */
     int iow_spec;           /* sample-parallel speculation (0: the sequential per-pixel kernel) */
     int iow_linear;         /* [build] the shader's linear object loop instead of the culling BVH */
@@ -333,6 +340,9 @@ typedef struct rt_path_info {
     int walk_stack;       /* entries of the wide walks' own node stack per lane (LDS) */
     uint64_t ref_walks;   /* INW: the last frame's closest-hit queries (segments + shadow rays) that the wide
                              walk or beam list handed to the reference's LBVH walks (stackless or stack) */
+    int time_bins;        /* INW: time-bin culling trees the wide closest-hit walks chose from (0: the swept
+                             tree; inw_time_bins, moving objects, walks that read no LDS-staged nodes) */
+    int beam_bins;        /* INW: beam lists per pixel (one per time bin; 0: one list over the swept boxes) */
 } rt_path_info;
 int rt_debug_path(rt_dev_scene *s, rt_path_info *out);
 

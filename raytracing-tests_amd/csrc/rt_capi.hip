@@ -33,7 +33,8 @@ rt_options default_options() {
     o.size = sizeof(rt_options);
     o.inw_wide_walk = 1; o.inw_order = 0; o.inw_beams = 1; o.inw_ri_grid = 1; o.inw_lds_nodes = 1;
     o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 0; o.inw_ring_sm = 0; o.inw_stackless = 1;
-    o.inw_device_build = 1; o.inw_claim_xcd = 1; o.inw_qnodes = 0;
+    o.inw_device_build = 1; o.inw_claim_xcd = 1; o.inw_qnodes = 0; o.inw_time_bins = 2;
+    o.inw_walk_bins = 1; o.inw_beam_bins = 1;
     o.iow_spec = 1; o.iow_linear = 0; o.iow_narrow = 0; o.iow_lds_bvh = 1;
     o.iow_leaf_batch = 32;  // 32 measured 2.5% faster on the bench frame than 65 (round 2)
     o.iow_coop_max = 4; o.iow_chunks_lpt = 0;
@@ -52,7 +53,8 @@ bool options_ok(const rt_options *o) {
            o->park_min >= -1 && o->spec_iters >= 0 && o->spec_probe >= 1 && o->spec_heavy >= -1 &&
            o->spec_rounds >= 0 && o->spec_tail_rounds >= 0 && o->spec_tail_budget >= 1 && o->spec_scan >= 0 &&
            o->spec_alt_cap >= 1024 && o->spec_alt_cap <= (1 << 24) && o->spec_alt_seg >= 0 && o->spec_alt_every >= 0 &&
-           o->spec_prior_from >= 1 && o->spec_solo >= 0 && o->spec_max_gb > 0.0;
+           o->spec_prior_from >= 1 && o->spec_solo >= 0 && o->spec_max_gb > 0.0 && o->inw_time_bins >= 0 &&
+           o->inw_time_bins <= 16;
 }
 rt_options g_opt = default_options();
 unsigned *g_px_rays = nullptr;        // rt_debug_pixel_rays(): rays per work unit
@@ -180,7 +182,9 @@ struct rt_dev_scene {
     float ri_lo[3] = {}, ri_hi[3] = {}, ri_inv[3] = {};
     int ri_dim[3] = {};
     int wdepth = 0;               // levels of the 4-wide culling BVH
-    uint32_t n_wnodes = 0;        // its nodes
+    uint32_t n_wnodes = 0;        // its nodes (every tree)
+    uint32_t n_wtree0 = 0;        // ... of the tree over the swept boxes (the first ones)
+    uint32_t wbins = 1, wbin_stride = 0;  // time-bin trees after it (rtamd::InwWide::bins)
     bool ri_ok = false;           // the RI grid applies (ri_cells / ri_ids hold it)
     DevBuf lbvh_ws, aabb, lcnt;   // rt_dev_scene_inw_update: device LBVH workspace, object boxes, leaf counts
     DevBuf build_ws, ri_fill, ri_tmp;  // ... and the device build of the wide walk and RI grid (rt_build.hip)
@@ -363,6 +367,10 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     if (!s->n_wnodes) return;  // no wide walk
     sc.wnodes = s->wnodes.as<float4>();
     sc.wroot = 1;
+    if (s->wbins > 1 && s->opt.inw_time_bins > 1) {  // (built at scene creation; 0 / 1 later: unused)
+        sc.wbin_base = s->n_wtree0; sc.wbin_stride = s->wbin_stride;
+        if (s->opt.inw_walk_bins) sc.wbins = s->wbins;  // the wide closest-hit walks (set_beam: the beam lists)
+    }
     sc.rank = s->wrank.as<uint32_t>();
     sc.leafbox = s->wleaf.as<float4>();
     sc.dfs_high = s->dfs_high;
@@ -391,10 +399,13 @@ int make_qnodes(rt_dev_scene *s) {
 // The wide walk's structures and the RI grid, built on the host (rtamd::inw_wide_build,
 // rtamd::ri_grid_build) and uploaded.
 // ms (may be null): host time of the builds, then of the uploads
-int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n, double *ms = nullptr) {
+// geom (may be null): the reference's GeometryBuff records, for the time-bin trees
+int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n, double *ms = nullptr, const float *geom = nullptr) {
     s->dfs_high = 0;
     s->sl_ok = false;
-    s->n_wnodes = 0;
+    s->n_wnodes = s->n_wtree0 = 0;
+    s->wbins = 1;
+    s->wbin_stride = 0;
     s->ri_ok = false;
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t high = 0;
@@ -404,6 +415,7 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n, double *ms = 
     rtamd::RiGrid g;
     const bool ok = walkable && s->opt.inw_wide_walk && rtamd::inw_wide_build(nodes, n, w);
     if (ok) g = rtamd::ri_grid_build(w.leafbox.data(), n);
+    if (ok && geom && s->opt.inw_time_bins > 1) rtamd::inw_wide_add_bins(geom, n, uint32_t(s->opt.inw_time_bins), w);
     const auto t1 = std::chrono::steady_clock::now();
     if (ms) ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (!ok) {  // the reference walk only (stackless where it cannot drop a push)
@@ -422,6 +434,9 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n, double *ms = 
         }
     }
     s->n_wnodes = uint32_t(w.wnodes.size() / 40);
+    s->n_wtree0 = w.n_tree0;
+    s->wbins = w.bins;
+    s->wbin_stride = w.bin_stride;
     s->dfs_high = w.dfs_high;
     s->sl_ok = sl;
     s->wdepth = w.depth;
@@ -470,7 +485,7 @@ int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const f
     HIP_OK(s->hot.store(hot.data(), hot.size() * sizeof(float)));
     HIP_OK(s->cold.store(cold.data(), cold.size() * sizeof(float)));
     HIP_OK(s->nodes.store(nodes, size_t(2 * n - 1) * 8 * sizeof(float)));
-    if (int rc = make_inw_wide(s, nodes, n); rc != RT_OK) return rc;
+    if (int rc = make_inw_wide(s, nodes, n, nullptr, geom); rc != RT_OK) return rc;
     if (s->n_lights) HIP_OK(s->lights.store(lights, size_t(s->n_lights) * 7 * sizeof(float)));
     else HIP_OK(s->lights.store(nullptr, 0));
     set_residency(s);
@@ -483,7 +498,9 @@ int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const f
 int make_inw_wide_device(rt_dev_scene *s, uint32_t n, double *ms) {
     s->dfs_high = 0;
     s->sl_ok = false;
-    s->n_wnodes = 0;
+    s->n_wnodes = s->n_wtree0 = 0;
+    s->wbins = 1;
+    s->wbin_stride = 0;
     s->ri_ok = false;
     const auto t0 = std::chrono::steady_clock::now();
     HIP_OK(s->wnodes.reserve(size_t(n) * 40 * sizeof(float)));
@@ -522,7 +539,7 @@ int make_inw_wide_device(rt_dev_scene *s, uint32_t n, double *ms) {
                 s->ri_ok = true;
             }
         }
-        s->n_wnodes = out.n_wnodes;
+        s->n_wnodes = s->n_wtree0 = out.n_wnodes;
         s->wdepth = out.depth;
         s->wbound = out.wbound;
         if (int rc = make_qnodes(s); rc != RT_OK) return rc;
@@ -598,12 +615,12 @@ int update_inw(rt_dev_scene *s, const float *geom, uint32_t n, const float *node
             // device LBVH back and build the walk structures there, as rt_dev_scene_inw does
             host_nodes.resize(nbytes / sizeof(float));
             HIP_OK(hipMemcpy(host_nodes.data(), s->nodes.p, nbytes, hipMemcpyDeviceToHost));
-            rc = make_inw_wide(s, host_nodes.data(), n, w);
+            rc = make_inw_wide(s, host_nodes.data(), n, w, geom);
             s->wbuild = 2;
         }
         if (rc != RT_OK) return rc;
     } else {
-        if (int rc = make_inw_wide(s, nodes, n, w); rc != RT_OK) return rc;
+        if (int rc = make_inw_wide(s, nodes, n, w, geom); rc != RT_OK) return rc;
         s->wbuild = 0;
     }
     if (ms) { ms[2] = w[0]; ms[3] = w[1]; }
@@ -1232,7 +1249,7 @@ int set_beam(rt_dev_scene *s, const rtk::Frame &f, rtk::InwScene &sc) {
     const double ap = std::fabs(double(f.aperture)), L = double(f.focus) - 1.0;
     const double d0 = 0.5 * ap * double(s->sf_max) * (1.0 + 1e-4) + 1e-6;
     if (!s->opt.inw_beams || !sc.wnodes || f.n_focus > 0 || !(L > 8.0 * d0 + 1e-3) ||
-        units * cap * 8.0 > 2.0e9)
+        units * cap * 8.0 * std::max<uint32_t>(1u, s->wbins) > 8.0e9)  // list capacity; each list is packed
         return RT_OK;
     const double cam = std::sqrt(double(f.pos[0]) * f.pos[0] + double(f.pos[1]) * f.pos[1] + double(f.pos[2]) * f.pos[2]);
     const double Lh = L + 1e-3 * (1.0 + cam), Ll = L - 1e-3 * (1.0 + cam);
@@ -1244,8 +1261,10 @@ int set_beam(rt_dev_scene *s, const rtk::Frame &f, rtk::InwScene &sc) {
     const double R = r + 2e-3 + 1e-5 * (cam + tfar);
     // object ids below 2^16: one uint32 per entry (the id, t's high half), else (id, t)
     const bool b16 = s->n <= 65536u && s->opt.inw_beams != 2;  // inw_beams = 2: the pairs (A/B)
-    const size_t need = size_t(units) * cap * (b16 ? sizeof(uint32_t) : sizeof(uint2)),
-                 need_n = size_t(units) * 2 * sizeof(uint32_t);
+    // one list per unit and time bin when the scene has time-bin trees (rt_options.inw_time_bins)
+    const uint32_t nb = s->wbins > 1 && s->opt.inw_time_bins > 1 && s->opt.inw_beam_bins ? s->wbins : 1u;
+    const size_t need = size_t(units) * nb * cap * (b16 ? sizeof(uint32_t) : sizeof(uint2)),
+                 need_n = size_t(units) * nb * 2 * sizeof(uint32_t);
     // the lists are an optional speed-up: on a device short of memory the frame runs without them
     size_t free_b = 0, total_b = 0;
     const size_t grow = (s->inw_beam.bytes < need ? need : 0) + (s->inw_beam_n.bytes < need_n ? need_n : 0);
@@ -1262,8 +1281,11 @@ int set_beam(rt_dev_scene *s, const rtk::Frame &f, rtk::InwScene &sc) {
     }
     sc.beam = s->inw_beam.as<uint2>();
     sc.beam_n = s->inw_beam_n.as<uint32_t>();
-    sc.beam_cut = reinterpret_cast<const float *>(s->inw_beam_n.as<uint32_t>() + size_t(units));
+    sc.beam_cut = reinterpret_cast<const float *>(s->inw_beam_n.as<uint32_t>() + size_t(units) * nb);
     sc.beam_cap = cap;
+    sc.beam_bins = nb > 1 ? nb : 0u;
+    sc.beam_units = uint32_t(units);
+    if (nb > 1) { sc.wbin_base = s->n_wtree0; sc.wbin_stride = s->wbin_stride; }
     sc.beam16 = b16 ? 1u : 0u;
     sc.beam_R = float(R);
     sc.beam_tmin = float(tmin);
@@ -1293,7 +1315,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
     // inw_ring_sm = 0: k_inw_sm's ring in LDS too when the staging keeps every node it would stage
     // anyway (a BVH top of at most kPmLdsNodes wide nodes: INW-04's rooms), else a global ring of
     // 256 entries; a power of two: the global ring of that size
-    const bool fits5 = s->n_wnodes ? s->n_wnodes <= rtk::kPmLdsNodes
+    const bool fits5 = s->n_wnodes ? s->n_wtree0 <= rtk::kPmLdsNodes
                                    : (s->sl_ok && 2 * size_t(s->n) - 1 <= size_t(rtk::kPmLdsNodes) * 10 / 2);
     const bool lring_sm = o.inw_ring_sm == 0 && blocks_ln > 0 && fits5;
     const uint32_t ring_sm = lring_sm ? rtk::kPmLdsRing : uint32_t(o.inw_ring_sm ? o.inw_ring_sm : 256);
@@ -1399,7 +1421,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         P.beams = sc.beam != nullptr;
         P.ri_grid = sc.ri_cells != nullptr;
         P.fused_cull = s->last_fu && sc.wnodes ? 1 : 0;  // the fused cull is the wide walk's
-        P.lds_nodes = s->last_ln ? int(std::min<uint32_t>(s->n_wnodes, uint32_t(rtk::kInwLdsNodes))) : 0;
+        P.lds_nodes = s->last_ln ? int(std::min<uint32_t>(s->n_wtree0, uint32_t(rtk::kInwLdsNodes))) : 0;
         P.stackless = sc.sl ? 1 : 0;
         // the LBVH nodes the stackless walks read from LDS (LN kernels without the wide walk)
         P.lbvh_lds_nodes = s->last_ln && sc.sl && !sc.wnodes
@@ -1409,7 +1431,9 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
         P.global_stack = sc.gstk != nullptr;
         P.walk_stack = sc.gstk ? rtk::kWStack : rtk::kFStack - 3;
         if (sc.gstk)
-            P.lds_nodes = int(std::min<uint32_t>(s->n_wnodes, uint32_t(rtk::kGqQn ? rtk::kQLdsNodes : rtk::kInwLdsNodes)));
+            P.lds_nodes = int(std::min<uint32_t>(s->n_wtree0, uint32_t(rtk::kGqQn ? rtk::kQLdsNodes : rtk::kInwLdsNodes)));
+        P.time_bins = sc.wnodes && !sc.gstk ? int(sc.wbins) : 0;  // the GQ walks read the staged (swept) tree
+        P.beam_bins = sc.beam ? int(sc.beam_bins) : 0;
     }
     if (epoch == 0) e = hipMemsetAsync(s->inw_ring.p, 0xff, s->inw_ring.bytes, st);
     if (e == hipSuccess) s->ring_frame = epoch + 1;
@@ -1606,7 +1630,7 @@ int rt_debug_wide_info(rt_dev_scene *s, uint32_t info[8], uint32_t *rank_out) {
     HIP_OK(hipSetDevice(s->device));
     HIP_OK(hipDeviceSynchronize());
     const uint32_t cells = s->ri_ok ? uint32_t(s->ri_dim[0]) * uint32_t(s->ri_dim[1]) * uint32_t(s->ri_dim[2]) : 0u;
-    const uint32_t v[8] = {s->n_wnodes, s->dfs_high, uint32_t(s->wdepth), s->ri_ok ? 1u : 0u, cells,
+    const uint32_t v[8] = {s->n_wtree0, s->dfs_high, uint32_t(s->wdepth), s->ri_ok ? 1u : 0u, cells,
                            s->sl_ok ? 1u : 0u, s->n, s->wbuild};
     std::memcpy(info, v, sizeof(v));
     if (rank_out && s->n_wnodes)
@@ -1633,6 +1657,7 @@ int rt_debug_path(rt_dev_scene *s, rt_path_info *out) {
         P.ring_entries = int(s->last_ring[0]);
         P.ring_lds = s->last_lring ? 1 : 0;
         if (s->last_lring && !s->last_gq) { P.lds_nodes = 0; P.lbvh_lds_nodes = 0; }  // the FStack ring instances stage no nodes
+        if (s->last_ln && !s->last_lring) P.time_bins = 0;  // the global-ring LN instance walks the staged swept tree
     }
     else if (std::strncmp(name, "k_inw_sm", 8) == 0) {
         P.order = 2;
@@ -1640,12 +1665,13 @@ int rt_debug_path(rt_dev_scene *s, rt_path_info *out) {
         P.ring_lds = s->last_lring_sm ? 1 : 0;
         if (s->last_lring_sm) P.lds_nodes = std::min(P.lds_nodes, int(rtk::kPmLdsNodes));
         if (s->last_lring_sm) P.lbvh_lds_nodes = std::min(P.lbvh_lds_nodes, int(rtk::kPmLdsNodes * 10 / 2));
+        if (s->last_ln) P.time_bins = 0;  // its walks read the staged top of the swept tree
         if (s->last_gq) {  // the GQ instance is pixel-major only: k_inw_sm ran the 236-node FStack kernel
             P.qnodes = 0; P.global_stack = 0; P.walk_stack = rtk::kFStack - 3;
-            P.lds_nodes = s->last_lring_sm ? std::min(s->n_wnodes, rtk::kPmLdsNodes) : std::min(s->n_wnodes, uint32_t(rtk::kInwLdsNodes));
+            P.lds_nodes = s->last_lring_sm ? std::min(s->n_wtree0, rtk::kPmLdsNodes) : std::min(s->n_wtree0, uint32_t(rtk::kInwLdsNodes));
         }
     }
-    if (P.order != 1) { P.beams = 0; P.claim_order = 0; }  // both serve the pixel-major kernel only
+    if (P.order != 1) { P.beams = 0; P.claim_order = 0; P.beam_bins = 0; }  // both serve the pixel-major kernel only
     *out = P;
     return RT_OK;
 }

@@ -733,6 +733,27 @@ bool iow_cull_build(const float *types, const float *rec, uint32_t n, IowCull &o
     return true;
 }
 
+// A 4-wide culling tree over `boxes` (6 floats each) appended to `out` as 10 float4 per node: lx ly
+// lz hx hy hz lx ly lz, child links as int bits; node links are rebased by `base` (the index of
+// the tree's first node in the whole array), empty slots keep their far-away link.  Returns nodes.
+static size_t wide_tree(const float *boxes, uint32_t n, size_t base, std::vector<float> &out, int *depth4) {
+    int depth = 0;
+    const std::vector<float> wide = bvh4_collapse(sah_build(boxes, n, &depth), depth4);
+    const size_t nw = wide.size() / 32, o0 = out.size();
+    out.resize(o0 + nw * 40, 0.0f);
+    for (size_t w = 0; w < nw; w++) {
+        float *o = &out[o0 + w * 40];
+        std::memcpy(o, &wide[w * 32], 24 * sizeof(float));
+        std::memcpy(o + 24, &wide[w * 32], 12 * sizeof(float));
+        for (int k = 0; k < 4; k++) {
+            int link = int(wide[w * 32 + 24 + size_t(k)]);
+            if (link > 0 && size_t(link) <= nw) link += int(base);
+            std::memcpy(o + 36 + k, &link, sizeof(link));
+        }
+    }
+    return nw;
+}
+
 bool inw_wide_build(const float *nodes, uint32_t n, InwWide &out) {
     if (n < 2) return false;
     const uint32_t nn = 2 * n - 1;
@@ -786,24 +807,103 @@ bool inw_wide_build(const float *nodes, uint32_t n, InwWide &out) {
             wbound = std::fmax(wbound, std::fmax(std::fabs(b[k] - e), std::fabs(b[3 + k] + e)));
         }
     }
-    int depth = 0, depth4 = 0;
-    const std::vector<float> wide = bvh4_collapse(sah_build(boxes.data(), n, &depth), &depth4);
-    // 10 float4 per node: lx ly lz hx hy hz lx ly lz, child links as int bits
-    const size_t nw = wide.size() / 32;
-    out.wnodes.assign(nw * 40, 0.0f);
-    for (size_t w = 0; w < nw; w++) {
-        std::memcpy(&out.wnodes[w * 40], &wide[w * 32], 24 * sizeof(float));
-        std::memcpy(&out.wnodes[w * 40 + 24], &wide[w * 32], 12 * sizeof(float));
-        for (int k = 0; k < 4; k++) {
-            const int link = int(wide[w * 32 + 24 + size_t(k)]);
-            std::memcpy(&out.wnodes[w * 40 + 36 + size_t(k)], &link, sizeof(link));
-        }
-    }
+    int depth4 = 0;
+    out.wnodes.clear();
+    wide_tree(boxes.data(), n, 0, out.wnodes, &depth4);
+    out.n_tree0 = uint32_t(out.wnodes.size() / 40);
+    out.bins = 1;
+    out.bin_stride = 0;
     out.leafbox.assign(size_t(n) * 8, 0.0f);
     for (uint32_t g = 0; g < n; g++) std::memcpy(&out.leafbox[size_t(g) * 8], nodes + size_t(leaf[g]) * 8, 8 * sizeof(float));
     out.dfs_high = high;
     out.depth = depth4;
     out.wbound = wbound;
+    return true;
+}
+
+// Time-bin trees.  Object g's centre at time ratio r is p - delta (1 - r) (the kernels' object
+// offset (o - p) + delta (1 - r), 01_BVH...glsl), so over [r0, r1] it sweeps the segment between
+// its centres at r0 and r1; its box there is that segment's box widened by the object's own half
+// extent, sqrt(sum_c (M_ic s_c)^2) under either orientation convention of the rotation M (the
+// ellipsoid's exact extent, and above a cuboid's), inflated as the swept culling boxes are.  A ray
+// that hits the object at a time in the bin hits it inside that box, so culling with it is as
+// conservative as with the swept box (the tree only decides which leaves get the
+// exact test).
+bool inw_wide_add_bins(const float *geom, uint32_t n, uint32_t bins, InwWide &w) {
+    if (bins < 2 || bins > 16 || n < 2 || w.wnodes.empty() || w.bins != 1) return false;
+    bool moving = false;
+    for (uint32_t g = 0; g < n && !moving; g++)
+        for (int a = 0; a < 3; a++) moving = moving || geom[size_t(g) * 28 + 15 + a] != 0.0f;
+    if (!moving) return false;
+    std::vector<float> ext(size_t(n) * 3);
+    for (uint32_t g = 0; g < n; g++) {
+        const float *f = geom + size_t(g) * 28;
+        for (int i = 0; i < 3; i++) {
+            double row = 0.0, col = 0.0;
+            for (int c = 0; c < 3; c++) {
+                const double a = double(f[3 + 3 * i + c]) * f[12 + c], b = double(f[3 + 3 * c + i]) * f[12 + c];
+                row += a * a;
+                col += b * b;
+            }
+            const double e = std::sqrt(std::fmax(row, col));
+            if (!std::isfinite(e)) return false;
+            ext[size_t(g) * 3 + i] = float(e);
+        }
+    }
+    std::vector<std::vector<float>> trees(bins);
+    size_t stride = 0;
+    std::vector<float> boxes(size_t(n) * 6);
+    for (uint32_t b = 0; b < bins; b++) {
+        const double r0 = double(b) / bins, r1 = double(b + 1) / bins;
+        for (uint32_t g = 0; g < n; g++) {
+            const float *f = geom + size_t(g) * 28;
+            float big = 0.0f;
+            double lo[3], hi[3];
+            for (int a = 0; a < 3; a++) {
+                const double c0 = double(f[a]) - double(f[15 + a]) * (1.0 - r0);
+                const double c1 = double(f[a]) - double(f[15 + a]) * (1.0 - r1);
+                lo[a] = std::fmin(c0, c1) - ext[size_t(g) * 3 + a];
+                hi[a] = std::fmax(c0, c1) + ext[size_t(g) * 3 + a];
+                big = std::fmax(big, float(std::fmax(std::fabs(lo[a]), std::fabs(hi[a]))));
+            }
+            for (int a = 0; a < 3; a++) {
+                const double e = (hi[a] - lo[a]) * 1e-3 + 1e-3 + double(big) * 1e-5;
+                // rounded outward to float
+                float l = float(lo[a] - e), h = float(hi[a] + e);
+                if (double(l) > lo[a] - e) l = std::nextafter(l, -INFINITY);
+                if (double(h) < hi[a] + e) h = std::nextafter(h, INFINITY);
+                boxes[size_t(g) * 6 + a] = l;
+                boxes[size_t(g) * 6 + 3 + a] = h;
+                w.wbound = std::fmax(w.wbound, std::fmax(std::fabs(l), std::fabs(h)));
+            }
+        }
+        int d4 = 0;
+        const size_t nw = wide_tree(boxes.data(), n, 0, trees[b], &d4);
+        stride = std::max(stride, nw);
+    }
+    // concatenate: tree b's first node at n_tree0 + b * stride (links rebased), padding nodes empty
+    const size_t n0 = w.wnodes.size() / 40;
+    w.wnodes.resize((n0 + bins * stride) * 40, 0.0f);
+    for (uint32_t b = 0; b < bins; b++) {
+        const size_t base = n0 + b * stride, nw = trees[b].size() / 40;
+        float *o = &w.wnodes[base * 40];
+        std::memcpy(o, trees[b].data(), trees[b].size() * sizeof(float));
+        for (size_t k = 0; k < nw; k++)
+            for (int j = 0; j < 4; j++) {
+                int link;
+                std::memcpy(&link, o + k * 40 + 36 + j, sizeof(link));
+                if (link > 0 && size_t(link) <= nw) link += int(base);
+                std::memcpy(o + k * 40 + 36 + j, &link, sizeof(link));
+            }
+        for (size_t k = nw; k < stride; k++) {  // padding: empty slots only
+            float *p = o + k * 40;
+            for (int j = 0; j < 36; j++) p[j] = 1e30f;
+            const int link = 1000000000;
+            for (int j = 0; j < 4; j++) std::memcpy(p + 36 + j, &link, sizeof(link));
+        }
+    }
+    w.bins = bins;
+    w.bin_stride = uint32_t(stride);
     return true;
 }
 

@@ -130,8 +130,17 @@ struct InwWide {
     std::vector<float> wnodes;     // 40 floats per node
     std::vector<uint32_t> rank;    // 2n: rank[inv * n + g]
     std::vector<float> leafbox;    // 8n: object g's LBVH leaf node
+    // Shutter-time bins (DESIGN.md §5.2 "Time-binned culling trees"): after the tree over the swept
+    // boxes (n_tree0 nodes) come `bins` trees of bin_stride nodes each (padded), tree b over the
+    // boxes the objects sweep while the ray time ratio lies in [b / bins, (b + 1) / bins]; their
+    // links are rebased to the concatenated array.  bins = 1: the swept tree only.
+    uint32_t n_tree0 = 0, bins = 1, bin_stride = 0;
 };
 bool inw_wide_build(const float *nodes, uint32_t n, InwWide &out);
+// Append the time-bin trees to a built InwWide from the reference's GeometryBuff records (28
+// floats: position, rotation, scale, position - last_position at 15..17).  false (nothing
+// appended): bins < 2, no object moves, or the records are malformed.
+bool inw_wide_add_bins(const float *geom, uint32_t n, uint32_t bins, InwWide &w);
 // The reference walk's stack high-water mark over both child orders (high; its pushes can only
 // drop while size + high > 40) and whether the node buffer has the layout the stackless LBVH walks
 // rely on (stackless: every internal node's children at L (odd), L + 1 with rightData = the node,

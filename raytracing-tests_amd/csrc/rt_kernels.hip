@@ -61,6 +61,7 @@ struct Ctr {
     unsigned long long *wdbg = nullptr;  // diagnostics: this wave's kDbg* row in LDS, or null
 #ifdef RT_DIAG_SPLIT
     unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // INW phase cycles of this wave (k_inw_pm/sm)
+    unsigned long long rnd[2] = {0, 0};  // k_inw_pm: wave cycles of the primary (0) and bounce (1) rounds
 #endif
 #ifdef RT_DIAG_OCC
     unsigned long long occ[kOccSlots] = {};  // INW lane occupancy per phase (OCC_TALLY), wave-uniform
@@ -2199,6 +2200,10 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
     const __amdgpu_buffer_rsrc_t wrs = wnode_rsrc(S);
 #endif
     int sp = 0, pend = -1, cur = S.wroot;
+    if (!LN && S.wbins > 1u) {  // the ray's time-bin tree (the staged nodes are the swept tree's)
+        const int b = min((int)(ratio * (float)S.wbins), (int)S.wbins - 1);
+        cur = 1 + (int)S.wbin_base + b * (int)S.wbin_stride;
+    }
     bool walking = ok, ovf = false;
     float lim = bt * 1.0001f + 1e-3f;
     if constexpr (PK) {
@@ -2366,7 +2371,9 @@ template <bool WANT_NORMAL, class KS = FStack>
 __device__ float inw_closest_beam(const InwScene &S, const KS &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
                                   f3 &normal, float &extra, float init_geom, Ctr &c, uint32_t unit, bool &ok) {
     const f3 id = f3{rcp(d.x), rcp(d.y), rcp(d.z)};  // the reference's reciprocals (test_aabb)
-    const uint32_t nw = S.beam_n[unit], n = nw & 0xffu;  // k_inw_beam: offset in the block's region << 8 | count
+    // the ray's time bin's list (beam_bins > 1): bin b's counts, cuts and lists after those of bins < b
+    const uint32_t bo = S.beam_bins > 1u ? min((uint32_t)(ratio * (float)S.beam_bins), S.beam_bins - 1u) * S.beam_units : 0u;
+    const uint32_t nw = S.beam_n[bo + unit], n = nw & 0xffu;  // k_inw_beam: offset in the block's region << 8 | count
     ok = nw != kBeamOff && K.size + S.dfs_high <= (uint32_t)kFStack && __builtin_isfinite(id.x) &&
          __builtin_isfinite(id.y) && __builtin_isfinite(id.z) && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
     const float tlim0 = tlim;
@@ -2374,7 +2381,7 @@ __device__ float inw_closest_beam(const InwScene &S, const KS &K, f3 o, f3 d, fl
     int bg = -1;
     uint32_t br = 0xffffffffu;
     const uint32_t *rank = S.rank + (invert ? S.n : 0u);
-    const size_t lbase = (size_t)(unit & ~63u) * S.beam_cap + (nw >> 8);
+    const size_t lbase = ((size_t)bo + (unit & ~63u)) * S.beam_cap + (nw >> 8);
     const uint2 *list = S.beam + lbase;
     const uint32_t *list16 = reinterpret_cast<const uint32_t *>(S.beam) + lbase;
     const float kap = S.beam_kappa;
@@ -2439,7 +2446,7 @@ __device__ float inw_closest_beam(const InwScene &S, const KS &K, f3 o, f3 d, fl
         }
     }
     // candidates not stored (entry >= cut) could still be reached below lim
-    if (ok && (ovf || !(lim < S.beam_cut[unit]))) ok = false;
+    if (ok && (ovf || !(lim < S.beam_cut[bo + unit]))) ok = false;
     if (!ok) return init_geom;
     if (bg < 0) return init_geom;
     tlim = bt;
@@ -3170,8 +3177,9 @@ __global__ __launch_bounds__(kBeamBlock) void k_inw_beam(Frame f, InwScene S, co
     const uint32_t u = blockIdx.x * kBeamBlock + threadIdx.x, lane = threadIdx.x & 63u;
     if (u >= units_total(f)) return;  // whole waves (units come in 8x8 blocks of 64)
     const UnitPix px = unit_pixel(f, u);
-    uint32_t *nout = const_cast<uint32_t *>(S.beam_n);
-    float *cout = const_cast<float *>(S.beam_cut);
+    const uint32_t bo = blockIdx.y * S.beam_units;  // time bin blockIdx.y (beam_bins > 1): its tree, its lists
+    uint32_t *nout = const_cast<uint32_t *>(S.beam_n) + bo;
+    float *cout = const_cast<float *>(S.beam_cut) + bo;
     const uint32_t cap = S.beam_cap;
     uint2 *L = lst + threadIdx.x;
     uint32_t nl = 0;
@@ -3187,7 +3195,7 @@ __global__ __launch_bounds__(kBeamBlock) void k_inw_beam(Frame f, InwScene S, co
         const uint32_t ox = cd.x < 0.0f ? 3u : 0u, oy = cd.y < 0.0f ? 4u : 1u, oz = cd.z < 0.0f ? 5u : 2u;
         const f3 rn = f3{cd.x < 0.0f ? R : -R, cd.y < 0.0f ? R : -R, cd.z < 0.0f ? R : -R};
         int *stk = st + threadIdx.x;
-        int sp = 0, cur = S.wroot;
+        int sp = 0, cur = S.beam_bins > 1u ? (int)(1u + S.wbin_base + blockIdx.y * S.wbin_stride) : S.wroot;
         while (!off) {
             const float4 *nd = S.wnodes + kInwNodeF4 * (cur - 1);
             const float4 nx = nd[ox], fx = nd[ox + 3], ny = nd[oy], fy = nd[oy + 3], nz = nd[oz], fz = nd[oz + 3];
@@ -3239,7 +3247,7 @@ __global__ __launch_bounds__(kBeamBlock) void k_inw_beam(Frame f, InwScene S, co
         if (lane >= d) incl += y;
     }
     const uint32_t at = incl - cnt;
-    const size_t base = (size_t)(u & ~63u) * cap + at;
+    const size_t base = ((size_t)bo + (u & ~63u)) * cap + at;
     if (S.beam16) {  // object ids < 2^16: the id and the high half of max(t, 0) (t rounded down)
         uint32_t *dst = reinterpret_cast<uint32_t *>(const_cast<uint2 *>(S.beam)) + base;
         for (uint32_t j = 0; j < cnt; j++) {
@@ -3715,12 +3723,16 @@ __global__ __launch_bounds__((pm_sub<LN, GQ>() * kBlock)) __attribute__((amdgpu_
         for (int round = 2 - kRounds; round < 2; round++) {
             const bool prim = bu != kBeamOff && !parked && K.top_primary();
             const bool go = busy && (round == 0 ? prim : (parked || K.size > 0u));
+            INW_T0(t_rnd);
             if (go) {
                 WalkPark wp{pslot, parked, false};
                 if (f.px_rays && !parked) atomicAdd(f.px_rays + px.out, 1u);  // rt_debug_pixel_rays (diagnostics only)
                 inw_segment<LIGHTS, WLN, FU, PK, QN>(S, f, K, s, col, dep, c, bu, &wp);
                 parked = PK && wp.parked;
             }
+#ifdef RT_DIAG_SPLIT
+            c.rnd[round] += (unsigned long long)clock64() - t_rnd;
+#endif
             if (busy && !parked && K.size == 0) {  // sample done: its sqrt(colour) (01_BVH...glsl:670) to the ring
                 if constexpr (LR) {
                     const uint32_t e = g & rmask;
@@ -3761,6 +3773,8 @@ __global__ __launch_bounds__((pm_sub<LN, GQ>() * kBlock)) __attribute__((amdgpu_
     }
     if (f.dbg && lane == 0) {
         for (int k = 0; k < 8; k++) atomicAdd(f.dbg + 8 + k, c.cyc[k]);
+        atomicAdd(f.dbg + 24, c.rnd[0]);
+        atomicAdd(f.dbg + 25, c.rnd[1]);
         // wall clock (100 MHz): first / last wave start, first queue drain, first / last wave exit
         const unsigned long long t_end = wall_clock64();
         unsigned long long *t = reinterpret_cast<unsigned long long *>(f.dbg) + 16;
@@ -4226,7 +4240,8 @@ hipError_t launch_iow03_resolve(const Frame &f, const SpecRecs &R, bool final_pa
 }
 hipError_t launch_inw_beam(const Frame &f, const InwScene &sc, const uint32_t *mode, uint32_t force, hipStream_t s) {
     const uint32_t n = units_of(f);
-    hipLaunchKernelGGL(k_inw_beam, dim3((n + kBeamBlock - 1) / kBeamBlock), dim3(kBeamBlock), 0, s, f, sc, mode, force);
+    const uint32_t nb = sc.beam_bins > 1u ? sc.beam_bins : 1u;
+    hipLaunchKernelGGL(k_inw_beam, dim3((n + kBeamBlock - 1) / kBeamBlock, nb), dim3(kBeamBlock), 0, s, f, sc, mode, force);
     return hipGetLastError();
 }
 // One frame of the on-chip-fold INW kernels: the probe (unless forced), then k_inw_pm and

@@ -83,6 +83,10 @@ struct InwScene {
     uint32_t dfs_high = 0;
     uint32_t n_wnodes = 0;  // wide nodes
     uint32_t n_lnodes = 0;  // the first n_lnodes wide nodes are staged in LDS (LN kernels only)
+    // Time-bin trees (wbins = 0: none): the wide closest-hit walk of a ray with time
+    // ratio r starts at node 1 + wbin_base + b * wbin_stride, b = min(int(r * wbins), wbins - 1),
+    // the root of the tree over the boxes the objects sweep in [b / wbins, (b + 1) / wbins]
+    uint32_t wbins = 0, wbin_base = 0, wbin_stride = 0;
     // Stackless LBVH walks (rt_options.inw_stackless; DESIGN.md §5 "Stackless LBVH
     // walk"): the reference's depth-first walks without their stack, by parent links, wherever no
     // push of the reference walk could drop (size + dfs_high <= 40).  sl = 0: off (or the node
@@ -116,6 +120,10 @@ struct InwScene {
     const uint32_t *beam_n = nullptr;
     const float *beam_cut = nullptr;
     uint32_t beam_cap = 0;
+    // beam_bins > 1: one list per pixel unit and time bin (k_inw_beam walks bin b's tree, the one at
+    // 1 + wbin_base + b * wbin_stride): the lists, counts and cuts of bin b follow those of bins < b
+    // (beam_units units each); a primary ray reads its time bin's list
+    uint32_t beam_bins = 0, beam_units = 0;
     float beam_R = 0.0f, beam_tmin = 0.0f, beam_tfar = 0.0f, beam_kappa = 0.0f;
     // Surrounding-RI grid (DESIGN.md §5 "RI grid"; null ri_cells = off): a uniform grid over the
     // LBVH leaf boxes; cell c lists (ri_ids[ri_cells[c] .. ri_cells[c + 1]]) every object whose

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert R.load().rt_abi_version() == R.ABI_VERSION == 4
+    assert R.load().rt_abi_version() == R.ABI_VERSION == 5
 
 
 def test_options_roundtrip_and_validation():

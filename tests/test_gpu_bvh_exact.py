@@ -170,6 +170,17 @@ def _same_frames(over, w, h, spp, scene):
     ({"inw_qnodes": 1}, INW1, 192, 108, 24),
     ({"inw_qnodes": 1, "inw_order": 1}, INW1, 97, 43, 7),
     ({"inw_qnodes": 1, "inw_order": 1}, INW1, 160, 96, 300),
+    # time-bin culling trees (default 4 for moving objects) against the swept tree alone, other
+    # bin counts (uneven sample splits, more bins than some spp), and the kernels that use them
+    ({"inw_time_bins": 0}, INW1, 192, 108, 24),
+    ({"inw_time_bins": 3}, INW1, 97, 43, 7),
+    ({"inw_time_bins": 16, "inw_order": -1}, INW1, 160, 96, 37),
+    ({"inw_time_bins": 5, "inw_lds_nodes": 0}, INW1, 128, 72, 300),
+    ({"inw_time_bins": 0, "inw_order": 2}, INW1, 200, 100, 37),
+    ({"inw_time_bins": 2, "inw_ring_pm": 1024}, INW1, 128, 72, 40),
+    ({"inw_beam_bins": 0}, INW1, 192, 108, 24),          # one beam list per pixel, bin trees for the walks
+    ({"inw_walk_bins": 0}, INW1, 97, 43, 7),             # beam lists per bin, the swept tree for the walks
+    ({"inw_walk_bins": 0, "inw_time_bins": 7}, INW1, 160, 96, 300),
     ({"inw_beams": 0, "inw_order": 1}, INW4, 128, 128, 16),
     ({"inw_fused_cull": 0, "inw_order": 1}, INW4, 128, 128, 16),
     ({"inw_ri_grid": 0, "inw_order": 1}, INW4, 128, 128, 16),

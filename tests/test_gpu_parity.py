@@ -316,6 +316,9 @@ def test_debug_path_reports_the_fold_ring(gpu):
     p = paths["lds"]
     assert p["kernel"].startswith("k_inw_pm") and p["ring_lds"] == 1 and p["ring_entries"] == 256
     assert p["lds_nodes"] == 0  # the FStack LDS-ring instances read every node from L1 / L2
+    assert p["time_bins"] == 2  # moving spheres: the walks pick one of 2 time-bin trees
+    assert p["beam_bins"] == 2  # ... and the primary rays one of 2 beam lists per pixel
+    assert paths["gq"]["time_bins"] == 0 and paths["global"]["time_bins"] == 0 and paths["sm"]["time_bins"] == 0
     assert p["qnodes"] == 0 and p["global_stack"] == 0 and p["walk_stack"] == 37
     p = paths["gq"]  # GQ: quantised nodes, the top ones staged in LDS, the 40-float stacks in global memory
     assert p["kernel"].startswith("k_inw_pm") and p["ring_lds"] == 1 and p["ring_entries"] == 256

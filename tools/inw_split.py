@@ -43,7 +43,7 @@ p = sc.params
 rgba = torch.zeros((p.height, p.width, 4), dtype=torch.float32, device=dev)
 depth = torch.zeros((p.height, p.width), dtype=torch.float32, device=dev)
 ctr = torch.zeros(6, dtype=torch.int64, device=dev)
-dbg = torch.zeros(24, dtype=torch.int64, device=dev)
+dbg = torch.zeros(32, dtype=torch.int64, device=dev)  # slots 8-15 phases, 16-20 timeline, 24-25 rounds
 st = torch.cuda.current_stream()
 if shard:
     from bench import tile_for, tiles_for_rank
@@ -83,6 +83,8 @@ names = ("closest_hit", "ri_walk", "fold", "claim_issue", "segment_step", "seg_p
          "seg_tail")
 cyc = dict(zip(names, d[8:16]))
 tot = cyc["fold"] + cyc["claim_issue"] + cyc["segment_step"]
+# k_inw_pm: whole-wave cycles of the primary round (beam lists) and the bounce round (wide walk)
+cyc["round0_primary"], cyc["round1_bounce"] = d[24], d[25]
 kname = C.create_string_buffer(64)
 lib.rt_debug_launches(scene, kname, 64)
 t = d[16:21]  # wall clock, 100 MHz
