@@ -137,6 +137,8 @@ typedef struct rt_options {
                                the L2); scenes built on the host */
     int inw_walk_bins;      /* 1 (default): the wide closest-hit walks use the time-bin trees */
     int inw_beam_bins;      /* 1 (default): a pixel's beam lists per time bin, from the time-bin trees */
+    int inw_sphere_records; /* 1 (default): in scenes of equal-scale ellipsoids with the identity rotation, the
+                               wide walk and beam lists test objects from 2-float4 sphere records */
     /* IOW-03 (In-One-Weekend 03) */
     int iow_spec;           /* sample-parallel speculation (0: the sequential per-pixel kernel) */
     int iow_linear;         /* [build] the shader's linear object loop instead of the culling BVH */
@@ -343,6 +345,7 @@ typedef struct rt_path_info {
     int time_bins;        /* INW: time-bin culling trees the wide closest-hit walks chose from (0: the swept
                              tree; inw_time_bins, moving objects, walks that read no LDS-staged nodes) */
     int beam_bins;        /* INW: beam lists per pixel (one per time bin; 0: one list over the swept boxes) */
+    int sphere_records;   /* INW: 1 when the object tests read the sphere records (inw_sphere_records) */
 } rt_path_info;
 int rt_debug_path(rt_dev_scene *s, rt_path_info *out);
 

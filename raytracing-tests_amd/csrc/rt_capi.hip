@@ -34,7 +34,7 @@ rt_options default_options() {
     o.inw_wide_walk = 1; o.inw_order = 0; o.inw_beams = 1; o.inw_ri_grid = 1; o.inw_lds_nodes = 1;
     o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 0; o.inw_ring_sm = 0; o.inw_stackless = 1;
     o.inw_device_build = 1; o.inw_claim_xcd = 1; o.inw_qnodes = 0; o.inw_time_bins = 2;
-    o.inw_walk_bins = 1; o.inw_beam_bins = 1;
+    o.inw_walk_bins = 1; o.inw_beam_bins = 1; o.inw_sphere_records = 1;
     o.iow_spec = 1; o.iow_linear = 0; o.iow_narrow = 0; o.iow_lds_bvh = 1;
     o.iow_leaf_batch = 32;  // 32 measured 2.5% faster on the bench frame than 65 (round 2)
     o.iow_coop_max = 4; o.iow_chunks_lpt = 0;
@@ -172,6 +172,8 @@ struct rt_dev_scene {
     int n_focus = 0;        // INW-01 MULTIFOCUS lens chain (0 = the reference's single focus)
     float focus[9] = {};
     DevBuf hot, cold, nodes, lights, sunflower, fib, ring, counter;
+    DevBuf sph;           // INW sphere scenes: 2 float4 per object (rtk::InwScene::sph)
+    bool sph_ok = false;
     DevBuf obox;  // IOW-03: per-object culling boxes (2 float4 each) for wave-cooperative queries
     DevBuf tex, tex_info;  // INW-04 material textures (float4 texels, (first, w, h, 0) per texture)
     DevBuf wnodes, wrank, wleaf;  // INW wide walk: culling BVH, depth-first ranks, LBVH leaf boxes
@@ -373,6 +375,7 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     }
     sc.rank = s->wrank.as<uint32_t>();
     sc.leafbox = s->wleaf.as<float4>();
+    if (s->sph_ok && s->opt.inw_sphere_records) sc.sph = s->sph.as<float4>();
     sc.dfs_high = s->dfs_high;
     sc.n_wnodes = s->n_wnodes;
     if (s->ri_ok && s->opt.inw_ri_grid) {
@@ -446,6 +449,24 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n, double *ms = 
     return RT_OK;
 }
 
+// Sphere records (rtk::InwScene::sph) when every object is an ellipsoid with equal scales and the
+// identity rotation (entries exactly 1 and +-0): (position, RN(1/scale)), (position - last_position,
+// RI).  false: some object is not.
+bool inw_sphere_records(const float *geom, uint32_t n, int layout, std::vector<float> &out) {
+    out.assign(size_t(n) * 8, 0.0f);
+    for (uint32_t j = 0; j < n; j++) {
+        const float *f = geom + size_t(j) * 28;
+        if (int(f[18] + 0.1f) != 1 || !(f[12] == f[13] && f[13] == f[14]) || !std::isfinite(f[12])) return false;
+        for (int k = 0; k < 9; k++)
+            if (f[3 + k] != ((k % 4) == 0 ? 1.0f : 0.0f)) return false;
+        float *o = out.data() + size_t(j) * 8;
+        o[0] = f[0]; o[1] = f[1]; o[2] = f[2]; o[3] = 1.0f / f[12];  // the hot record's is (RN(1/scale))
+        o[4] = f[15]; o[5] = f[16]; o[6] = f[17];
+        o[7] = layout == 4 ? f[19] : f[20];  // the RI the surrounding-RI walk adds (the hot record's)
+    }
+    return n > 0;
+}
+
 // The kernels' hot / cold records from the reference's GeometryBuff(_04) records (28 floats).
 void inw_records(const float *geom, uint32_t n, int layout, std::vector<float> &hot, std::vector<float> &cold) {
     hot.assign(size_t(n) * rtk::kInwHot, 0.0f);
@@ -484,6 +505,11 @@ int make_inw(rt_dev_scene *s, const float *geom, uint32_t n, int layout, const f
     s->n = n; s->layout = layout; s->n_lights = layout == 4 ? n_lights : 0;
     HIP_OK(s->hot.store(hot.data(), hot.size() * sizeof(float)));
     HIP_OK(s->cold.store(cold.data(), cold.size() * sizeof(float)));
+    {
+        std::vector<float> sph;
+        s->sph_ok = inw_sphere_records(geom, n, layout, sph);
+        if (s->sph_ok) HIP_OK(s->sph.store(sph.data(), sph.size() * sizeof(float)));
+    }
     HIP_OK(s->nodes.store(nodes, size_t(2 * n - 1) * 8 * sizeof(float)));
     if (int rc = make_inw_wide(s, nodes, n, nullptr, geom); rc != RT_OK) return rc;
     if (s->n_lights) HIP_OK(s->lights.store(lights, size_t(s->n_lights) * 7 * sizeof(float)));
@@ -580,6 +606,14 @@ int update_inw(rt_dev_scene *s, const float *geom, uint32_t n, const float *node
     const uint32_t nl = s->layout == 4 ? n_lights : 0;
     HIP_OK(s->hot.store(hot.data(), hot.size() * sizeof(float)));
     HIP_OK(s->cold.store(cold.data(), cold.size() * sizeof(float)));
+    {
+        std::vector<float> sph;
+        s->sph_ok = false;  // (the scene is marked broken until the update completes)
+        if (inw_sphere_records(geom, n, s->layout, sph)) {
+            HIP_OK(s->sph.store(sph.data(), sph.size() * sizeof(float)));
+            s->sph_ok = true;
+        }
+    }
     if (nl) HIP_OK(s->lights.store(lights, size_t(nl) * 7 * sizeof(float)));
     lap(0);
     const size_t nbytes = size_t(2 * n - 1) * 8 * sizeof(float);
@@ -1434,6 +1468,7 @@ int launch_scene_inw_fold(rt_dev_scene *s, rtk::Frame &f, hipStream_t st) {
             P.lds_nodes = int(std::min<uint32_t>(s->n_wtree0, uint32_t(rtk::kGqQn ? rtk::kQLdsNodes : rtk::kInwLdsNodes)));
         P.time_bins = sc.wnodes && !sc.gstk ? int(sc.wbins) : 0;  // the GQ walks read the staged (swept) tree
         P.beam_bins = sc.beam ? int(sc.beam_bins) : 0;
+        P.sphere_records = sc.sph ? 1 : 0;
     }
     if (epoch == 0) e = hipMemsetAsync(s->inw_ring.p, 0xff, s->inw_ring.bytes, st);
     if (e == hipSuccess) s->ring_frame = epoch + 1;

@@ -2170,7 +2170,9 @@ struct WalkPark {
     bool parked;    // out: parked again
 };
 // QN: the quantised nodes (S.qnodes, cull4q; requires FU), LN then meaning the staged ones in g_inw_qlds.
-template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false, bool QN = false, class KS = FStack>
+// SP: the sphere-record object test is compiled in (INW-01 kernels; INW-04's keep their registers)
+template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false, bool QN = false, class KS = FStack,
+          bool SP = true>
 __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float ratio, bool invert, float &tlim,
                                    f3 &normal, float &extra, float init_geom, Ctr &c, bool &ok,
                                    WalkPark *wp = nullptr) {
@@ -2218,16 +2220,24 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
     auto leaf = [&](int g) {
         c.prims++;
         const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
-        const Xf x = load_xf(S, g);  // loaded with the box, before its test: one memory latency
-        float te;
-        const bool inb = test_aabb_te(n0, n1, o, id, tlim0, te);
-        f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
-        f3 to = tmul(x.R, ov), td = tmul(x.R, d);
-        keep_before_branch(to, td);
-        if (!inb) return;
-        float t = -1.0f;
-        if (x.type == 1) t = t_ellipsoid(to, td, x.is);
-        else if (x.type == 2) t = t_cuboid(to, td, x.scale);
+        float te, t = -1.0f;
+        if (SP && S.sph) {  // a sphere scene: 2 float4 instead of 7, no rotation (R = I: tmul(R, v) = v)
+            const float4 p = S.sph[2 * g], q = S.sph[2 * g + 1];
+            const bool inb = test_aabb_te(n0, n1, o, id, tlim0, te);
+            const f3 to = (o - mk(p.x, p.y, p.z)) + mk(q.x, q.y, q.z) * (1.0f - ratio);
+            keep_before_branch(to, d);
+            if (!inb) return;
+            t = t_ellipsoid(to, d, f3{p.w, p.w, p.w});
+        } else {
+            const Xf x = load_xf(S, g);  // loaded with the box, before its test: one memory latency
+            const bool inb = test_aabb_te(n0, n1, o, id, tlim0, te);
+            f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+            f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+            keep_before_branch(to, td);
+            if (!inb) return;
+            if (x.type == 1) t = t_ellipsoid(to, td, x.is);
+            else if (x.type == 2) t = t_cuboid(to, td, x.scale);
+        }
         if (t > 0.0f && t < tlim0) {
             if (t < te) ovf = true;  // the guard above: the reference walk decides this ray
             const uint32_t r = rank[g];
@@ -2412,30 +2422,50 @@ __device__ float inw_closest_beam(const InwScene &S, const KS &K, f3 o, f3 d, fl
             const int g = (int)e.x;
             c.prims++;
             float4 n0, n1;
-            Xf x;
+            float te, t = -1.0f;
+            bool inb;
 #ifndef RT_INW_BEAM_VLOAD
             // one candidate for every active lane (a wave's lanes trace samples of one pixel and step
             // through its list together): scalar loads, C3 184.7 -> 182.5 ms
             // (profiles/r06_ab_beam_sload_ring_il.json; -DRT_INW_BEAM_VLOAD: vector loads only)
             const int g0 = __builtin_amdgcn_readfirstlane(g);
-            if (__ballot(g != g0) == 0ull) {
-                n0 = sload4(S.leafbox, 2 * g0); n1 = sload4(S.leafbox, 2 * g0 + 1);
-                x = load_xf_s(S, g0);
-            } else
+            const bool uni_g = __ballot(g != g0) == 0ull;
+#else
+            const int g0 = g;
+            const bool uni_g = false;
 #endif
-            {
-                n0 = S.leafbox[2 * g]; n1 = S.leafbox[2 * g + 1];
-                x = load_xf(S, g);
+            if (S.sph) {  // a sphere scene (inw_traverse_wide's leaf test): 2 float4, R = I
+                float4 p, q;
+                if (uni_g) {
+                    n0 = sload4(S.leafbox, 2 * g0); n1 = sload4(S.leafbox, 2 * g0 + 1);
+                    p = sload4(S.sph, 2 * g0); q = sload4(S.sph, 2 * g0 + 1);
+                } else {
+                    n0 = S.leafbox[2 * g]; n1 = S.leafbox[2 * g + 1];
+                    p = S.sph[2 * g]; q = S.sph[2 * g + 1];
+                }
+                inb = test_aabb_te(n0, n1, o, id, tlim0, te);
+                const f3 to = (o - mk(p.x, p.y, p.z)) + mk(q.x, q.y, q.z) * (1.0f - ratio);
+                keep_before_branch(to, d);
+                if (inb) t = t_ellipsoid(to, d, f3{p.w, p.w, p.w});
+            } else {
+                Xf x;
+                if (uni_g) {
+                    n0 = sload4(S.leafbox, 2 * g0); n1 = sload4(S.leafbox, 2 * g0 + 1);
+                    x = load_xf_s(S, g0);
+                } else {
+                    n0 = S.leafbox[2 * g]; n1 = S.leafbox[2 * g + 1];
+                    x = load_xf(S, g);
+                }
+                inb = test_aabb_te(n0, n1, o, id, tlim0, te);
+                f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+                f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+                keep_before_branch(to, td);
+                if (inb) {
+                    if (x.type == 1) t = t_ellipsoid(to, td, x.is);
+                    else if (x.type == 2) t = t_cuboid(to, td, x.scale);
+                }
             }
-            float te;
-            const bool inb = test_aabb_te(n0, n1, o, id, tlim0, te);
-            f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
-            f3 to = tmul(x.R, ov), td = tmul(x.R, d);
-            keep_before_branch(to, td);
             if (inb) {
-                float t = -1.0f;
-                if (x.type == 1) t = t_ellipsoid(to, td, x.is);
-                else if (x.type == 2) t = t_cuboid(to, td, x.scale);
                 if (t > 0.0f && t < tlim0) {
                     if (t < te) ovf = true;  // the leaf-entry guard (inw_traverse_wide)
                     const uint32_t r = rank[g];
@@ -2559,20 +2589,31 @@ __device__ float inw_ri_grid(const InwScene &S, f3 hp, float ratio, Ctr &c, bool
         if (k + 1 < e) gn = S.ri_ids[k + 1];
         c.prims++;
         const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
-        const Xf x = load_xf(S, g);
         const uint32_t rg = S.rank[g];
-        if (!(hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z)) continue;
-        f3 v = (hp - x.pos) + x.delta * (1.0f - ratio);
-        v = tmul(x.R, v);
-        v.x *= x.is.x; v.y *= x.is.y; v.z *= x.is.z;
         bool inside;
-        if (x.type == 1) inside = dot(v, v) <= 1.0f;
-        else if (x.type == 2) inside = fabsf(v.x) <= 0.5f && fabsf(v.y) <= 0.5f && fabsf(v.z) <= 0.5f;
-        else inside = false;
+        float ri;
+        if (S.sph) {  // sphere records (RI in q.w): R = I, so v = ov * is, the same floats
+            const float4 p = S.sph[2 * g], q = S.sph[2 * g + 1];
+            if (!(hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z)) continue;
+            f3 v = (hp - mk(p.x, p.y, p.z)) + mk(q.x, q.y, q.z) * (1.0f - ratio);
+            v.x *= p.w; v.y *= p.w; v.z *= p.w;
+            inside = dot(v, v) <= 1.0f;
+            ri = q.w;
+        } else {
+            const Xf x = load_xf(S, g);
+            if (!(hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z)) continue;
+            f3 v = (hp - x.pos) + x.delta * (1.0f - ratio);
+            v = tmul(x.R, v);
+            v.x *= x.is.x; v.y *= x.is.y; v.z *= x.is.z;
+            if (x.type == 1) inside = dot(v, v) <= 1.0f;
+            else if (x.type == 2) inside = fabsf(v.x) <= 0.5f && fabsf(v.y) <= 0.5f && fabsf(v.z) <= 0.5f;
+            else inside = false;
+            ri = x.ri_acc;
+        }
         if (inside) {
             if (nin == kRiMax) { ok = false; return 1.0f; }
             rk[nin] = rg;
-            rv[nin] = x.ri_acc;
+            rv[nin] = ri;
             nin++;
         }
     }
@@ -2717,7 +2758,7 @@ __device__ __forceinline__ float inw_closest(const InwScene &S, KS &K, f3 o, f3 
                                              float &tlim, f3 &normal, float &extra, float init_geom, Ctr &c,
                                              WalkPark *wp = nullptr) {
     bool ok = false;
-    const float g = inw_traverse_wide<WANT_NORMAL, LN, FU, PK, QN>(S, K, o, d, ratio, invert, tlim, normal, extra,
+    const float g = inw_traverse_wide<WANT_NORMAL, LN, FU, PK, QN, KS, EO>(S, K, o, d, ratio, invert, tlim, normal, extra,
                                                                    init_geom, c, ok, wp);
     if (PK && wp->parked) return g;
     OCC_TALLY(c, kOccRef, !ok);

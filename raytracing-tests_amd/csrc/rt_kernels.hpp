@@ -80,6 +80,13 @@ struct InwScene {
     int wroot = 0;
     const uint32_t *rank = nullptr;
     const float4 *leafbox = nullptr;  // per object: its LBVH leaf node (2 float4: the reference's leaf box)
+    // Sphere scenes (DESIGN.md §5.2 "Sphere records"; null = off): every object an ellipsoid of equal
+    // scales with the identity rotation; per object 2 float4, (position, RN(1/scale)) and (position -
+    // last_position, its RI).  The wide walk's, the beam lists' and the RI grid's object tests read
+    // these instead of the 7-float4 record: R = I makes the object-space ray the world one, the same
+    // floats (up to the signs of zero terms, which neither t nor the inside test can see); the
+    // winner's normal still comes from the full record
+    const float4 *sph = nullptr;
     uint32_t dfs_high = 0;
     uint32_t n_wnodes = 0;  // wide nodes
     uint32_t n_lnodes = 0;  // the first n_lnodes wide nodes are staged in LDS (LN kernels only)

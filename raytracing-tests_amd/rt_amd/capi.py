@@ -75,7 +75,7 @@ class RtOptions(C.Structure):
     _fields_ = [("size", C.c_uint32)] + [(n, C.c_int) for n in (
         "inw_wide_walk", "inw_order", "inw_beams", "inw_ri_grid", "inw_lds_nodes", "inw_fused_cull",
         "inw_claim_order", "inw_ring_pm", "inw_ring_sm", "inw_stackless", "inw_device_build", "inw_claim_xcd",
-        "inw_qnodes", "inw_time_bins", "inw_walk_bins", "inw_beam_bins",
+        "inw_qnodes", "inw_time_bins", "inw_walk_bins", "inw_beam_bins", "inw_sphere_records",
         "iow_spec", "iow_linear", "iow_narrow", "iow_lds_bvh", "iow_leaf_batch", "iow_coop_max", "iow_chunks_lpt",
         "rounds_seq", "rounds_spec", "park_min",
         "spec_iters", "spec_probe", "spec_heavy", "spec_rounds", "spec_tail_rounds", "spec_tail_budget", "spec_scan",
@@ -93,7 +93,7 @@ class RtPathInfo(C.Structure):
                 ("lds_nodes", C.c_int), ("claim_order", C.c_int), ("ring_entries", C.c_int), ("iow_bvh", C.c_int),
                 ("ring_lds", C.c_int), ("stackless", C.c_int), ("lbvh_lds_nodes", C.c_int),
                 ("qnodes", C.c_int), ("global_stack", C.c_int), ("walk_stack", C.c_int), ("ref_walks", C.c_uint64),
-                ("time_bins", C.c_int), ("beam_bins", C.c_int)]
+                ("time_bins", C.c_int), ("beam_bins", C.c_int), ("sphere_records", C.c_int)]
 
     ORDERS = {0: None, 1: "pixel-major", 2: "sample-major", 3: "per-pixel", 4: "sample-parallel", 5: "sequential"}
 

@@ -181,6 +181,10 @@ def _same_frames(over, w, h, spp, scene):
     ({"inw_beam_bins": 0}, INW1, 192, 108, 24),          # one beam list per pixel, bin trees for the walks
     ({"inw_walk_bins": 0}, INW1, 97, 43, 7),             # beam lists per bin, the swept tree for the walks
     ({"inw_walk_bins": 0, "inw_time_bins": 7}, INW1, 160, 96, 300),
+    # the 7-float4 object records against the 2-float4 sphere records (default for sphere scenes)
+    ({"inw_sphere_records": 0}, INW1, 192, 108, 24),
+    ({"inw_sphere_records": 0, "inw_order": 2}, INW1, 200, 100, 37),
+    ({"inw_sphere_records": 0, "inw_order": -1, "inw_beams": 2}, INW1, 97, 43, 7),
     ({"inw_beams": 0, "inw_order": 1}, INW4, 128, 128, 16),
     ({"inw_fused_cull": 0, "inw_order": 1}, INW4, 128, 128, 16),
     ({"inw_ri_grid": 0, "inw_order": 1}, INW4, 128, 128, 16),

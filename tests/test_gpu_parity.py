@@ -318,6 +318,7 @@ def test_debug_path_reports_the_fold_ring(gpu):
     assert p["lds_nodes"] == 0  # the FStack LDS-ring instances read every node from L1 / L2
     assert p["time_bins"] == 2  # moving spheres: the walks pick one of 2 time-bin trees
     assert p["beam_bins"] == 2  # ... and the primary rays one of 2 beam lists per pixel
+    assert p["sphere_records"] == 1  # equal-scale unrotated ellipsoids: the 2-float4 object records
     assert paths["gq"]["time_bins"] == 0 and paths["global"]["time_bins"] == 0 and paths["sm"]["time_bins"] == 0
     assert p["qnodes"] == 0 and p["global_stack"] == 0 and p["walk_stack"] == 37
     p = paths["gq"]  # GQ: quantised nodes, the top ones staged in LDS, the 40-float stacks in global memory
@@ -328,6 +329,7 @@ def test_debug_path_reports_the_fold_ring(gpu):
     assert p["lds_nodes"] > 5
     p = paths["sm"]
     assert p["kernel"].startswith("k_inw_sm") and p["ring_lds"] == 0 and p["lds_nodes"] > 5
+    assert p["sphere_records"] == 1
     # INW-04's room (4 wide nodes): the sample-major ring goes to LDS as well (inw_ring_sm = 0),
     # beside every node the staging would take anyway; a power of two keeps the global ring
     sc = R.make_scene(R.PRESET_INW04_CORNELL, 7, 0, width=64, height=64, spp=8)
