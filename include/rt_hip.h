@@ -139,6 +139,8 @@ typedef struct rt_options {
     int inw_beam_bins;      /* 1 (default): a pixel's beam lists per time bin, from the time-bin trees */
     int inw_sphere_records; /* 1 (default): in scenes of equal-scale ellipsoids with the identity rotation, the
                                wide walk and beam lists test objects from 2-float4 sphere records */
+    int inw_compact_nodes;  /* 1 (default): the wide walk reads its nodes from global memory as 7 float4
+                               (112 B) instead of 10 (the repeated low planes dropped) */
     /* IOW-03 (In-One-Weekend 03) */
     int iow_spec;           /* sample-parallel speculation (0: the sequential per-pixel kernel) */
     int iow_linear;         /* [build] the shader's linear object loop instead of the culling BVH */

@@ -802,6 +802,20 @@ hipError_t inw_wide_build_device(const float4 *nodes, const uint32_t *lcnt, uint
     return hipSuccess;
 }
 
+// The wide nodes without the repeated low planes (InwScene::cnodes): 7 float4 per node, lx ly lz
+// hx hy hz links, for the buffer-load walk (a ray's far plane of axis a sits at a + 3 (1 - s_a))
+__global__ __launch_bounds__(kB) void k_compact_wnodes(const float4 *wn, uint32_t nw, float4 *cn) {
+    const uint32_t i = blockIdx.x * kB + threadIdx.x;
+    if (i >= nw * 7u) return;
+    const uint32_t w = i / 7u, k = i - 7u * w;
+    cn[i] = wn[(size_t)w * 10 + (k < 6u ? k : 9u)];
+}
+hipError_t inw_compact_wnodes(const float4 *wnodes, uint32_t nw, float4 *cnodes, hipStream_t s) {
+    if (!nw) return hipSuccess;
+    hipLaunchKernelGGL(k_compact_wnodes, dim3(nblk(nw * 7u)), dim3(kB), 0, s, wnodes, nw, cnodes);
+    return hipGetLastError();
+}
+
 size_t ri_scan_temp_bytes(size_t cells) {
     size_t sb = 0;
     (void)hipcub::DeviceScan::InclusiveSum(nullptr, sb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)cells);

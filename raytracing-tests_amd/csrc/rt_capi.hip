@@ -34,7 +34,7 @@ rt_options default_options() {
     o.inw_wide_walk = 1; o.inw_order = 0; o.inw_beams = 1; o.inw_ri_grid = 1; o.inw_lds_nodes = 1;
     o.inw_fused_cull = 1; o.inw_claim_order = 1; o.inw_ring_pm = 0; o.inw_ring_sm = 0; o.inw_stackless = 1;
     o.inw_device_build = 1; o.inw_claim_xcd = 1; o.inw_qnodes = 0; o.inw_time_bins = 2;
-    o.inw_walk_bins = 1; o.inw_beam_bins = 1; o.inw_sphere_records = 1;
+    o.inw_walk_bins = 1; o.inw_beam_bins = 1; o.inw_sphere_records = 1; o.inw_compact_nodes = 1;
     o.iow_spec = 1; o.iow_linear = 0; o.iow_narrow = 0; o.iow_lds_bvh = 1;
     o.iow_leaf_batch = 32;  // 32 measured 2.5% faster on the bench frame than 65 (round 2)
     o.iow_coop_max = 4; o.iow_chunks_lpt = 0;
@@ -178,6 +178,7 @@ struct rt_dev_scene {
     DevBuf tex, tex_info;  // INW-04 material textures (float4 texels, (first, w, h, 0) per texture)
     DevBuf wnodes, wrank, wleaf;  // INW wide walk: culling BVH, depth-first ranks, LBVH leaf boxes
     DevBuf qnodes;                // ... the culling BVH quantised (4 float4 per node, rtk::inw_quantize_wnodes)
+    DevBuf cnodes;                // ... without the repeated low planes (7 float4 per node, rtk::inw_compact_wnodes)
     DevBuf gstk;                  // k_inw_pm's GQ instance: the reference's 40-float stacks, 160 B per lane
     DevBuf walk_ctr;              // the last frame's closest-hit queries handed to the LBVH walks (u64)
     DevBuf ri_cells, ri_ids;      // INW surrounding-RI grid (cell offsets, object ids)
@@ -376,6 +377,7 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
     sc.rank = s->wrank.as<uint32_t>();
     sc.leafbox = s->wleaf.as<float4>();
     if (s->sph_ok && s->opt.inw_sphere_records) sc.sph = s->sph.as<float4>();
+    if (s->opt.inw_compact_nodes) sc.cnodes = s->cnodes.as<float4>();
     sc.dfs_high = s->dfs_high;
     sc.n_wnodes = s->n_wnodes;
     if (s->ri_ok && s->opt.inw_ri_grid) {
@@ -394,6 +396,8 @@ void set_wide(const rt_dev_scene *s, rtk::InwScene &sc) {
 constexpr float kQMargin = 2e-3f;
 int make_qnodes(rt_dev_scene *s) {
     if (!s->n_wnodes) return RT_OK;
+    HIP_OK(s->cnodes.reserve(size_t(s->n_wnodes) * 7 * sizeof(float4)));
+    HIP_OK(rtk::inw_compact_wnodes(s->wnodes.as<float4>(), s->n_wnodes, s->cnodes.as<float4>(), nullptr));
     HIP_OK(s->qnodes.reserve(size_t(s->n_wnodes) * rtk::kQNodeF4 * sizeof(float4)));
     HIP_OK(rtk::inw_quantize_wnodes(s->wnodes.as<float4>(), s->n_wnodes, s->qnodes.as<float4>(), kQMargin, nullptr));
     return RT_OK;

@@ -2008,13 +2008,29 @@ __device__ __forceinline__ void inw_wnode_nf(const InwScene &S, int cur, uint32_
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wnode_rsrc(const InwScene &S) {
+// The buffer-load walk's node layout: 10 float4 (wnodes: the far planes 48 B after the near ones)
+// or, with InwScene::cnodes, 7 float4 (the far plane of axis a at a + 3 (1 - s_a): its own offset)
+struct WnodeBuf {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t stride, lk;     // bytes per node, offset of the links
+    uint32_t fx, fy, fz;     // far-plane offsets of this ray's octant
+};
+__device__ __forceinline__ WnodeBuf wnode_buf(const InwScene &S, uint32_t oxb, uint32_t oyb, uint32_t ozb) {
+    WnodeBuf w;
+    const bool c = S.cnodes != nullptr;
+    w.stride = c ? 112u : (uint32_t)kInwNodeF4 * 16u;
+    w.lk = c ? 96u : 144u;
+    // cnodes: near at 16 a + 48 s_a, far at 16 a + 48 (1 - s_a): near + far = 32 a + 48
+    w.fx = c ? 48u - oxb : oxb + 48u;
+    w.fy = c ? 80u - oyb : oyb + 48u;
+    w.fz = c ? 112u - ozb : ozb + 48u;
     // dword 3 = 0x00020000: the gfx9-family raw-buffer format word; num_records bounds the nodes
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(S.wnodes), (short)0,
-                                             (int)(S.n_wnodes * (uint32_t)kInwNodeF4 * 16u), 0x00020000);
+    w.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(c ? S.cnodes : S.wnodes), (short)0,
+                                             (int)(S.n_wnodes * w.stride), 0x00020000);
+    return w;
 }
 template <bool LN>
-__device__ __forceinline__ void inw_wnode_nf_buf(const InwScene &S, __amdgpu_buffer_rsrc_t rs, int cur, uint32_t oxb,
+__device__ __forceinline__ void inw_wnode_nf_buf(const InwScene &S, const WnodeBuf &W, int cur, uint32_t oxb,
                                                  uint32_t oyb, uint32_t ozb, float4 &nx, float4 &ny, float4 &nz,
                                                  float4 &fx, float4 &fy, float4 &fz, float4 &lk) {
     if (LN && (uint32_t)(cur - 1) < S.n_lnodes) {
@@ -2023,11 +2039,11 @@ __device__ __forceinline__ void inw_wnode_nf_buf(const InwScene &S, __amdgpu_buf
         nx = px[0]; fx = px[3]; ny = py[0]; fy = py[3]; nz = pz[0]; fz = pz[3]; lk = nd[9];
         return;
     }
-    const uint32_t b = __umul24((uint32_t)(cur - 1), (uint32_t)(kInwNodeF4 * 16));  // v_mul_u32_u24 (ids < 2^24)
-    nx = bload4(rs, b + oxb); fx = bload4(rs, b + oxb + 48u);
-    ny = bload4(rs, b + oyb); fy = bload4(rs, b + oyb + 48u);
-    nz = bload4(rs, b + ozb); fz = bload4(rs, b + ozb + 48u);
-    lk = bload4(rs, b + 144u);
+    const uint32_t b = __umul24((uint32_t)(cur - 1), W.stride);  // v_mul_u32_u24 (ids < 2^24)
+    nx = bload4(W.rs, b + oxb); fx = bload4(W.rs, b + W.fx);
+    ny = bload4(W.rs, b + oyb); fy = bload4(W.rs, b + W.fy);
+    nz = bload4(W.rs, b + ozb); fz = bload4(W.rs, b + W.fz);
+    lk = bload4(W.rs, b + W.lk);
 }
 // FU: one fused multiply-add per plane, plane * (1/d) + (-o * (1/d)), the second term computed
 // once per ray (noid).  Its rounding error in t is at most |o| * 2^-23 * |1/d| per axis, against a
@@ -2199,7 +2215,7 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
     float *const wsb = K.walk_stack(PK ? 8u : 0u, 3, cap);  // entry p at wsb[p * kBlock]
     const uint32_t ox = d.x < 0.0f ? 3u : 0u, oy = d.y < 0.0f ? 4u : 1u, oz = d.z < 0.0f ? 5u : 2u;
 #ifndef RT_INW_NO_BUFLOAD
-    const __amdgpu_buffer_rsrc_t wrs = wnode_rsrc(S);
+    const WnodeBuf wrs = wnode_buf(S, ox * 16u, oy * 16u, oz * 16u);
 #endif
     int sp = 0, pend = -1, cur = S.wroot;
     if (!LN && S.wbins > 1u) {  // the ray's time-bin tree (the staged nodes are the swept tree's)

@@ -77,6 +77,9 @@ struct InwScene {
     // order (rank[g] with invert false, rank[n + g] with invert true), its LBVH leaf node, and the
     // depth-first stack high-water mark (pushes can only drop when size + dfs_high > 40)
     const float4 *wnodes = nullptr;
+    // the same nodes as 7 float4 (lx ly lz hx hy hz links; DESIGN.md §5.2 "Compact nodes"), read by
+    // the buffer-load walk from global memory when set (the LDS staging and the other walks keep wnodes)
+    const float4 *cnodes = nullptr;
     int wroot = 0;
     const uint32_t *rank = nullptr;
     const float4 *leafbox = nullptr;  // per object: its LBVH leaf node (2 float4: the reference's leaf box)
@@ -336,6 +339,8 @@ hipError_t inw_wide_build_device(const float4 *nodes, const uint32_t *lcnt, uint
 // the quantised form of nw wide nodes (InwScene::qnodes): 4 float4 per node, planes rounded
 // outward by at least `margin` beyond the wide node's (rt_build.hip)
 hipError_t inw_quantize_wnodes(const float4 *wnodes, uint32_t nw, float4 *qnodes, float margin, hipStream_t s);
+// InwScene::cnodes from the wide nodes (rt_build.hip)
+hipError_t inw_compact_wnodes(const float4 *wnodes, uint32_t nw, float4 *cnodes, hipStream_t s);
 // the surrounding-RI grid on the device (rtamd::ri_grid_build's cells and ids) over the extent
 // inw_wide_build_device returned: per-cell counts scanned into cells[0..nc] with the total and an
 // over-64 flag read back (synchronises), then the ids

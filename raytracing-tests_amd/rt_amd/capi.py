@@ -75,7 +75,7 @@ class RtOptions(C.Structure):
     _fields_ = [("size", C.c_uint32)] + [(n, C.c_int) for n in (
         "inw_wide_walk", "inw_order", "inw_beams", "inw_ri_grid", "inw_lds_nodes", "inw_fused_cull",
         "inw_claim_order", "inw_ring_pm", "inw_ring_sm", "inw_stackless", "inw_device_build", "inw_claim_xcd",
-        "inw_qnodes", "inw_time_bins", "inw_walk_bins", "inw_beam_bins", "inw_sphere_records",
+        "inw_qnodes", "inw_time_bins", "inw_walk_bins", "inw_beam_bins", "inw_sphere_records", "inw_compact_nodes",
         "iow_spec", "iow_linear", "iow_narrow", "iow_lds_bvh", "iow_leaf_batch", "iow_coop_max", "iow_chunks_lpt",
         "rounds_seq", "rounds_spec", "park_min",
         "spec_iters", "spec_probe", "spec_heavy", "spec_rounds", "spec_tail_rounds", "spec_tail_budget", "spec_scan",

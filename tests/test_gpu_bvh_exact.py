@@ -185,6 +185,9 @@ def _same_frames(over, w, h, spp, scene):
     ({"inw_sphere_records": 0}, INW1, 192, 108, 24),
     ({"inw_sphere_records": 0, "inw_order": 2}, INW1, 200, 100, 37),
     ({"inw_sphere_records": 0, "inw_order": -1, "inw_beams": 2}, INW1, 97, 43, 7),
+    # the buffer-load walk's 10-float4 nodes against the 7-float4 copy (default)
+    ({"inw_compact_nodes": 0}, INW1, 192, 108, 24),
+    ({"inw_compact_nodes": 0, "inw_lds_nodes": 0, "inw_order": 2}, INW4, 128, 128, 16),
     ({"inw_beams": 0, "inw_order": 1}, INW4, 128, 128, 16),
     ({"inw_fused_cull": 0, "inw_order": 1}, INW4, 128, 128, 16),
     ({"inw_ri_grid": 0, "inw_order": 1}, INW4, 128, 128, 16),
