@@ -484,6 +484,18 @@ int rt_debug_wide_info(rt_dev_scene *s, uint32_t info[8], uint32_t *rank_out);
  * `levels` SAH / collapse levels (0 = its own cap, 256); a deeper tree is built on the host instead
  * (rt_debug_wide_info info[7] = 2), which lets a test reach that fallback with an ordinary scene. */
 int rt_debug_build_level_cap(int levels);
+/* Test hooks for the host build of the time-bin culling trees and the sphere records (no device;
+ * DESIGN.md §5.2).  rt_debug_time_bins builds the wide walk's trees from the reference's LBVH nodes
+ * and GeometryBuff records (28 floats each) with `bins` time bins and copies the 4-wide nodes (40
+ * floats each, links as int bits) into wnodes_out when wnodes_cap holds them; info = {nodes of the
+ * swept tree, bins built (1: none), nodes per bin tree, all nodes}.  rt_debug_bin_boxes writes the
+ * culling boxes (lo xyz, hi xyz per object) of bin b of `bins`.  rt_debug_sphere_records writes the
+ * 2-float4 sphere records (8 floats per object) and returns 1, or 0 when some object does not
+ * qualify. */
+int rt_debug_time_bins(const float *nodes, const float *geom, uint32_t n, uint32_t bins, float *wnodes_out,
+                       uint32_t wnodes_cap, uint32_t info[4]);
+int rt_debug_bin_boxes(const float *geom, uint32_t n, uint32_t bins, uint32_t b, float *boxes_out);
+int rt_debug_sphere_records(const float *geom, uint32_t n, int layout, float *out);
 
 #ifdef __cplusplus
 }

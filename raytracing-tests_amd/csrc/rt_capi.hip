@@ -1979,6 +1979,48 @@ int rt_inw_host_build(const float *nodes, uint32_t n, uint32_t info[8], double *
     return RT_OK;
 }
 
+int rt_debug_time_bins(const float *nodes, const float *geom, uint32_t n, uint32_t bins, float *wnodes_out,
+                       uint32_t wnodes_cap, uint32_t info[4]) {
+    if (!nodes || !geom || n == 0 || !info) return RT_E_ARG;
+    try {
+        rtamd::InwWide w;
+        if (!rtamd::inw_wide_build(nodes, n, w)) { std::memset(info, 0, 4 * sizeof(uint32_t)); return RT_OK; }
+        rtamd::inw_wide_add_bins(geom, n, bins, w);
+        const uint32_t total = uint32_t(w.wnodes.size() / 40);
+        const uint32_t v[4] = {w.n_tree0, w.bins, w.bin_stride, total};
+        std::memcpy(info, v, sizeof(v));
+        if (wnodes_out && wnodes_cap >= total) std::memcpy(wnodes_out, w.wnodes.data(), w.wnodes.size() * sizeof(float));
+    } catch (...) {
+        return RT_E_ARG;
+    }
+    return RT_OK;
+}
+
+int rt_debug_bin_boxes(const float *geom, uint32_t n, uint32_t bins, uint32_t b, float *boxes_out) {
+    if (!geom || !boxes_out || n == 0 || bins == 0 || b >= bins) return RT_E_ARG;
+    try {
+        std::vector<float> boxes;
+        float wb = 0.0f;
+        if (!rtamd::inw_bin_boxes(geom, n, bins, b, boxes, wb)) return RT_E_ARG;
+        std::memcpy(boxes_out, boxes.data(), boxes.size() * sizeof(float));
+    } catch (...) {
+        return RT_E_ARG;
+    }
+    return RT_OK;
+}
+
+int rt_debug_sphere_records(const float *geom, uint32_t n, int layout, float *out) {
+    if (!geom || !out || n == 0 || (layout != 1 && layout != 4)) return RT_E_ARG;
+    try {
+        std::vector<float> r;
+        if (!inw_sphere_records(geom, n, layout, r)) return 0;
+        std::memcpy(out, r.data(), r.size() * sizeof(float));
+    } catch (...) {
+        return RT_E_ARG;
+    }
+    return 1;
+}
+
 int rt_iow_host_build(const float *types, const float *records, uint32_t n, uint32_t info[4], double *ms) {
     if (!types || !records || n == 0) return RT_E_ARG;
     try {

@@ -829,57 +829,63 @@ bool inw_wide_build(const float *nodes, uint32_t n, InwWide &out) {
 // that hits the object at a time in the bin hits it inside that box, so culling with it is as
 // conservative as with the swept box (the tree only decides which leaves get the
 // exact test).
+bool inw_bin_boxes(const float *geom, uint32_t n, uint32_t bins, uint32_t b, std::vector<float> &boxes, float &wbound) {
+    boxes.assign(size_t(n) * 6, 0.0f);
+    const double r0 = double(b) / bins, r1 = double(b + 1) / bins;
+    for (uint32_t g = 0; g < n; g++) {
+        const float *f = geom + size_t(g) * 28;
+        double lo[3], hi[3];
+        float big = 0.0f;
+        for (int a = 0; a < 3; a++) {
+            double row = 0.0, col = 0.0;  // the half extent along axis a under either orientation of M
+            for (int c = 0; c < 3; c++) {
+                const double x = double(f[3 + 3 * a + c]) * f[12 + c], y = double(f[3 + 3 * c + a]) * f[12 + c];
+                row += x * x;
+                col += y * y;
+            }
+            const double e = std::sqrt(std::fmax(row, col));
+            if (!std::isfinite(e)) return false;
+            const double c0 = double(f[a]) - double(f[15 + a]) * (1.0 - r0);
+            const double c1 = double(f[a]) - double(f[15 + a]) * (1.0 - r1);
+            lo[a] = std::fmin(c0, c1) - e;
+            hi[a] = std::fmax(c0, c1) + e;
+            big = std::fmax(big, float(std::fmax(std::fabs(lo[a]), std::fabs(hi[a]))));
+        }
+        for (int a = 0; a < 3; a++) {
+            const double e = (hi[a] - lo[a]) * 1e-3 + 1e-3 + double(big) * 1e-5;  // as the swept boxes
+            float l = float(lo[a] - e), h = float(hi[a] + e);  // rounded outward to float
+            if (double(l) > lo[a] - e) l = std::nextafter(l, -INFINITY);
+            if (double(h) < hi[a] + e) h = std::nextafter(h, INFINITY);
+            boxes[size_t(g) * 6 + a] = l;
+            boxes[size_t(g) * 6 + 3 + a] = h;
+            wbound = std::fmax(wbound, std::fmax(std::fabs(l), std::fabs(h)));
+        }
+    }
+    return true;
+}
+
+// Time-bin trees (see inw_bin_boxes for the boxes).  Object g's centre at time ratio r is
+// p - delta (1 - r) (the kernels' object offset (o - p) + delta (1 - r), 01_BVH...glsl), so over
+// [r0, r1] it sweeps the segment between its centres at r0 and r1; its box there is that segment's
+// box widened by the object's own half extent, sqrt(sum_c (M_ic s_c)^2) under either orientation
+// convention of the rotation M (the ellipsoid's exact extent, and above a cuboid's), inflated as
+// the swept culling boxes are.  A ray that hits the object at a time in the bin hits it inside that
+// box, so culling with it is as conservative as with the swept box (the tree only
+// decides which leaves get the exact test).
 bool inw_wide_add_bins(const float *geom, uint32_t n, uint32_t bins, InwWide &w) {
     if (bins < 2 || bins > 16 || n < 2 || w.wnodes.empty() || w.bins != 1) return false;
     bool moving = false;
     for (uint32_t g = 0; g < n && !moving; g++)
         for (int a = 0; a < 3; a++) moving = moving || geom[size_t(g) * 28 + 15 + a] != 0.0f;
     if (!moving) return false;
-    std::vector<float> ext(size_t(n) * 3);
-    for (uint32_t g = 0; g < n; g++) {
-        const float *f = geom + size_t(g) * 28;
-        for (int i = 0; i < 3; i++) {
-            double row = 0.0, col = 0.0;
-            for (int c = 0; c < 3; c++) {
-                const double a = double(f[3 + 3 * i + c]) * f[12 + c], b = double(f[3 + 3 * c + i]) * f[12 + c];
-                row += a * a;
-                col += b * b;
-            }
-            const double e = std::sqrt(std::fmax(row, col));
-            if (!std::isfinite(e)) return false;
-            ext[size_t(g) * 3 + i] = float(e);
-        }
-    }
     std::vector<std::vector<float>> trees(bins);
     size_t stride = 0;
-    std::vector<float> boxes(size_t(n) * 6);
+    std::vector<float> boxes;
+    float wbound = w.wbound;
     for (uint32_t b = 0; b < bins; b++) {
-        const double r0 = double(b) / bins, r1 = double(b + 1) / bins;
-        for (uint32_t g = 0; g < n; g++) {
-            const float *f = geom + size_t(g) * 28;
-            float big = 0.0f;
-            double lo[3], hi[3];
-            for (int a = 0; a < 3; a++) {
-                const double c0 = double(f[a]) - double(f[15 + a]) * (1.0 - r0);
-                const double c1 = double(f[a]) - double(f[15 + a]) * (1.0 - r1);
-                lo[a] = std::fmin(c0, c1) - ext[size_t(g) * 3 + a];
-                hi[a] = std::fmax(c0, c1) + ext[size_t(g) * 3 + a];
-                big = std::fmax(big, float(std::fmax(std::fabs(lo[a]), std::fabs(hi[a]))));
-            }
-            for (int a = 0; a < 3; a++) {
-                const double e = (hi[a] - lo[a]) * 1e-3 + 1e-3 + double(big) * 1e-5;
-                // rounded outward to float
-                float l = float(lo[a] - e), h = float(hi[a] + e);
-                if (double(l) > lo[a] - e) l = std::nextafter(l, -INFINITY);
-                if (double(h) < hi[a] + e) h = std::nextafter(h, INFINITY);
-                boxes[size_t(g) * 6 + a] = l;
-                boxes[size_t(g) * 6 + 3 + a] = h;
-                w.wbound = std::fmax(w.wbound, std::fmax(std::fabs(l), std::fabs(h)));
-            }
-        }
+        if (!inw_bin_boxes(geom, n, bins, b, boxes, wbound)) return false;
         int d4 = 0;
-        const size_t nw = wide_tree(boxes.data(), n, 0, trees[b], &d4);
-        stride = std::max(stride, nw);
+        stride = std::max(stride, wide_tree(boxes.data(), n, 0, trees[b], &d4));
     }
     // concatenate: tree b's first node at n_tree0 + b * stride (links rebased), padding nodes empty
     const size_t n0 = w.wnodes.size() / 40;
@@ -904,6 +910,7 @@ bool inw_wide_add_bins(const float *geom, uint32_t n, uint32_t bins, InwWide &w)
     }
     w.bins = bins;
     w.bin_stride = uint32_t(stride);
+    w.wbound = wbound;
     return true;
 }
 

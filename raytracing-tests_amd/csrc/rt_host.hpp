@@ -141,6 +141,9 @@ bool inw_wide_build(const float *nodes, uint32_t n, InwWide &out);
 // floats: position, rotation, scale, position - last_position at 15..17).  false (nothing
 // appended): bins < 2, no object moves, or the records are malformed.
 bool inw_wide_add_bins(const float *geom, uint32_t n, uint32_t bins, InwWide &w);
+// The culling boxes of bin b of `bins` (6 floats per object: lo xyz, hi xyz), rounded outward; the
+// largest |coordinate| goes into wbound (max).  false: a record's extent is not finite.
+bool inw_bin_boxes(const float *geom, uint32_t n, uint32_t bins, uint32_t b, std::vector<float> &boxes, float &wbound);
 // The reference walk's stack high-water mark over both child orders (high; its pushes can only
 // drop while size + high > 40) and whether the node buffer has the layout the stackless LBVH walks
 // rely on (stackless: every internal node's children at L (odd), L + 1 with rightData = the node,

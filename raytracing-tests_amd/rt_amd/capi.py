@@ -187,6 +187,9 @@ SIGNATURES = {
     "rt_tile_deal": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _IP, C.c_int]),
     "rt_group_create": (C.c_void_p, [_IP, C.c_int]),
     "rt_debug_build_level_cap": (C.c_int, [C.c_int]),
+    "rt_debug_time_bins": (C.c_int, [_FP, _FP, C.c_uint32, C.c_uint32, _FP, C.c_uint32, _U32P]),
+    "rt_debug_bin_boxes": (C.c_int, [_FP, C.c_uint32, C.c_uint32, C.c_uint32, _FP]),
+    "rt_debug_sphere_records": (C.c_int, [_FP, C.c_uint32, C.c_int, _FP]),
     "rt_group_free": (None, [C.c_void_p]),
     "rt_render_multi_async": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(RtCamera), C.POINTER(RtParams), C.c_int,
                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
