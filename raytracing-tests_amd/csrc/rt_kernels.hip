@@ -2144,6 +2144,15 @@ __device__ __forceinline__ void keep_before_branch(f3 to, f3 td) {
 #endif
 }
 
+// Scalar loads of wave-uniform records (constant address space: s_load through the scalar cache,
+// no vector-memory / TA work)
+typedef float sv4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const sv4f csv4f;
+__device__ __forceinline__ float4 sload4(const float4 *p, int i) {
+    const sv4f v = ((const csv4f *)(const void *)p)[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // ---------------------------------------------------------------- INW wide walk
 // The reference's closest hit (01_BVH...glsl:431-473) is the nearest hit among the objects whose
 // LBVH leaf box its depth-first walk reaches, ties to the one it reaches first.  With finite ray
@@ -2286,6 +2295,20 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
                 } else {
                     float4 nx, ny, nz, fx, fy, fz;
 #ifndef RT_INW_NO_BUFLOAD
+#ifdef RT_INW_NODE_SLOAD
+                    // every stepping lane at one node with one octant (30% of C3's node steps are at one
+                    // node): the node's planes by scalar loads, off the TA path
+                    const int c0 = __builtin_amdgcn_readfirstlane(cur);
+                    const uint32_t oc = ox + 8u * oy + 64u * oz, oc0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)oc);
+                    if (S.cnodes && (!LN || (uint32_t)(c0 - 1) >= S.n_lnodes) && __ballot(cur != c0 || oc != oc0) == 0ull) {
+                        const float4 *nd = S.cnodes + 7 * (c0 - 1);
+                        const int sx = (int)(oc0 & 7u), sy = (int)((oc0 >> 3) & 7u), sz = (int)(oc0 >> 6);  // 0|3, 1|4, 2|5
+                        nx = sload4(nd, sx); fx = sload4(nd, 3 - sx);
+                        ny = sload4(nd, sy); fy = sload4(nd, 5 - sy);
+                        nz = sload4(nd, sz); fz = sload4(nd, 7 - sz);
+                        lk = sload4(nd, 6);
+                    } else
+#endif
                     inw_wnode_nf_buf<LN>(S, wrs, cur, ox * 16u, oy * 16u, oz * 16u, nx, ny, nz, fx, fy, fz, lk);
 #else
                     inw_wnode_nf<LN>(S, cur, ox, oy, oz, nx, ny, nz, fx, fy, fz, lk);
@@ -2359,15 +2382,8 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
     return (float)bg;
 }
 
-// Scalar loads of wave-uniform records (constant address space: s_load through the scalar cache,
-// no vector-memory / TA work): the beam lists' candidates are the same object for every active lane
-// of one pixel (they step through the list together)
-typedef float sv4f __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(4))) const sv4f csv4f;
-__device__ __forceinline__ float4 sload4(const float4 *p, int i) {
-    const sv4f v = ((const csv4f *)(const void *)p)[i];
-    return make_float4(v.x, v.y, v.z, v.w);
-}
+// load_xf by scalar loads (sload4): the beam lists' candidates are the same object for every active
+// lane of one pixel (they step through the list together)
 __device__ __forceinline__ Xf load_xf_s(const InwScene &S, int g) {  // load_xf of a wave-uniform g
     const float4 a = sload4(S.hot, 7 * g), b = sload4(S.hot, 7 * g + 1), c = sload4(S.hot, 7 * g + 2),
                  d = sload4(S.hot, 7 * g + 3), e = sload4(S.hot, 7 * g + 4), f = sload4(S.hot, 7 * g + 5),

@@ -22,7 +22,7 @@ RT=$(/opt/rocm/lib/llvm/bin/clang -print-file-name=libclang_rt.asan-x86_64.so)
     OMP_NUM_THREADS=4 \
     timeout -k 10 1500 python -m pytest -q -p no:cacheprovider -m "not gpu" \
       tests/test_host_logic.py tests/test_oracle_golden.py tests/test_oracle_kat.py tests/test_progressive.py \
-      tests/test_textures.py tests/test_stages_oracle.py tests/test_abi.py tests/test_multiproc.py 2>&1
+      tests/test_textures.py tests/test_stages_oracle.py tests/test_abi.py tests/test_multiproc.py tests/test_time_bins.py 2>&1
   echo "# exit status $?"
 } > "$LOG" 2>&1
 tail -3 "$LOG"
