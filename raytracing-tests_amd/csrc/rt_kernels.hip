@@ -2233,11 +2233,14 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
     }
     bool walking = ok, ovf = false;
     float lim = bt * 1.0001f + 1e-3f;
+    // the leaf-entry guard: the best hit's leaf-box entry, and the smallest t of the
+    // other hits; the reference's walk accepts the best hit for certain when t2 > bte
+    float bte = 0.0f, t2 = tlim0;
     if constexpr (PK) {
         if (wp->resume) {  // a parked walk: its state from the slot (ok held when it parked)
             const float4 a = wp->slot[0], b = wp->slot[1];
             cur = __float_as_int(a.x); sp = __float_as_int(a.y); bg = __float_as_int(a.z); br = __float_as_uint(a.w);
-            bt = b.x; lim = b.y;
+            bt = b.x; lim = b.y; bte = b.z; t2 = b.w;
         }
         wp->parked = false;
     }
@@ -2264,9 +2267,16 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
             else if (x.type == 2) t = t_cuboid(to, td, x.scale);
         }
         if (t > 0.0f && t < tlim0) {
-            if (t < te) ovf = true;  // the guard above: the reference walk decides this ray
             const uint32_t r = rank[g];
-            if (t < bt || (t == bt && r < br)) { bt = t; bg = g; br = r; lim = bt * 1.0001f + 1e-3f; }
+#ifdef RT_INW_GUARD_ANY
+            if (t < te) ovf = true;  // round-5 guard: any hit below its leaf-box entry
+#endif
+            if (t < bt || (t == bt && r < br)) {
+                if (bg >= 0) t2 = fminf(t2, bt);
+                bt = t; bg = g; br = r; bte = te; lim = bt * 1.0001f + 1e-3f;
+            } else {
+                t2 = fminf(t2, t);
+            }
         }
     };
     for (;;) {
@@ -2356,7 +2366,7 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
                 if (ovf) walking = false;
                 if (walking) {
                     wp->slot[0] = make_float4(__int_as_float(cur), __int_as_float(sp), __int_as_float(bg), __uint_as_float(br));
-                    wp->slot[1] = make_float4(bt, lim, 0.0f, 0.0f);
+                    wp->slot[1] = make_float4(bt, lim, bte, t2);
                     wp->parked = true;
                 }
                 break;
@@ -2364,6 +2374,9 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
         }
     }
     if (PK && wp->parked) return init_geom;
+    // the best hit passes the reference's leaf-box test for certain unless another hit's t could
+    // have lowered its running limit to the box entry first (rare: a face on its box, C5)
+    if (bg >= 0 && !(t2 > bte)) ovf = true;
     if (ovf) ok = false;
     if (!ok) return init_geom;
     if (bg < 0) return init_geom;
@@ -2429,6 +2442,7 @@ __device__ float inw_closest_beam(const InwScene &S, const KS &K, f3 o, f3 d, fl
     const float kap = S.beam_kappa;
     float lim = bt * kap + 0.01f;
     bool ovf = false;
+    float bte = 0.0f, t2 = tlim0;  // the leaf-entry guard's state (inw_traverse_wide)
     uint32_t k = 0;
     // packed entries hold t rounded down (and 0 for a negative entry): the list stays sorted, and a
     // ray stops at a stored t above lim no earlier than at the exact one
@@ -2499,14 +2513,22 @@ __device__ float inw_closest_beam(const InwScene &S, const KS &K, f3 o, f3 d, fl
             }
             if (inb) {
                 if (t > 0.0f && t < tlim0) {
-                    if (t < te) ovf = true;  // the leaf-entry guard (inw_traverse_wide)
                     const uint32_t r = rank[g];
-                    if (t < bt || (t == bt && r < br)) { bt = t; bg = g; br = r; lim = bt * kap * 1.00001f + 0.01f; }
+#ifdef RT_INW_GUARD_ANY
+                    if (t < te) ovf = true;
+#endif
+                    if (t < bt || (t == bt && r < br)) {  // the leaf-entry guard as in inw_traverse_wide
+                        if (bg >= 0) t2 = fminf(t2, bt);
+                        bt = t; bg = g; br = r; bte = te; lim = bt * kap * 1.00001f + 0.01f;
+                    } else {
+                        t2 = fminf(t2, t);
+                    }
                 }
             }
             k++;
         }
     }
+    if (bg >= 0 && !(t2 > bte)) ovf = true;
     // candidates not stored (entry >= cut) could still be reached below lim
     if (ok && (ovf || !(lim < S.beam_cut[bo + unit]))) ok = false;
     if (!ok) return init_geom;
