@@ -480,6 +480,9 @@ void inw_records(const float *geom, uint32_t n, int layout, std::vector<float> &
         float *h = hot.data() + size_t(j) * rtk::kInwHot;
         float *c = cold.data() + size_t(j) * rtk::kInwCold;
         for (int k = 0; k < 20; k++) h[k] = f[k];  // pos R scale delta type extra
+        bool ident = true;  // the rotation exactly the identity (entries 1 and +-0): type + 0.5 (rtk::Xf::ident)
+        for (int k = 0; k < 9; k++) ident = ident && f[3 + k] == ((k % 4) == 0 ? 1.0f : 0.0f);
+        if (ident && (f[18] == 1.0f || f[18] == 2.0f)) h[18] = f[18] + 0.5f;
         for (int k = 0; k < 3; k++) {
             h[20 + k] = 1.0f / f[12 + k];                  // a / scale  -> a * RN(1/scale)
             h[23 + k] = 1.0f / (f[12 + k] * f[12 + k]);    // a / (s*s)  -> a * RN(1/RN(s*s))

@@ -1800,7 +1800,10 @@ struct GStack {
     }
 };
 
-struct Xf { f3 pos, scale, delta, is, is2; m3 R; int type; float extra, ri_acc; };
+// ident: the rotation is exactly the identity (the host marks the record's type field with + 0.5;
+// int(type + 0.1) still reads the type): the wide walk's object test then skips both 3 x 3 products
+// and, for a cuboid, reuses the ray's reciprocals (DESIGN.md §5.2 "Unrotated objects")
+struct Xf { f3 pos, scale, delta, is, is2; m3 R; int type; bool ident; float extra, ri_acc; };
 
 __device__ __forceinline__ Xf load_xf(const InwScene &S, int g) {
     const float4 *h = S.hot + (size_t)g * 7;
@@ -1811,6 +1814,7 @@ __device__ __forceinline__ Xf load_xf(const InwScene &S, int g) {
     x.scale = mk(d.x, d.y, d.z);
     x.delta = mk(d.w, e.x, e.y);
     x.type = (int)(e.z + 0.1f);
+    x.ident = e.z - (float)x.type > 0.25f;
     x.extra = e.w;
     x.is = mk(f.x, f.y, f.z);
     x.is2 = mk(f.w, q.x, q.y);
@@ -2259,12 +2263,23 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
         } else {
             const Xf x = load_xf(S, g);  // loaded with the box, before its test: one memory latency
             const bool inb = test_aabb_te(n0, n1, o, id, tlim0, te);
-            f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
-            f3 to = tmul(x.R, ov), td = tmul(x.R, d);
-            keep_before_branch(to, td);
-            if (!inb) return;
-            if (x.type == 1) t = t_ellipsoid(to, td, x.is);
-            else if (x.type == 2) t = t_cuboid(to, td, x.scale);
+            const f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+#ifndef RT_INW_NO_IDENT
+            if (x.ident) {  // R = I: tmul(R, v) is v (up to zero signs, which t cannot see; d has no
+                            // zero component here), and rcp(d) is the ray's own id
+                keep_before_branch(ov, d);
+                if (!inb) return;
+                if (x.type == 1) t = t_ellipsoid(ov, d, x.is);
+                else if (x.type == 2) t = t_cuboid_rcp(ov, id, x.scale);
+            } else
+#endif
+            {
+                f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+                keep_before_branch(to, td);
+                if (!inb) return;
+                if (x.type == 1) t = t_ellipsoid(to, td, x.is);
+                else if (x.type == 2) t = t_cuboid(to, td, x.scale);
+            }
         }
         if (t > 0.0f && t < tlim0) {
             const uint32_t r = rank[g];
@@ -2407,6 +2422,7 @@ __device__ __forceinline__ Xf load_xf_s(const InwScene &S, int g) {  // load_xf 
     x.scale = mk(d.x, d.y, d.z);
     x.delta = mk(d.w, e.x, e.y);
     x.type = (int)(e.z + 0.1f);
+    x.ident = e.z - (float)x.type > 0.25f;
     x.extra = e.w;
     x.is = mk(f.x, f.y, f.z);
     x.is2 = mk(f.w, q.x, q.y);

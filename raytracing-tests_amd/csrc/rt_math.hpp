@@ -112,6 +112,23 @@ __device__ __forceinline__ float t_ellipsoid(f3 o, f3 d, f3 is) {
     }
     return t > 0.0f ? t : -1.0f;
 }
+// t_cuboid with the reciprocals of d given (id = 1/d, correctly rounded as rcp computes them)
+__device__ __forceinline__ float t_cuboid_rcp(f3 o, f3 id3, f3 s) {
+    f3 bmin = (-s) * 0.5f, bmax = s * 0.5f;
+    float id = id3.x;
+    float t1 = (bmin.x - o.x) * id, t2 = (bmax.x - o.x) * id;
+    float tmin = fminf(t1, t2), tmax = fmaxf(t1, t2);
+    id = id3.y;
+    t1 = (bmin.y - o.y) * id; t2 = (bmax.y - o.y) * id;
+    tmin = fmaxf(tmin, fminf(fminf(t1, t2), tmax));
+    tmax = fminf(tmax, fmaxf(fmaxf(t1, t2), tmin));
+    id = id3.z;
+    t1 = (bmin.z - o.z) * id; t2 = (bmax.z - o.z) * id;
+    tmin = fmaxf(tmin, fminf(fminf(t1, t2), tmax));
+    tmax = fminf(tmax, fmaxf(fmaxf(t1, t2), tmin));
+    float t = tmax > tmin ? (tmin > 0.0f ? tmin : tmax) : -1.0f;
+    return t > 0.0f ? t : -1.0f;
+}
 __device__ __forceinline__ float t_cuboid(f3 o, f3 d, f3 s) {
     f3 bmin = (-s) * 0.5f, bmax = s * 0.5f;
     float id = rcp(d.x);
