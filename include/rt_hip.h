@@ -138,7 +138,7 @@ typedef struct rt_options {
     int inw_walk_bins;      /* 1 (default): the wide closest-hit walks use the time-bin trees */
     int inw_beam_bins;      /* 1 (default): a pixel's beam lists per time bin, from the time-bin trees */
     int inw_sphere_records; /* 1 (default): in scenes of equal-scale ellipsoids with the identity rotation, the
-                               wide walk and beam lists test objects from 2-float4 sphere records */
+                               wide walk, beam lists and RI grid read 3-float4 sphere records */
     int inw_compact_nodes;  /* 1 (default): the wide walk reads its nodes from global memory as 7 float4
                                (112 B) instead of 10 (the repeated low planes dropped) */
     /* IOW-03 (In-One-Weekend 03) */
@@ -490,7 +490,7 @@ int rt_debug_build_level_cap(int levels);
  * floats each, links as int bits) into wnodes_out when wnodes_cap holds them; info = {nodes of the
  * swept tree, bins built (1: none), nodes per bin tree, all nodes}.  rt_debug_bin_boxes writes the
  * culling boxes (lo xyz, hi xyz per object) of bin b of `bins`.  rt_debug_sphere_records writes the
- * 2-float4 sphere records (8 floats per object) and returns 1, or 0 when some object does not
+ * 3-float4 sphere records (12 floats per object) and returns 1, or 0 when some object does not
  * qualify. */
 int rt_debug_time_bins(const float *nodes, const float *geom, uint32_t n, uint32_t bins, float *wnodes_out,
                        uint32_t wnodes_cap, uint32_t info[4]);

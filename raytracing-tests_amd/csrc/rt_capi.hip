@@ -455,18 +455,20 @@ int make_inw_wide(rt_dev_scene *s, const float *nodes, uint32_t n, double *ms = 
 
 // Sphere records (rtk::InwScene::sph) when every object is an ellipsoid with equal scales and the
 // identity rotation (entries exactly 1 and +-0): (position, RN(1/scale)), (position - last_position,
-// RI).  false: some object is not.
+// RI), (RN(1/RN(scale^2)) per axis, extra).  false: some object is not.
 bool inw_sphere_records(const float *geom, uint32_t n, int layout, std::vector<float> &out) {
-    out.assign(size_t(n) * 8, 0.0f);
+    out.assign(size_t(n) * 12, 0.0f);
     for (uint32_t j = 0; j < n; j++) {
         const float *f = geom + size_t(j) * 28;
         if (int(f[18] + 0.1f) != 1 || !(f[12] == f[13] && f[13] == f[14]) || !std::isfinite(f[12])) return false;
         for (int k = 0; k < 9; k++)
             if (f[3 + k] != ((k % 4) == 0 ? 1.0f : 0.0f)) return false;
-        float *o = out.data() + size_t(j) * 8;
+        float *o = out.data() + size_t(j) * 12;
         o[0] = f[0]; o[1] = f[1]; o[2] = f[2]; o[3] = 1.0f / f[12];  // the hot record's is (RN(1/scale))
         o[4] = f[15]; o[5] = f[16]; o[6] = f[17];
         o[7] = layout == 4 ? f[19] : f[20];  // the RI the surrounding-RI walk adds (the hot record's)
+        for (int k = 0; k < 3; k++) o[8 + k] = 1.0f / (f[12 + k] * f[12 + k]);  // the hot record's is2
+        o[11] = f[19];  // its extra data
     }
     return n > 0;
 }

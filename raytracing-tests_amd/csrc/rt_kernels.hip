@@ -2199,6 +2199,36 @@ struct WalkPark {
     bool parked;    // out: parked again
 };
 // QN: the quantised nodes (S.qnodes, cull4q; requires FU), LN then meaning the staged ones in g_inw_qlds.
+// The hit object's normal and extra data (01_BVH...glsl:FillHitData's inputs) at t = bt.  SP with
+// sphere records: from their third float4 (RN(1/RN(s*s)) per axis, extra) -- R = I, so the
+// object-space ray is the world one (h's components are nonzero products: the same floats) and
+// mul(I, nl) is evaluated with the literal identity, the same operations as with R loaded
+template <bool SP>
+__device__ __forceinline__ void inw_hit_normal(const InwScene &S, int bg, f3 o, f3 d, float ratio, float bt, f3 &normal,
+                                               float &extra) {
+#ifndef RT_INW_SPH_NO_NORMAL
+    if (SP && S.sph) {
+        const float4 p = S.sph[3 * bg], q = S.sph[3 * bg + 1], w = S.sph[3 * bg + 2];
+        const f3 ov = (o - mk(p.x, p.y, p.z)) + mk(q.x, q.y, q.z) * (1.0f - ratio);
+        const f3 h = ov + d * bt;
+        const f3 nl = normalize(f3{h.x * w.x, h.y * w.y, h.z * w.z});
+        const m3 I = m3{f3{1.0f, 0.0f, 0.0f}, f3{0.0f, 1.0f, 0.0f}, f3{0.0f, 0.0f, 1.0f}};
+        normal = mul(I, nl);
+        extra = w.w;
+        return;
+    }
+#endif
+    const Xf x = load_xf(S, bg);
+    f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+    f3 to = tmul(x.R, ov), td = tmul(x.R, d);
+    f3 h = to + td * bt, nl;
+    if (x.type == 1) nl = normalize(f3{h.x * x.is2.x, h.y * x.is2.y, h.z * x.is2.z});
+    else if (x.type == 2) nl = cuboid_normal(h, x.scale);
+    else nl = f3{0, 0, 0};
+    normal = mul(x.R, nl);
+    extra = x.extra;
+}
+
 // SP: the sphere-record object test is compiled in (INW-01 kernels; INW-04's keep their registers)
 template <bool WANT_NORMAL, bool LN = false, bool FU = false, bool PK = false, bool QN = false, class KS = FStack,
           bool SP = true>
@@ -2254,7 +2284,7 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
         const float4 n0 = S.leafbox[2 * g], n1 = S.leafbox[2 * g + 1];
         float te, t = -1.0f;
         if (SP && S.sph) {  // a sphere scene: 2 float4 instead of 7, no rotation (R = I: tmul(R, v) = v)
-            const float4 p = S.sph[2 * g], q = S.sph[2 * g + 1];
+            const float4 p = S.sph[3 * g], q = S.sph[3 * g + 1];
             const bool inb = test_aabb_te(n0, n1, o, id, tlim0, te);
             const f3 to = (o - mk(p.x, p.y, p.z)) + mk(q.x, q.y, q.z) * (1.0f - ratio);
             keep_before_branch(to, d);
@@ -2396,17 +2426,7 @@ __device__ float inw_traverse_wide(const InwScene &S, KS &K, f3 o, f3 d, float r
     if (!ok) return init_geom;
     if (bg < 0) return init_geom;
     tlim = bt;
-    if (WANT_NORMAL) {
-        const Xf x = load_xf(S, bg);
-        f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
-        f3 to = tmul(x.R, ov), td = tmul(x.R, d);
-        f3 h = to + td * bt, nl;
-        if (x.type == 1) nl = normalize(f3{h.x * x.is2.x, h.y * x.is2.y, h.z * x.is2.z});
-        else if (x.type == 2) nl = cuboid_normal(h, x.scale);
-        else nl = f3{0, 0, 0};
-        normal = mul(x.R, nl);
-        extra = x.extra;
-    }
+    if (WANT_NORMAL) inw_hit_normal<SP>(S, bg, o, d, ratio, bt, normal, extra);
     return (float)bg;
 }
 
@@ -2500,10 +2520,10 @@ __device__ float inw_closest_beam(const InwScene &S, const KS &K, f3 o, f3 d, fl
                 float4 p, q;
                 if (uni_g) {
                     n0 = sload4(S.leafbox, 2 * g0); n1 = sload4(S.leafbox, 2 * g0 + 1);
-                    p = sload4(S.sph, 2 * g0); q = sload4(S.sph, 2 * g0 + 1);
+                    p = sload4(S.sph, 3 * g0); q = sload4(S.sph, 3 * g0 + 1);
                 } else {
                     n0 = S.leafbox[2 * g]; n1 = S.leafbox[2 * g + 1];
-                    p = S.sph[2 * g]; q = S.sph[2 * g + 1];
+                    p = S.sph[3 * g]; q = S.sph[3 * g + 1];
                 }
                 inb = test_aabb_te(n0, n1, o, id, tlim0, te);
                 const f3 to = (o - mk(p.x, p.y, p.z)) + mk(q.x, q.y, q.z) * (1.0f - ratio);
@@ -2550,17 +2570,7 @@ __device__ float inw_closest_beam(const InwScene &S, const KS &K, f3 o, f3 d, fl
     if (!ok) return init_geom;
     if (bg < 0) return init_geom;
     tlim = bt;
-    if (WANT_NORMAL) {
-        const Xf x = load_xf(S, bg);
-        f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
-        f3 to = tmul(x.R, ov), td = tmul(x.R, d);
-        f3 h = to + td * bt, nl;
-        if (x.type == 1) nl = normalize(f3{h.x * x.is2.x, h.y * x.is2.y, h.z * x.is2.z});
-        else if (x.type == 2) nl = cuboid_normal(h, x.scale);
-        else nl = f3{0, 0, 0};
-        normal = mul(x.R, nl);
-        extra = x.extra;
-    }
+    if (WANT_NORMAL) inw_hit_normal<true>(S, bg, o, d, ratio, bt, normal, extra);
     return (float)bg;
 }
 
@@ -2663,7 +2673,7 @@ __device__ float inw_ri_grid(const InwScene &S, f3 hp, float ratio, Ctr &c, bool
         bool inside;
         float ri;
         if (S.sph) {  // sphere records (RI in q.w): R = I, so v = ov * is, the same floats
-            const float4 p = S.sph[2 * g], q = S.sph[2 * g + 1];
+            const float4 p = S.sph[3 * g], q = S.sph[3 * g + 1];
             if (!(hp.x <= n0.w && hp.y <= n1.x && hp.z <= n1.y && hp.x >= n0.x && hp.y >= n0.y && hp.z >= n0.z)) continue;
             f3 v = (hp - mk(p.x, p.y, p.z)) + mk(q.x, q.y, q.z) * (1.0f - ratio);
             v.x *= p.w; v.y *= p.w; v.z *= p.w;

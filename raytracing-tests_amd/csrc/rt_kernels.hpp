@@ -84,8 +84,8 @@ struct InwScene {
     const uint32_t *rank = nullptr;
     const float4 *leafbox = nullptr;  // per object: its LBVH leaf node (2 float4: the reference's leaf box)
     // Sphere scenes (DESIGN.md §5.2 "Sphere records"; null = off): every object an ellipsoid of equal
-    // scales with the identity rotation; per object 2 float4, (position, RN(1/scale)) and (position -
-    // last_position, its RI).  The wide walk's, the beam lists' and the RI grid's object tests read
+    // scales with the identity rotation; per object 3 float4, (position, RN(1/scale)), (position -
+    // last_position, its RI) and (RN(1/RN(scale^2)) per axis, extra: the hit normal's inputs).  The wide walk's, the beam lists' and the RI grid's object tests read
     // these instead of the 7-float4 record: R = I makes the object-space ray the world one, the same
     // floats (up to the signs of zero terms, which neither t nor the inside test can see); the
     // winner's normal still comes from the full record

@@ -95,11 +95,12 @@ def test_sphere_records():
     lib = R.load()
     sc = R.make_scene(R.PRESET_INW01_RANDOM, 1234, 300, width=8, height=8, spp=1)
     g = np.ascontiguousarray(sc.geom, np.float32)
-    out = np.zeros((sc.n, 8), np.float32)
+    out = np.zeros((sc.n, 12), np.float32)
     assert lib.rt_debug_sphere_records(R.fptr(g), sc.n, 1, R.fptr(out)) == 1
     assert (out[:, 0:3] == g[:, 0:3]).all() and (out[:, 4:7] == g[:, 15:18]).all()
     assert (out[:, 3] == np.float32(1.0) / g[:, 12]).all()  # the hot record's RN(1/scale)
     assert (out[:, 7] == g[:, 20]).all()  # the RI the surrounding-RI walk adds (layout 1)
+    assert (out[:, 8:11] == np.float32(1.0) / (g[:, 12:15] * g[:, 12:15])).all() and (out[:, 11] == g[:, 19]).all()
     # a rotated object, unequal scales or a cuboid: no sphere records
     for col, val in ((4, 0.5), (13, 2.0 * g[0, 12]), (18, 2.0)):
         h = g.copy()
@@ -107,4 +108,4 @@ def test_sphere_records():
         assert lib.rt_debug_sphere_records(R.fptr(h), sc.n, 1, R.fptr(out)) == 0, col
     cb = R.make_scene(R.PRESET_INW04_CORNELL, 7, 0, width=8, height=8, spp=1)
     g4 = np.ascontiguousarray(cb.geom, np.float32)
-    assert lib.rt_debug_sphere_records(R.fptr(g4), cb.n, 4, R.fptr(np.zeros((cb.n, 8), np.float32))) == 0
+    assert lib.rt_debug_sphere_records(R.fptr(g4), cb.n, 4, R.fptr(np.zeros((cb.n, 12), np.float32))) == 0
