@@ -2220,6 +2220,20 @@ __device__ __forceinline__ void inw_hit_normal(const InwScene &S, int bg, f3 o, 
 #endif
     const Xf x = load_xf(S, bg);
     f3 ov = (o - x.pos) + x.delta * (1.0f - ratio);
+#ifndef RT_INW_NO_IDENT
+    if (x.ident) {  // R = I: h = ov + d bt has the same floats (d has no zero component here), and
+                    // mul(I, nl) with the literal identity repeats the loaded R's operations
+        const f3 h = ov + d * bt;
+        f3 nl;
+        if (x.type == 1) nl = normalize(f3{h.x * x.is2.x, h.y * x.is2.y, h.z * x.is2.z});
+        else if (x.type == 2) nl = cuboid_normal(h, x.scale);
+        else nl = f3{0, 0, 0};
+        const m3 I = m3{f3{1.0f, 0.0f, 0.0f}, f3{0.0f, 1.0f, 0.0f}, f3{0.0f, 0.0f, 1.0f}};
+        normal = mul(I, nl);
+        extra = x.extra;
+        return;
+    }
+#endif
     f3 to = tmul(x.R, ov), td = tmul(x.R, d);
     f3 h = to + td * bt, nl;
     if (x.type == 1) nl = normalize(f3{h.x * x.is2.x, h.y * x.is2.y, h.z * x.is2.z});
